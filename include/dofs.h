@@ -1,0 +1,188 @@
+/*
+ * dofs.h — C-ABI drop-in boundary for the dense-optical-flow clustering + 3D-lifting hot path.
+ *
+ * Reference interfaces replaced (DmitriyZhuravlev/DenseOpticalFlowSegmentation3D @ v1):
+ *   dofs_segment / dofs_segment_batch_device
+ *       ← Forest get_segmented_array(const cv::Mat& flow, const cv::Mat& bev,
+ *                                     const cv::Matx33f& persp, const cv::Matx33f& inv,
+ *                                     const std::vector<cv::Matx33f>& inv_upper, int neighbor=8)
+ *         cpp/src/segment.cpp:34-72 (blur :52, build_graph :55, segment_graph :62)
+ *         which in turn covers build_graph       cpp/inc/graph.hpp:22-23, cpp/src/graph.cpp:51-103
+ *                              segment_graph     cpp/inc/graph.hpp:120-122, cpp/src/graph.cpp:503-536
+ *                              Forest::new_merge cpp/src/graph.cpp:272-384
+ *                              Forest::get_best_segments cpp/src/graph.cpp:391-429
+ *         and the overlay's label semantics      cpp/src/draw.cpp:118-147 (score > 0.7, ascending slots)
+ *   dofs_lift / dofs_lift_batch
+ *       ← Solution get_bottom_variants(const cv::Point2f& dir, const std::vector<cv::Point2i>& box,
+ *                                      const cv::Matx33f& mat, const cv::Matx33f& inv,
+ *                                      const cv::Matx33f& inv_upper, int cls)
+ *         cpp/inc/lifting_3d.hpp:13-16, cpp/src/lifting_3d.cpp:350-439
+ *   dofs_intersect ← cv::Point2f get_intersect(a1, a2, b1, b2)   cpp/inc/lifting_3d.hpp:26, lifting_3d.cpp:63-110
+ *   dofs_calib     ← std::pair<Matx33f,Matx33f> get_mat()        cpp/inc/lifting_3d.hpp:17, lifting_3d.cpp:482-514
+ *                    cv::Matx33f get_mat_upper(int cls)          cpp/inc/lifting_3d.hpp:18, lifting_3d.cpp:441-480
+ *
+ * Conventions
+ *   - Plain C types only. Matrices are row-major float[9] (cv::Matx33f layout).
+ *   - The flow field is H×W interleaved (u,v) float32 (cv::Mat CV_32FC2 layout).
+ *   - Unlike the reference (which blurs the caller's Mat in place, segment.cpp:52), caller buffers
+ *     are never mutated; the blurred field is returned on request (dofs_result.blurred).
+ *   - Every entry point returns a dofs_status; no exceptions cross the ABI. An invalid `neighbor`
+ *     falls back to the 4-neighbourhood exactly like segment.cpp:38-43 (not an error).
+ *   - One dofs_ctx per host thread; each context owns one HIP stream unless a stream is passed.
+ *   - The GPU library (libdofs_hip.so) requires a gfx950 device; there is no CPU fallback.
+ */
+#ifndef DOFS_H
+#define DOFS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DOFS_ABI_VERSION 1
+
+typedef enum dofs_status {
+    DOFS_OK = 0,
+    DOFS_ERR_INVALID_ARG = 1,
+    DOFS_ERR_NO_DEVICE = 2,
+    DOFS_ERR_DEVICE = 3,      /* a HIP runtime call failed; see dofs_last_error() */
+    DOFS_ERR_CAPACITY = 4,    /* result capacity too small; n_snapshots holds the required count */
+    DOFS_ERR_OOM = 5
+} dofs_status;
+
+/* Constants of the path; dofs_default_params() fills the reference values. */
+typedef struct dofs_params {
+    double blur_sigma;        /* 3.0   GaussianBlur(flow, flow, Size(0,0), 3.0)      segment.cpp:52 */
+    int32_t neighbor;         /* 8     get_segmented_array(..., 8)                    segment.cpp:154 */
+    int32_t min_size;         /* 500   Forest::new_merge default                      graph.hpp:93   */
+    double score_threshold;   /* 0.3   Forest::new_merge default                      graph.hpp:93   */
+    double overlay_min_score; /* 0.7   plot_best_segments_simple(..., 0.7)            segment.cpp:166 */
+    double min_convexity[3];  /* 3/4, 1/2, 20/29 per class                            graph.cpp:328-339 */
+    int32_t obj_size[3][2];   /* {258,84},{349,165},{370,180} BEV (l, w) per class     lifting_3d.cpp:257 */
+} dofs_params;
+
+/* Solution (graph.hpp:25-46). valid == 0 <=> Solution::rectangle is empty. */
+typedef struct dofs_solution {
+    int32_t cls;
+    int32_t valid;
+    float ps_bev[4][2];
+    float lower_face[4][2];
+    float upper_face[4][2];
+    float rectangle[4][2];
+    double w_error;
+    double h_error;
+    double orient;
+} dofs_solution;
+
+/* One non-empty slot of Forest::segment_history (graph.hpp:48-57, graph.cpp:348-356).
+ * slot  = history index = union-find root pixel id at the winning merge.
+ * event = index of the winning merge in Kruskal order (0 .. H*W-2).
+ * Member pixels (SegmentData::seg) = leaf_order[seg_begin .. seg_begin + size). */
+typedef struct dofs_snapshot {
+    int32_t slot;
+    int32_t event;
+    int32_t size;
+    int32_t seg_begin;
+    int32_t bbox[4];          /* xmin, ymin, xmax, ymax (inclusive), graph.cpp:197-207 */
+    double score;
+    double move;
+    dofs_solution sol;
+} dofs_snapshot;
+
+typedef struct dofs_stats {
+    int64_t n_edges;          /* graph edges (build_graph size) */
+    int64_t n_merges;         /* unions performed = H*W-1 */
+    int64_t n_candidates;     /* merges passing the size / row / move filters (graph.cpp:280-300) */
+    int64_t n_scored;         /* candidates with get_score != -1 */
+    int64_t n_qualified;      /* candidates passing convexity and score > threshold */
+    int64_t n_snapshots;      /* non-empty history slots */
+} dofs_stats;
+
+/* Caller-owned result buffers. Optional pointers may be NULL. */
+typedef struct dofs_result {
+    dofs_snapshot* snapshots; /* sorted by slot ascending */
+    int32_t snapshot_capacity;
+    int32_t n_snapshots;
+    int32_t* labels;          /* [H*W] overlay label: max slot among snapshots with score > overlay_min_score, else -1 */
+    int32_t* leaf_order;      /* [H*W] pixel ids in dendrogram leaf order */
+    float* blurred;           /* [H*W*2] blurred flow */
+    dofs_stats stats;
+} dofs_result;
+
+/* Per-merge record (debug / parity of the order-dependent replay): state of the merged set
+ * right after Forest::merge (graph.cpp:170-218) for merge k in Kruskal order. */
+typedef struct dofs_event {
+    int32_t start;            /* Edge::start (pixel id) */
+    int32_t end;              /* Edge::end */
+    double weight;            /* Edge::weight */
+    int32_t root;             /* parent_b returned by merge */
+    int32_t size;
+    int32_t rank;
+    int32_t bbox[4];
+    float mean[2];            /* Node::flow_value of the root */
+} dofs_event;
+
+/* Fixed-size 3D-box record for the frame-parallel gather (one per snapshot). */
+typedef struct dofs_box_record {
+    int32_t frame;
+    int32_t slot;
+    int32_t cls;
+    int32_t size;
+    float score;
+    float move;
+    float lower_face[4][2];
+    float upper_face[4][2];
+} dofs_box_record;
+
+typedef struct dofs_ctx dofs_ctx;
+
+int32_t dofs_abi_version(void);
+void dofs_default_params(dofs_params* p);
+
+/* get_mat() + get_mat_upper(0..2): persp = image→BEV, inv = BEV→image, inv_upper[cls] (host code). */
+int32_t dofs_calib(float persp[9], float inv[9], float inv_upper[27]);
+
+dofs_ctx* dofs_create(int32_t device);
+void dofs_destroy(dofs_ctx* ctx);
+const char* dofs_last_error(dofs_ctx* ctx);
+
+/* get_segmented_array on host buffers (H2D, run, D2H). row_stride_bytes = 0 → packed (W*8). */
+int32_t dofs_segment(dofs_ctx* ctx, const float* flow_uv, int32_t H, int32_t W, size_t row_stride_bytes,
+                     const float persp[9], const float inv[9], const float inv_upper[27],
+                     const dofs_params* params, dofs_result* out);
+
+/* Per-merge event stream of the last frame segmented by `ctx` (frame index within the last batch).
+ * events must hold H*W-1 records. */
+int32_t dofs_events(dofs_ctx* ctx, int32_t frame, dofs_event* events, int64_t capacity);
+
+/* Frame-parallel batch on device-resident input: d_flow = B×H×W×2 float32 (device pointer),
+ * stream = hipStream_t or NULL (the context's stream). Results stay on the device until
+ * dofs_batch_fetch / dofs_batch_records. */
+int32_t dofs_segment_batch_device(dofs_ctx* ctx, const float* d_flow, int32_t B, int32_t H, int32_t W,
+                                  const float persp[9], const float inv[9], const float inv_upper[27],
+                                  const dofs_params* params, void* stream);
+int32_t dofs_batch_fetch(dofs_ctx* ctx, int32_t frame, dofs_result* out);
+/* Device pointer to the batch's fixed-capacity box records (B × capacity records, frame-major;
+ * unused records have slot == -1) and per-frame counts (device int32[B]). */
+int32_t dofs_batch_records_device(dofs_ctx* ctx, void** d_records, void** d_counts, int32_t* capacity);
+
+/* get_bottom_variants on the GPU (one candidate, or n candidates with per-candidate class). */
+int32_t dofs_lift(dofs_ctx* ctx, const float dir[2], const int32_t box[4], const float mat[9],
+                  const float inv[9], const float inv_upper[9], int32_t cls, dofs_solution* out);
+int32_t dofs_lift_batch(dofs_ctx* ctx, int32_t n, const float* dirs, const int32_t* boxes,
+                        const int32_t* cls, const float mat[9], const float inv[9],
+                        const float inv_upper[27], dofs_solution* out);
+
+/* get_intersect (host code, exact float semantics of lifting_3d.cpp:63-89). */
+void dofs_intersect(const float a1[2], const float a2[2], const float b1[2], const float b2[2], float out[2]);
+
+/* Synthetic flow fields of the benchmark spec (DESIGN.md §Synthetic input), generated on device:
+ * frame b uses seed0 + b. d_out = B×H×W×2 float32. */
+int32_t dofs_synth_flow_device(float* d_out, int32_t B, int32_t H, int32_t W, uint64_t seed0, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DOFS_H */

@@ -1,0 +1,177 @@
+"""ctypes binding of the CPU oracle (oracle/_build/liboracle.so) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module. The product
+package (denseopticalflowsegmentation3d_amd/) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from denseopticalflowsegmentation3d_amd.abi import (
+    DofsParams, DofsResult, DofsSnapshot, DofsSolution, DofsEvent, default_params,
+)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIBS: dict[str, C.CDLL] = {}
+
+
+def build() -> None:
+    """Compile the oracle with its Makefile (gcc, -ffp-contract=off)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib(opt: str = "O2") -> C.CDLL:
+    name = "liboracle.so" if opt == "O2" else "liboracle_O0.so"
+    if name in _LIBS:
+        return _LIBS[name]
+    path = os.path.join(_HERE, "_build", name)
+    if not os.path.exists(path):
+        build()
+    L = C.CDLL(path)
+    fp = C.POINTER(C.c_float)
+    ip = C.POINTER(C.c_int32)
+    dp = C.POINTER(C.c_double)
+    L.oracle_default_params.argtypes = [C.POINTER(DofsParams)]
+    L.oracle_gaussian_kernel.argtypes = [C.c_double, fp, C.c_int32]
+    L.oracle_gaussian_kernel.restype = C.c_int32
+    L.oracle_blur.argtypes = [fp, C.c_int32, C.c_int32, C.c_double, fp]
+    L.oracle_intersect.argtypes = [fp, fp, fp, fp, fp]
+    L.oracle_lift.argtypes = [fp, ip, fp, fp, fp, C.c_int32, C.POINTER(DofsSolution)]
+    L.oracle_score.argtypes = [ip, fp, fp, fp, fp, C.POINTER(DofsSolution)]
+    L.oracle_score.restype = C.c_double
+    L.oracle_calib.argtypes = [fp, fp, fp]
+    L.oracle_perspective_transform.argtypes = [fp, fp, dp]
+    L.oracle_build_graph.argtypes = [fp, C.c_int32, C.c_int32, C.c_int32, ip, ip, dp, C.c_int64]
+    L.oracle_build_graph.restype = C.c_int64
+    L.oracle_synth_flow.argtypes = [fp, C.c_int32, C.c_int32, C.c_uint64]
+    L.oracle_segment.argtypes = [fp, C.c_int32, C.c_int32, fp, fp, fp, C.POINTER(DofsParams), C.c_int32,
+                                 C.POINTER(DofsResult), C.POINTER(DofsEvent)]
+    L.oracle_segment.restype = C.c_int32
+    _LIBS[name] = L
+    return L
+
+
+def _f(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def gaussian_kernel(sigma: float = 3.0) -> np.ndarray:
+    out = np.zeros(64, np.float32)
+    n = lib().oracle_gaussian_kernel(sigma, _ptr(out, C.c_float), 64)
+    return out[:n].copy()
+
+
+def blur(flow: np.ndarray, sigma: float = 3.0) -> np.ndarray:
+    flow = _f(flow)
+    H, W = flow.shape[:2]
+    out = np.empty_like(flow)
+    lib().oracle_blur(_ptr(flow, C.c_float), H, W, sigma, _ptr(out, C.c_float))
+    return out
+
+
+def intersect(a1, a2, b1, b2) -> np.ndarray:
+    v = [_f(x) for x in (a1, a2, b1, b2)]
+    out = np.zeros(2, np.float32)
+    lib().oracle_intersect(*[_ptr(x, C.c_float) for x in v], _ptr(out, C.c_float))
+    return out
+
+
+def lift(direction, box, mat, inv, inv_upper, cls: int) -> DofsSolution:
+    d = _f(direction)
+    b = np.ascontiguousarray(box, dtype=np.int32)
+    s = DofsSolution()
+    lib().oracle_lift(_ptr(d, C.c_float), _ptr(b, C.c_int32), _ptr(_f(mat), C.c_float), _ptr(_f(inv), C.c_float),
+                      _ptr(_f(inv_upper), C.c_float), cls, C.byref(s))
+    return s
+
+
+def score(box, direction, persp, inv, inv_upper27):
+    b = np.ascontiguousarray(box, dtype=np.int32)
+    s = DofsSolution()
+    v = lib().oracle_score(_ptr(b, C.c_int32), _ptr(_f(direction), C.c_float), _ptr(_f(persp), C.c_float),
+                           _ptr(_f(inv), C.c_float), _ptr(_f(inv_upper27), C.c_float), C.byref(s))
+    return v, s
+
+
+def calib():
+    persp = np.zeros(9, np.float32)
+    inv = np.zeros(9, np.float32)
+    up = np.zeros(27, np.float32)
+    lib().oracle_calib(_ptr(persp, C.c_float), _ptr(inv, C.c_float), _ptr(up, C.c_float))
+    return persp.reshape(3, 3), inv.reshape(3, 3), up.reshape(3, 3, 3)
+
+
+def perspective_transform(src, dst) -> np.ndarray:
+    out = np.zeros(9, np.float64)
+    lib().oracle_perspective_transform(_ptr(_f(src), C.c_float), _ptr(_f(dst), C.c_float), _ptr(out, C.c_double))
+    return out.reshape(3, 3)
+
+
+def build_graph(blurred: np.ndarray, neighbor: int = 8):
+    blurred = _f(blurred)
+    H, W = blurred.shape[:2]
+    cap = 4 * H * W
+    s = np.zeros(cap, np.int32)
+    e = np.zeros(cap, np.int32)
+    w = np.zeros(cap, np.float64)
+    n = lib().oracle_build_graph(_ptr(blurred, C.c_float), H, W, neighbor, _ptr(s, C.c_int32), _ptr(e, C.c_int32),
+                                 _ptr(w, C.c_double), cap)
+    return s[:n].copy(), e[:n].copy(), w[:n].copy()
+
+
+def synth_flow(H: int, W: int, seed: int = 0) -> np.ndarray:
+    out = np.zeros((H, W, 2), np.float32)
+    lib().oracle_synth_flow(_ptr(out, C.c_float), H, W, seed)
+    return out
+
+
+class OracleResult:
+    def __init__(self, H, W, snaps, labels, leaf_order, blurred, stats, events):
+        self.H, self.W = H, W
+        self.snapshots = snaps
+        self.labels = labels
+        self.leaf_order = leaf_order
+        self.blurred = blurred
+        self.stats = stats
+        self.events = events
+
+    def members(self, snap) -> np.ndarray:
+        return np.sort(self.leaf_order[snap["seg_begin"]:snap["seg_begin"] + snap["size"]])
+
+
+def segment(flow: np.ndarray, persp, inv, inv_upper, params: DofsParams | None = None, mode: int = 0,
+            events: bool = False, opt: str = "O2") -> OracleResult:
+    """get_segmented_array restated on the CPU (mode 0 fast, 1 faithful, 2 faithful + self-check)."""
+    flow = _f(flow)
+    H, W = flow.shape[:2]
+    N = H * W
+    if params is None:
+        params = default_params()
+    cap = max(N, 1)
+    snaps = np.zeros(cap, dtype=DofsSnapshot.np_dtype())
+    labels = np.zeros(N, np.int32)
+    leaf = np.zeros(N, np.int32)
+    blurred = np.zeros((H, W, 2), np.float32)
+    ev = np.zeros(max(N - 1, 1), dtype=DofsEvent.np_dtype()) if events else None
+    res = DofsResult()
+    res.snapshots = snaps.ctypes.data_as(C.POINTER(DofsSnapshot))
+    res.snapshot_capacity = cap
+    res.labels = _ptr(labels, C.c_int32)
+    res.leaf_order = _ptr(leaf, C.c_int32)
+    res.blurred = _ptr(blurred, C.c_float)
+    rc = lib(opt).oracle_segment(_ptr(flow, C.c_float), H, W, _ptr(_f(persp), C.c_float), _ptr(_f(inv), C.c_float),
+                                 _ptr(_f(inv_upper), C.c_float), C.byref(params), mode, C.byref(res),
+                                 ev.ctypes.data_as(C.POINTER(DofsEvent)) if events else None)
+    if rc != 0:
+        raise RuntimeError(f"oracle_segment failed with status {rc}")
+    st = {k: getattr(res.stats, k) for k, _ in res.stats._fields_}
+    return OracleResult(H, W, snaps[:res.n_snapshots].copy(), labels, leaf, blurred, st,
+                        ev[:max(N - 1, 0)] if events else None)
