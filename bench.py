@@ -1,0 +1,168 @@
+"""Benchmark: Mpixels/s of segment + lifting_3d on synthetic 1080p flow fields (BASELINE.json metric).
+
+One step = one batch of `--batch` synthetic 1920x1080 flow fields per GPU pushed through the whole
+HIP path (blur → MST → Kruskal replay → per-merge filters + 3D lifting → snapshots → labels), then
+the fixed-size 3D-box records of every frame gathered to all ranks (RCCL all_gather over xGMI when
+N > 1). Inputs are generated on device before timing (resident in HBM); frames are independent, so
+ranks shard frames with no data-path collective besides the box gather ("scaling": "weak").
+
+Usage: python bench.py [--gpus N --steps K --warmup W --batch B]
+       (N > 1 under torch.distributed.run, one process per GPU)
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from denseopticalflowsegmentation3d_amd import runtime  # noqa: E402
+from denseopticalflowsegmentation3d_amd.abi import DofsBoxRecord, default_params  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+GATHER_PER_FRAME = 64  # box records per frame in the gathered block
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8, help="frames per GPU per step")
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--cpu-frames", type=int, default=1, help="frames of the CPU baseline sample (0 = skip)")
+    ap.add_argument("--no-stages", action="store_true", help="skip the per-stage event timing pass")
+    return ap.parse_args()
+
+
+def cpu_baseline(H, W, frames):
+    """Reference-faithful CPU restatement (oracle mode 1: std::multiset / std::set structures, -O2,
+    one thread) on a bounded sample of the same workload."""
+    from oracle import binding as ob
+    persp, inv, up = ob.calib()
+    total = 0.0
+    for s in range(frames):
+        flow = ob.synth_flow(H, W, s)
+        t0 = time.perf_counter()
+        ob.segment(flow, persp, inv, up, mode=1)
+        total += time.perf_counter() - t0
+    return {"value": round(frames * H * W / total / 1e6, 4), "unit": "Mpixels/sec", "cores": 1, "kind": "port",
+            "sample": f"{frames} synthetic {W}x{H} frame(s) (seed 0..{frames - 1}), faithful mode "
+                      f"(std::multiset edge sort + std::set unions + set-copy snapshots), g++ -O2, "
+                      f"{total:.1f} s"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B, H, W = a.batch, a.height, a.width
+    N = H * W
+
+    ctx = runtime.Dofs(local)
+    persp, inv, up = runtime.calib()
+    prm = default_params()
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    flows = torch.empty((B, H, W, 2), dtype=torch.float32, device=dev)
+    runtime.synth_flow_device(flows.data_ptr(), B, H, W, seed0=rank * B, stream=sh)
+    rec_bytes = 4 * B + B * GATHER_PER_FRAME * DofsBoxRecord.np_dtype().itemsize
+    rec = torch.empty(rec_bytes, dtype=torch.uint8, device=dev)
+    gathered = torch.empty(world * rec_bytes, dtype=torch.uint8, device=dev) if world > 1 else None
+
+    def step():
+        ctx.segment_batch_device(flows.data_ptr(), B, H, W, persp, inv, up, params=prm, stream=sh)
+        ctx.records_copy(rec.data_ptr(), GATHER_PER_FRAME, stream=sh)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, rec)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(a.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms_ev = e0.elapsed_time(e1)
+    t = torch.tensor([max(wall, ms_ev / 1e3)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    frames = world * B * a.steps
+    value = frames * N / elapsed / 1e6
+
+    # per-stage device-event timing of extra profiled batches (not part of the timed region)
+    stages, roof = None, None
+    if not a.no_stages:
+        ctx.profile(True)
+        for _ in range(max(2, a.steps // 2)):
+            step()
+        torch.cuda.synchronize()
+        ms, nb = ctx.profile_read()
+        ctx.profile(False)
+        stages = {k: round(v / nb, 3) for k, v in ms.items()}
+        # the path's input read (8 B/px, the north star's HBM roofline) over the measured batch time
+        t_batch = sum(v for v in ms.values()) / nb / 1e3
+        achieved = B * N * 8 / t_batch / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                "kernel": "whole path per batch (8 B/px flow read); see DESIGN.md §Roofline"}
+
+    if rank == 0:
+        res = ctx.fetch(0, want_blur=False)
+        out = {
+            "metric": "Mpixels/sec segment+lifting_3d @1080p",
+            "value": round(value, 3),
+            "unit": "Mpixels/sec",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32+f64",
+            "data": "synthetic (on-device splitmix64 flow fields, DESIGN.md §Synthetic input)",
+            "config": {"workload": f"{W}x{H} synthetic flow, full segment + lifting_3d (BASELINE config 3 shape)",
+                       "frames_per_gpu_per_step": B, "frames_per_sec": round(frames / elapsed, 3),
+                       "parallelism": f"frame-parallel x{world}", "snapshots_frame0": int(len(res.snapshots)),
+                       "candidates_frame0": int(res.stats["n_candidates"])},
+            "roofline": roof,
+            "stages_ms_per_batch": stages,
+            "cpu_baseline": None,
+        }
+        if world == 1 and a.cpu_frames > 0:
+            out["cpu_baseline"] = cpu_baseline(H, W, a.cpu_frames)
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

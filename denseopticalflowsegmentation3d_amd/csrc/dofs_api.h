@@ -1,0 +1,369 @@
+// dofs_api.h — implementation of the C-ABI of include/dofs.h over a pipeline backend.
+// dofs_hip.hip instantiates it with the HIP backend and exports the extern "C" symbols.
+#pragma once
+
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "dofs_pipeline.h"
+
+namespace dofs {
+
+// ---- host-side constants (boundary helpers, not on the hot path) ------------------------------
+
+inline void default_params(dofs_params* p) {
+    p->blur_sigma = 3.0;              // segment.cpp:52
+    p->neighbor = 8;                  // segment.cpp:154
+    p->min_size = 500;                // graph.hpp:93
+    p->score_threshold = 0.3;         // graph.hpp:93
+    p->overlay_min_score = 0.7;       // segment.cpp:166
+    p->min_convexity[0] = 3.0 / 4.0;  // graph.cpp:328-339
+    p->min_convexity[1] = 1.0 / 2.0;
+    p->min_convexity[2] = 20.0 / 29.0;
+    const int sz[3][2] = {{258, 84}, {349, 165}, {370, 180}};  // lifting_3d.cpp:257
+    for (int c = 0; c < 3; ++c) {
+        p->obj_size[c][0] = sz[c][0];
+        p->obj_size[c][1] = sz[c][1];
+    }
+}
+
+// cv::getPerspectiveTransform: 8x8 system (float point products), Gaussian elimination with
+// partial pivoting in double, back substitution by division, M(2,2) = 1.
+inline void perspective_transform(const float src[4][2], const float dst[4][2], float out[9]) {
+    double a[8][9];
+    for (int i = 0; i < 4; ++i) {
+        const float sx = src[i][0], sy = src[i][1], dx = dst[i][0], dy = dst[i][1];
+        double* r0 = a[i];
+        double* r1 = a[i + 4];
+        for (int j = 0; j < 9; ++j) r0[j] = r1[j] = 0.0;
+        r0[0] = r1[3] = sx;
+        r0[1] = r1[4] = sy;
+        r0[2] = r1[5] = 1.0;
+        r0[6] = -sx * dx;
+        r0[7] = -sy * dx;
+        r1[6] = -sx * dy;
+        r1[7] = -sy * dy;
+        r0[8] = dx;
+        r1[8] = dy;
+    }
+    for (int c = 0; c < 8; ++c) {
+        int piv = c;
+        for (int r = c + 1; r < 8; ++r)
+            if (fabs(a[r][c]) > fabs(a[piv][c])) piv = r;
+        if (piv != c)
+            for (int j = c; j < 9; ++j) {
+                double t = a[c][j];
+                a[c][j] = a[piv][j];
+                a[piv][j] = t;
+            }
+        const double nd = -1 / a[c][c];
+        for (int r = c + 1; r < 8; ++r) {
+            const double al = a[r][c] * nd;
+            for (int j = c + 1; j < 9; ++j) a[r][j] += al * a[c][j];
+        }
+    }
+    double x[8];
+    for (int r = 7; r >= 0; --r) {
+        double s = a[r][8];
+        for (int j = r + 1; j < 8; ++j) s -= a[r][j] * x[j];
+        x[r] = s / a[r][r];
+    }
+    for (int i = 0; i < 8; ++i) out[i] = (float)x[i];
+    out[8] = 1.0f;
+}
+
+// get_mat (lifting_3d.cpp:482-514) + get_mat_upper (:441-480)
+inline void calib(float persp[9], float inv[9], float inv_upper[27]) {
+    const float bev[4][2] = {{100.f, 13000.f}, {100.f, 6000.f}, {800.f, 6000.f}, {800.f, 13000.f}};
+    const float img[4][2] = {{215.f, 265.f}, {90.f, 121.f}, {294.f, 120.f}, {625.f, 265.f}};
+    perspective_transform(img, bev, persp);
+    perspective_transform(bev, img, inv);
+    const float up[3][4][2] = {{{215, 176}, {90, 85}, {294, 85}, {625, 176}},
+                               {{215, 185}, {90, 80}, {294, 80}, {625, 185}},
+                               {{215, 140}, {90, 55}, {294, 55}, {625, 140}}};
+    for (int c = 0; c < 3; ++c) perspective_transform(bev, up[c], inv_upper + 9 * c);
+}
+
+inline int64_t graph_edges(int H, int W, bool nbr8) {  // build_graph size (graph.cpp:62-93)
+    int64_t e = (int64_t)(W - 1) * H + (int64_t)W * (H - 1);
+    if (nbr8) e += 2 * (int64_t)(W - 1) * (H - 1);
+    return e;
+}
+
+struct KLiftBatch {
+    const F2* dirs;
+    const int* boxes;
+    const int* cls;
+    dofs_solution* out;
+    LiftMats L;
+    DOFS_HD void operator()(int, int64_t i) const {
+        lift_one(mk(dirs[i].x, dirs[i].y), boxes + 4 * i, L, cls[i], out + i);
+    }
+};
+
+// Synthetic benchmark flow (DESIGN.md §Synthetic input): splitmix64 noise quantised to 2^-10 in
+// [-0.0996, 0.0996] plus three constant-flow rectangles, jittered by ±5 % for seeds != 0.
+DOFS_HD inline unsigned long long splitmix64(unsigned long long x) {
+    unsigned long long z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+DOFS_HD inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+struct KSynth {
+    F2* out;
+    int H, W;
+    unsigned long long seed0;
+    DOFS_HD void operator()(int f, int64_t p) const {
+        const unsigned long long seed = seed0 + (unsigned long long)f;
+        const int64_t N = (int64_t)H * W;
+        F2 v;
+        {
+            unsigned long long z0 = splitmix64((seed << 32) + (unsigned long long)(2 * p));
+            unsigned long long z1 = splitmix64((seed << 32) + (unsigned long long)(2 * p + 1));
+            v.x = (float)((int)((z0 >> 11) % 205ull) - 102) * (1.0f / 1024.0f);
+            v.y = (float)((int)((z1 >> 11) % 205ull) - 102) * (1.0f / 1024.0f);
+        }
+        const int x = (int)(p % W), y = (int)(p / W);
+        const int rect[3][4] = {{550, 900, 250, 800}, {100, 350, 400, 750}, {400, 500, 500, 900}};
+        const float uv[3][2] = {{2.5f, 1.9f}, {-1.8f, 0.6f}, {0.3f, 2.2f}};
+        for (int r = 0; r < 3; ++r) {
+            int x0 = (int)((int64_t)W * rect[r][0] / 1000), x1 = (int)((int64_t)W * rect[r][1] / 1000);
+            int y0 = (int)((int64_t)H * rect[r][2] / 1000), y1 = (int)((int64_t)H * rect[r][3] / 1000);
+            if (seed != 0) {
+                unsigned long long zx = splitmix64((seed << 32) + 0xF0000000ull + 2ull * r);
+                unsigned long long zy = splitmix64((seed << 32) + 0xF0000000ull + 2ull * r + 1);
+                int jx = (int)((int64_t)(zx % 101ull) * W / 1000) - (int)((int64_t)50 * W / 1000);
+                int jy = (int)((int64_t)(zy % 101ull) * H / 1000) - (int)((int64_t)50 * H / 1000);
+                x0 = clampi(x0 + jx, 0, W);
+                x1 = clampi(x1 + jx, 0, W);
+                y0 = clampi(y0 + jy, 0, H);
+                y1 = clampi(y1 + jy, 0, H);
+            }
+            if (x >= x0 && x < x1 && y >= y0 && y < y1) {
+                v.x = uv[r][0];
+                v.y = uv[r][1];
+            }
+        }
+        out[(int64_t)f * N + p] = v;
+    }
+};
+
+// ---- context -----------------------------------------------------------------------------------
+
+template <class Backend>
+struct Context {
+    Backend be;
+    Pipeline<Backend> pipe;
+    std::string err;
+    void* d_in = nullptr;
+    size_t d_in_bytes = 0;
+    void* d_scratch = nullptr;
+    size_t d_scratch_bytes = 0;
+    bool have_batch = false;
+    int last_B = 0, last_H = 0, last_W = 0;
+    dofs_params last_prm;
+
+    explicit Context(int device) : be(device), pipe(be) { default_params(&last_prm); }
+    ~Context() {
+        if (d_in) be.free(d_in);
+        if (d_scratch) be.free(d_scratch);
+    }
+    void* scratch(size_t bytes) {
+        if (bytes > d_scratch_bytes) {
+            if (d_scratch) be.free(d_scratch);
+            d_scratch = be.alloc(bytes);
+            d_scratch_bytes = d_scratch ? bytes : 0;
+        }
+        return d_scratch;
+    }
+    int fail(int code, const std::string& msg) {
+        err = msg;
+        return code;
+    }
+    int check() {
+        if (!be.ok()) return fail(DOFS_ERR_DEVICE, be.error());
+        return DOFS_OK;
+    }
+};
+
+template <class Backend>
+int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int H, int W, const float persp[9],
+            const float inv[9], const float inv_upper[27], const dofs_params* params) {
+    if (B <= 0 || H <= 0 || W <= 0 || !persp || !inv || !inv_upper) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
+    if (H > 32767 || W > 32767) return cx->fail(DOFS_ERR_INVALID_ARG, "H and W must be < 32768");
+    if ((int64_t)H * W >= (1 << 26)) return cx->fail(DOFS_ERR_INVALID_ARG, "H*W must be < 2^26");
+    dofs_params prm;
+    if (params)
+        prm = *params;
+    else
+        default_params(&prm);
+    // segment.cpp:38-43: anything but 8 segments with the 4-neighbourhood (logged, not an error)
+    const int nbr8 = prm.neighbor == 8 ? 1 : 0;
+    Dims d = Pipeline<Backend>::dims_for(B, H, W, nbr8);
+    if (!cx->pipe.reserve(d)) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    cx->pipe.set_params(prm, persp, inv, inv_upper);
+    cx->pipe.run(d_flow, fstride);
+    cx->have_batch = true;
+    cx->last_B = B;
+    cx->last_H = H;
+    cx->last_W = W;
+    cx->last_prm = prm;
+    return cx->check();
+}
+
+template <class Backend>
+int api_fetch(Context<Backend>* cx, int frame, dofs_result* out) {
+    if (!cx->have_batch || frame < 0 || frame >= cx->last_B || !out) return cx->fail(DOFS_ERR_INVALID_ARG, "no frame");
+    Backend& be = cx->be;
+    const Ws& w = cx->pipe.w;
+    const Dims& d = w.d;
+    int ctr[kCounters];
+    be.d2h(ctr, w.ctr + (int64_t)frame * kCounters, sizeof(ctr));
+    be.sync();
+    const int ns = ctr[C_SNAP];
+    out->n_snapshots = ns;
+    out->stats.n_edges = graph_edges(cx->last_H, cx->last_W, cx->last_prm.neighbor == 8);
+    out->stats.n_merges = d.M;
+    out->stats.n_candidates = ctr[C_CAND];
+    out->stats.n_scored = ctr[C_SCORED];
+    out->stats.n_qualified = ctr[C_QUAL];
+    out->stats.n_snapshots = ns;
+    if (out->snapshots) {
+        if (ns > out->snapshot_capacity || ns > w.snap_cap) return cx->fail(DOFS_ERR_CAPACITY, "snapshot capacity");
+        if (ns) be.d2h(out->snapshots, w.snaps + (int64_t)frame * w.snap_cap, sizeof(dofs_snapshot) * (size_t)ns);
+    } else if (ns > w.snap_cap) {
+        return cx->fail(DOFS_ERR_CAPACITY, "snapshot capacity");
+    }
+    if (out->labels) be.d2h(out->labels, w.labels + (int64_t)frame * d.N, sizeof(int) * (size_t)d.N);
+    if (out->leaf_order) be.d2h(out->leaf_order, w.leaf_order + (int64_t)frame * d.N, sizeof(int) * (size_t)d.N);
+    if (out->blurred) be.d2h(out->blurred, w.blur + (int64_t)frame * d.N, sizeof(F2) * (size_t)d.N);
+    be.sync();
+    return cx->check();
+}
+
+template <class Backend>
+int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity) {
+    if (!cx->have_batch || frame < 0 || frame >= cx->last_B || !ev) return cx->fail(DOFS_ERR_INVALID_ARG, "no frame");
+    const Ws& w = cx->pipe.w;
+    const Dims& d = w.d;
+    if (capacity < d.M) return cx->fail(DOFS_ERR_CAPACITY, "event capacity");
+    if (d.M <= 0) return DOFS_OK;
+    Backend& be = cx->be;
+    std::vector<int> eu((size_t)d.M), evv((size_t)d.M);
+    std::vector<unsigned long long> key((size_t)d.M);
+    std::vector<NodeVal> v((size_t)d.M);
+    be.d2h(eu.data(), w.EU + (int64_t)frame * d.M, 4 * (size_t)d.M);
+    be.d2h(evv.data(), w.EV + (int64_t)frame * d.M, 4 * (size_t)d.M);
+    be.d2h(key.data(), w.key_out + (int64_t)frame * d.M, 8 * (size_t)d.M);
+    be.d2h(v.data(), w.V + (int64_t)frame * d.NL + d.N, sizeof(NodeVal) * (size_t)d.M);
+    be.sync();
+    for (int64_t i = 0; i < d.M; ++i) {
+        dofs_event& e = ev[i];
+        e.start = eu[i];
+        e.end = evv[i];
+        memcpy(&e.weight, &key[i], sizeof(double));
+        e.root = v[i].root;
+        e.size = v[i].size;
+        e.rank = v[i].rank;
+        e.bbox[0] = v[i].x0;
+        e.bbox[1] = v[i].y0;
+        e.bbox[2] = v[i].x1;
+        e.bbox[3] = v[i].y1;
+        e.mean[0] = v[i].mx;
+        e.mean[1] = v[i].my;
+    }
+    return cx->check();
+}
+
+template <class Backend>
+int api_segment(Context<Backend>* cx, const float* flow, int H, int W, size_t stride, const float persp[9],
+                const float inv[9], const float inv_upper[27], const dofs_params* params, dofs_result* out) {
+    if (!flow || H <= 0 || W <= 0 || !out) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
+    const size_t row = (size_t)W * 2 * sizeof(float);
+    if (stride == 0) stride = row;
+    if (stride < row) return cx->fail(DOFS_ERR_INVALID_ARG, "row stride too small");
+    const size_t bytes = row * (size_t)H;
+    if (bytes > cx->d_in_bytes) {
+        if (cx->d_in) cx->be.free(cx->d_in);
+        cx->d_in = cx->be.alloc(bytes);
+        cx->d_in_bytes = cx->d_in ? bytes : 0;
+        if (!cx->d_in) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    }
+    if (stride == row) {
+        cx->be.h2d(cx->d_in, flow, bytes);
+    } else {
+        for (int y = 0; y < H; ++y)
+            cx->be.h2d((char*)cx->d_in + row * y, (const char*)flow + stride * y, row);
+    }
+    int rc = api_run(cx, (const F2*)cx->d_in, (int64_t)H * W, 1, H, W, persp, inv, inv_upper, params);
+    if (rc) return rc;
+    int n = 0;  // more history slots than the device snapshot capacity: grow it and run again
+    cx->be.d2h(&n, cx->pipe.w.ctr + C_SNAP, sizeof(int));
+    cx->be.sync();
+    if (n > cx->pipe.snap_cap) {
+        while (cx->pipe.snap_cap < n) cx->pipe.snap_cap *= 2;
+        cx->pipe.cap.B = 0;  // force a new layout
+        rc = api_run(cx, (const F2*)cx->d_in, (int64_t)H * W, 1, H, W, persp, inv, inv_upper, params);
+        if (rc) return rc;
+    }
+    return api_fetch(cx, 0, out);
+}
+
+template <class Backend>
+int api_records_copy(Context<Backend>* cx, void* dst, int per_frame, void* stream) {
+    if (!cx->have_batch || !dst || per_frame < 0) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
+    const Ws& w = cx->pipe.w;
+    const int B = cx->last_B;
+    const int k = per_frame < w.snap_cap ? per_frame : w.snap_cap;
+    cx->be.set_stream(stream);
+    cx->be.copy2d(dst, sizeof(int), w.ctr + C_SNAP, sizeof(int) * kCounters, sizeof(int), B);
+    if (k > 0)
+        cx->be.copy2d((char*)dst + sizeof(int) * B, sizeof(dofs_box_record) * per_frame, w.recs,
+                      sizeof(dofs_box_record) * w.snap_cap, sizeof(dofs_box_record) * k, B);
+    return cx->check();
+}
+
+template <class Backend>
+int api_lift_batch(Context<Backend>* cx, int n, const float* dirs, const int* boxes, const int* cls, const float mat[9],
+                   const float inv[9], const float inv_upper[27], dofs_solution* out) {
+    if (n <= 0 || !dirs || !boxes || !cls || !mat || !inv || !inv_upper || !out)
+        return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
+    for (int i = 0; i < n; ++i)
+        if (cls[i] < 0 || cls[i] > 2) return cx->fail(DOFS_ERR_INVALID_ARG, "cls must be 0..2");
+    const size_t b_dirs = sizeof(F2) * n, b_box = 16 * (size_t)n, b_cls = 4 * (size_t)n,
+                 b_out = sizeof(dofs_solution) * n;
+    const size_t o_box = (b_dirs + 255) & ~(size_t)255;
+    const size_t o_cls = (o_box + b_box + 255) & ~(size_t)255;
+    const size_t o_out = (o_cls + b_cls + 255) & ~(size_t)255;
+    char* s = (char*)cx->scratch(o_out + b_out);
+    if (!s) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    Backend& be = cx->be;
+    be.h2d(s, dirs, b_dirs);
+    be.h2d(s + o_box, boxes, b_box);
+    be.h2d(s + o_cls, cls, b_cls);
+    KLiftBatch k;
+    k.dirs = (const F2*)s;
+    k.boxes = (const int*)(s + o_box);
+    k.cls = (const int*)(s + o_cls);
+    k.out = (dofs_solution*)(s + o_out);
+    memcpy(k.L.persp, mat, sizeof(k.L.persp));
+    memcpy(k.L.inv, inv, sizeof(k.L.inv));
+    memcpy(k.L.inv_upper, inv_upper, sizeof(k.L.inv_upper));
+    dofs_params prm;
+    default_params(&prm);
+    for (int c = 0; c < 3; ++c) {
+        k.L.obj_size[c][0] = prm.obj_size[c][0];
+        k.L.obj_size[c][1] = prm.obj_size[c][1];
+    }
+    be.launch(1, n, k);
+    be.d2h(out, s + o_out, b_out);
+    be.sync();
+    return cx->check();
+}
+
+}  // namespace dofs

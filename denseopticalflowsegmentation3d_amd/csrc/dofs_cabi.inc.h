@@ -1,0 +1,118 @@
+// dofs_cabi.inc.h — extern "C" entry points of include/dofs.h. Included once by a translation unit
+// that has defined `using DofsBackend = <backend>;` (dofs_hip.hip: the HIP backend).
+#pragma once
+
+#include "dofs_api.h"
+
+struct dofs_ctx : dofs::Context<DofsBackend> {
+    explicit dofs_ctx(int device) : dofs::Context<DofsBackend>(device) {}
+};
+
+extern "C" {
+
+int32_t dofs_abi_version(void) { return DOFS_ABI_VERSION; }
+
+void dofs_default_params(dofs_params* p) {
+    if (p) dofs::default_params(p);
+}
+
+int32_t dofs_calib(float persp[9], float inv[9], float inv_upper[27]) {
+    if (!persp || !inv || !inv_upper) return DOFS_ERR_INVALID_ARG;
+    dofs::calib(persp, inv, inv_upper);
+    return DOFS_OK;
+}
+
+void dofs_intersect(const float a1[2], const float a2[2], const float b1[2], const float b2[2], float out[2]) {
+    dofs::P2 r = dofs::intersect(dofs::mk(a1[0], a1[1]), dofs::mk(a2[0], a2[1]), dofs::mk(b1[0], b1[1]),
+                                 dofs::mk(b2[0], b2[1]));
+    out[0] = r.x;
+    out[1] = r.y;
+}
+
+dofs_ctx* dofs_create(int32_t device) {
+    if (!DofsBackend::device_ok(device)) return nullptr;
+    dofs_ctx* c = new dofs_ctx(device);
+    if (!c->be.ok()) {
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+void dofs_destroy(dofs_ctx* ctx) { delete ctx; }
+
+const char* dofs_last_error(dofs_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int32_t dofs_segment(dofs_ctx* ctx, const float* flow_uv, int32_t H, int32_t W, size_t row_stride_bytes,
+                     const float persp[9], const float inv[9], const float inv_upper[27], const dofs_params* params,
+                     dofs_result* out) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    ctx->be.set_stream(nullptr);
+    return dofs::api_segment(ctx, flow_uv, H, W, row_stride_bytes, persp, inv, inv_upper, params, out);
+}
+
+int32_t dofs_events(dofs_ctx* ctx, int32_t frame, dofs_event* events, int64_t capacity) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    return dofs::api_events(ctx, frame, events, capacity);
+}
+
+int32_t dofs_segment_batch_device(dofs_ctx* ctx, const float* d_flow, int32_t B, int32_t H, int32_t W,
+                                  const float persp[9], const float inv[9], const float inv_upper[27],
+                                  const dofs_params* params, void* stream) {
+    if (!ctx || !d_flow) return DOFS_ERR_INVALID_ARG;
+    ctx->be.set_stream(stream);
+    return dofs::api_run(ctx, (const dofs::F2*)d_flow, (int64_t)H * W, B, H, W, persp, inv, inv_upper, params);
+}
+
+int32_t dofs_batch_fetch(dofs_ctx* ctx, int32_t frame, dofs_result* out) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    return dofs::api_fetch(ctx, frame, out);
+}
+
+int32_t dofs_batch_records_device(dofs_ctx* ctx, void** d_records, void** d_counts, int32_t* capacity) {
+    if (!ctx || !ctx->have_batch) return DOFS_ERR_INVALID_ARG;
+    if (d_records) *d_records = ctx->pipe.w.recs;
+    if (d_counts) *d_counts = ctx->pipe.w.ctr;  // int32 counters, stride kCounters, count at C_SNAP
+    if (capacity) *capacity = ctx->pipe.w.snap_cap;
+    return DOFS_OK;
+}
+
+int32_t dofs_batch_records_copy(dofs_ctx* ctx, void* d_dst, int32_t per_frame, void* stream) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    return dofs::api_records_copy(ctx, d_dst, per_frame, stream);
+}
+
+int32_t dofs_profile(dofs_ctx* ctx, int32_t enable) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    ctx->be.profile(enable != 0);
+    return DOFS_OK;
+}
+
+int32_t dofs_profile_read(dofs_ctx* ctx, double ms[8], int32_t* batches) {
+    if (!ctx || !ms) return DOFS_ERR_INVALID_ARG;
+    int n = ctx->be.profile_read(ms);
+    if (batches) *batches = n;
+    return ctx->check();
+}
+
+int32_t dofs_lift(dofs_ctx* ctx, const float dir[2], const int32_t box[4], const float mat[9], const float inv[9],
+                  const float inv_upper[9], int32_t cls, dofs_solution* out) {
+    if (!ctx || cls < 0 || cls > 2 || !inv_upper) return DOFS_ERR_INVALID_ARG;
+    float up[27] = {0};
+    for (int i = 0; i < 9; ++i) up[9 * cls + i] = inv_upper[i];
+    return dofs::api_lift_batch(ctx, 1, dir, box, &cls, mat, inv, up, out);
+}
+
+int32_t dofs_lift_batch(dofs_ctx* ctx, int32_t n, const float* dirs, const int32_t* boxes, const int32_t* cls,
+                        const float mat[9], const float inv[9], const float inv_upper[27], dofs_solution* out) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    return dofs::api_lift_batch(ctx, n, dirs, boxes, cls, mat, inv, inv_upper, out);
+}
+
+int32_t dofs_synth_flow_device(float* d_out, int32_t B, int32_t H, int32_t W, uint64_t seed0, void* stream) {
+    if (!d_out || B <= 0 || H <= 0 || W <= 0) return DOFS_ERR_INVALID_ARG;
+    dofs::KSynth k{(dofs::F2*)d_out, H, W, (unsigned long long)seed0};
+    return DofsBackend::launch_static(stream, B, (int64_t)H * W, k);
+}
+
+}  // extern "C"

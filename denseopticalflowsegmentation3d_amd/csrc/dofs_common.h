@@ -1,0 +1,68 @@
+// dofs_common.h — shared types of the MI355X clustering + lifting pipeline.
+//
+// The including translation unit defines, before including this header:
+//   DOFS_HD                          function qualifier of per-element kernel bodies
+//   DOFS_HDM                         host+device qualifier of pure math helpers (dofs_lift.h)
+//   dofs_ld / dofs_st                relaxed agent-scope load / store of an int
+//   dofs_cas / dofs_exch             agent-scope compare-and-swap / exchange of an int
+//   dofs_amin_u64 / dofs_amax_u64    agent-scope atomic min / max of a uint64
+//   dofs_amin / dofs_amax / dofs_aadd / dofs_aor   agent-scope atomics on int
+//   dofs_amin_u32                    agent-scope atomic min of a uint32
+// dofs_hip.hip maps them to HIP atomics on gfx950; the test-only host emulator maps them to plain
+// sequential operations.
+#pragma once
+
+#include <stdint.h>
+
+#include "../../include/dofs.h"
+
+namespace dofs {
+
+struct F2 {
+    float x, y;
+};
+
+struct I4 {
+    int x0, y0, x1, y1;
+};
+
+// Value of one Kruskal-reconstruction-tree node = state of a union-find root right after the merge
+// that created it (graph.cpp:170-218): size, union-by-rank root and rank, float running mean, bbox.
+struct NodeVal {
+    float mx, my;
+    int size;
+    int root;
+    int16_t x0, y0, x1, y1;
+    int rank;
+    int pad;
+};
+static_assert(sizeof(NodeVal) == 32, "NodeVal must stay 32 bytes (one gather = 2 x dwordx4)");
+
+constexpr int kMaxTaps = 64;
+constexpr int kRoundsMax = 40;        // Borůvka round flags per frame
+constexpr int kCounters = 64;         // per-frame counter block (ints)
+enum Counter {
+    C_PATHS = 0,
+    C_CAND = 1,
+    C_SCORED = 2,
+    C_QUAL = 3,
+    C_SNAP = 4,
+    C_MST = 5,
+    C_ACT = 8  // C_ACT + r: Borůvka round r found a cross-component edge
+};
+
+constexpr uint32_t kNoEdge = 0xFFFFFFFFu;
+constexpr int kIntMax = 0x7FFFFFFF;
+
+// Linear dimensions of one frame and of the batch.
+struct Dims {
+    int H, W;
+    int64_t N;   // pixels
+    int64_t M;   // MST edges = merges = N - 1
+    int64_t NL;  // KRT nodes = label space = N + M
+    int64_t P2;  // power of two >= N (segment tree leaves)
+    int B;       // frames in the batch
+    int nbr8;
+};
+
+}  // namespace dofs

@@ -1,0 +1,221 @@
+// dofs_hip.hip — HIP/CDNA4 (gfx950) backend of the dense-optical-flow clustering + 3D-lifting path
+// and the exported C-ABI (include/dofs.h). Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off.
+//
+// Every per-element body in dofs_kernels.h runs here as a grid-stride kernel over a 2-D grid
+// (x: elements, y: frames of the batch), 256-thread workgroups (4 wave64s). Atomics are agent-scope
+// (coherent across the 8 XCDs); union-find loads inside a launch use relaxed agent-scope atomic loads
+// so a stale L1/L2 line can never be re-read forever (MI355X_MICROARCH.md §inter-workgroup visibility).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <array>
+#include <string>
+#include <vector>
+
+#define DOFS_HD __device__
+#define DOFS_HDM __host__ __device__
+
+__device__ inline int dofs_ld(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ inline void dofs_st(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ inline int dofs_cas(int* p, int expected, int v) {
+    int old = expected;
+    __hip_atomic_compare_exchange_strong(p, &old, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return old;
+}
+__device__ inline int dofs_exch(int* p, int v) { return atomicExch(p, v); }
+__device__ inline void dofs_amin_u64(unsigned long long* p, unsigned long long v) { atomicMin(p, v); }
+__device__ inline void dofs_amax_u64(unsigned long long* p, unsigned long long v) { atomicMax(p, v); }
+__device__ inline void dofs_amin_u32(unsigned* p, unsigned v) { atomicMin(p, v); }
+__device__ inline void dofs_amin(int* p, int v) { atomicMin(p, v); }
+__device__ inline void dofs_amax(int* p, int v) { atomicMax(p, v); }
+__device__ inline int dofs_aadd(int* p, int v) { return atomicAdd(p, v); }
+__device__ inline void dofs_aor(int* p, int v) { atomicOr(p, v); }
+
+#include "dofs_common.h"
+#include "dofs_kernels.h"
+
+namespace dofs {
+
+constexpr int kBlock = 256;
+
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_generic(F f, int64_t n) {
+    const int fr = blockIdx.y;
+    const int64_t step = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += step) f(fr, i);
+}
+
+struct HipBackend {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    hipError_t last = hipSuccess;
+    std::string msg;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+
+    static bool device_ok(int dev) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || dev < 0 || dev >= n) return false;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+        return std::string(prop.gcnArchName).rfind("gfx950", 0) == 0;
+    }
+
+    explicit HipBackend(int dev) : device(dev) {
+        note(hipSetDevice(dev), "hipSetDevice");
+        note(hipStreamCreateWithFlags(&own, hipStreamNonBlocking), "hipStreamCreate");
+        stream = own;
+    }
+    ~HipBackend() {
+        for (auto e : pool) (void)hipEventDestroy(e);
+        if (tmp) (void)hipFree(tmp);
+        if (own) (void)hipStreamDestroy(own);
+    }
+    void note(hipError_t e, const char* what) {
+        if (e != hipSuccess && last == hipSuccess) {
+            last = e;
+            msg = std::string(what) + ": " + hipGetErrorString(e);
+        }
+    }
+    bool ok() const { return last == hipSuccess; }
+    std::string error() const { return msg; }
+    void set_stream(void* s) {
+        (void)hipSetDevice(device);
+        stream = s ? (hipStream_t)s : own;
+    }
+
+    void* alloc(size_t bytes) {
+        void* p = nullptr;
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) {
+            note(e, "hipMalloc");
+            return nullptr;
+        }
+        return p;
+    }
+    void free(void* p) {
+        if (p) note(hipFree(p), "hipFree");
+    }
+    void memset(void* p, int v, size_t bytes) { note(hipMemsetAsync(p, v, bytes, stream), "hipMemsetAsync"); }
+    void h2d(void* d, const void* h, size_t bytes) {
+        note(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream), "hipMemcpyAsync H2D");
+        sync();
+    }
+    void d2h(void* h, const void* d, size_t bytes) {
+        note(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync D2H");
+    }
+    void sync() { note(hipStreamSynchronize(stream), "hipStreamSynchronize"); }
+    void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height) {
+        note(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToDevice, stream),
+             "hipMemcpy2DAsync");
+    }
+
+    // ---- stage timing: events at stage boundaries, resolved lazily (no sync in the hot path) ----
+    static constexpr int kStages = 8;
+    bool prof = false;
+    std::vector<std::array<hipEvent_t, kStages + 1>> pending;
+    std::array<hipEvent_t, kStages + 1> cur{};
+    double acc[kStages] = {0};
+    int batches = 0;
+    std::vector<hipEvent_t> pool;
+    hipEvent_t ev_get() {
+        hipEvent_t e;
+        if (!pool.empty()) {
+            e = pool.back();
+            pool.pop_back();
+        } else {
+            note(hipEventCreate(&e), "hipEventCreate");
+        }
+        return e;
+    }
+    void profile(bool on) { prof = on; }
+    void mark(int id) {
+        if (!prof) return;
+        if (id == 0) cur.fill(nullptr);
+        cur[id] = ev_get();
+        note(hipEventRecord(cur[id], stream), "hipEventRecord");
+        if (id == kStages) pending.push_back(cur);
+    }
+    int profile_read(double* ms) {
+        sync();
+        for (auto& ev : pending) {
+            int prev = -1;
+            for (int s = 0; s <= kStages; ++s) {
+                if (!ev[s]) continue;
+                if (prev >= 0) {
+                    float t = 0.f;
+                    note(hipEventElapsedTime(&t, ev[prev], ev[s]), "hipEventElapsedTime");
+                    acc[prev] += t;
+                }
+                prev = s;
+            }
+            for (auto e : ev)
+                if (e) pool.push_back(e);
+            ++batches;
+        }
+        pending.clear();
+        for (int s = 0; s < kStages; ++s) {
+            ms[s] = acc[s];
+            acc[s] = 0;
+        }
+        int n = batches;
+        batches = 0;
+        return n;
+    }
+
+    template <class F>
+    static int launch_on(hipStream_t s, int nf, int64_t n, const F& f) {
+        if (n <= 0 || nf <= 0) return DOFS_OK;
+        int64_t gx = (n + kBlock - 1) / kBlock;
+        if (gx > 8192) gx = 8192;
+        hipLaunchKernelGGL(k_generic<F>, dim3((unsigned)gx, (unsigned)nf), dim3(kBlock), 0, s, f, n);
+        return hipGetLastError() == hipSuccess ? DOFS_OK : DOFS_ERR_DEVICE;
+    }
+    template <class F>
+    static int launch_static(void* s, int nf, int64_t n, const F& f) {
+        return launch_on((hipStream_t)s, nf, n, f);
+    }
+    template <class F>
+    void launch(int nf, int64_t n, const F& f) {
+        if (launch_on(stream, nf, n, f) != DOFS_OK) note(hipErrorLaunchFailure, "kernel launch");
+    }
+
+    void* temp(size_t bytes) {
+        if (bytes > tmp_bytes) {
+            sync();
+            if (tmp) (void)hipFree(tmp);
+            tmp = alloc(bytes);
+            tmp_bytes = tmp ? bytes : 0;
+        }
+        return tmp;
+    }
+    // exclusive prefix sum of each frame's segment [f*n, (f+1)*n)
+    void scan_excl(const int* in, int* out, int64_t n, int nf) {
+        for (int f = 0; f < nf; ++f) {
+            size_t bytes = 0;
+            note(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in + f * n, out + f * n, (int)n, stream), "scan size");
+            void* t = temp(bytes);
+            note(hipcub::DeviceScan::ExclusiveSum(t, bytes, in + f * n, out + f * n, (int)n, stream), "scan");
+        }
+    }
+    // stable LSD radix sort of (key, value) pairs by the 64-bit key, per frame
+    void sort_pairs(const unsigned long long* kin, unsigned long long* kout, const unsigned* vin, unsigned* vout,
+                    int64_t n, int nf) {
+        for (int f = 0; f < nf; ++f) {
+            size_t bytes = 0;
+            note(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kin + f * n, kout + f * n, vin + f * n, vout + f * n,
+                                                    (int)n, 0, 64, stream),
+                 "sort size");
+            void* t = temp(bytes);
+            note(hipcub::DeviceRadixSort::SortPairs(t, bytes, kin + f * n, kout + f * n, vin + f * n, vout + f * n,
+                                                    (int)n, 0, 64, stream),
+                 "sort");
+        }
+    }
+};
+
+}  // namespace dofs
+
+using DofsBackend = dofs::HipBackend;
+#include "dofs_cabi.inc.h"

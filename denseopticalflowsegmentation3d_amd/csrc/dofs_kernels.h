@@ -1,0 +1,980 @@
+// dofs_kernels.h — per-element bodies of every kernel of the pipeline.
+//
+// Each functor's operator()(f, i) handles element i of frame f. The HIP translation unit wraps them
+// in grid-stride __global__ launchers; the test-only host emulator loops over (f, i).
+//
+// Stages (reference → kernel):
+//   segment.cpp:52 GaussianBlur            KBlurRow, KBlurCol
+//   segment.cpp:20-32 diff + graph.cpp:51-103 build_graph (implicit: weights computed on the fly)
+//                                          KBoruvka* : minimum spanning tree under the strict order
+//                                          (weight, emission index) = Kruskal's order (multiset
+//                                          upper-bound insertion == stable sort)
+//   graph.cpp:519-531 Kruskal loop         KMst* + radix sort of the N-1 MST edges
+//                                          KDnc* : Kruskal reconstruction tree (KRT) by top-down
+//                                          divide and conquer over rank blocks
+//   graph.cpp:170-218 Forest::merge        KTree*, KJump, KOrd, KPathInit, KReplay: bottom-up replay
+//                                          of union-by-rank roots, ranks, float running means, bboxes
+//                                          along heavy paths of the KRT
+//   graph.cpp:272-356 Forest::new_merge    KFilter, KLift (get_score x3 classes), KSlot*, KSnapshot
+//   draw.cpp:118-147 overlay labels        KSeg*, KLabel
+#pragma once
+
+#include "dofs_common.h"
+#include "dofs_lift.h"
+
+namespace dofs {
+
+// Workspace: device pointers (frame-major; per-frame strides by size class) + constants.
+struct Ws {
+    Dims d;
+    // inputs
+    const F2* flow;
+    int64_t flow_fstride;  // F2 elements between frames of the input
+    // blur
+    F2* tmp;
+    F2* blur;
+    float bk[kMaxTaps];
+    int bn;
+    // Borůvka (per pixel, stride N)
+    int* comp;
+    unsigned long long* bw;
+    unsigned* bi;
+    int* uf;
+    int* mstbits;
+    int* cnt;
+    int* off;
+    // MST edges (stride M)
+    unsigned long long* key_in;
+    unsigned* val_in;
+    unsigned long long* key_out;
+    unsigned* val_out;
+    int* EU;
+    int* EV;
+    int* lu;
+    int* lv;
+    int* own;
+    int* MINR;
+    int* parentE;
+    int* childA;
+    int* childB;
+    // label / node space (stride NL)
+    int* stamp;
+    int* P;
+    int* CS;
+    int* MX;
+    I4* BBacc;
+    int* SZ;
+    I4* BB;
+    int* anc0;
+    int* acc0;
+    int* anc1;
+    int* acc1;
+    int* ord;
+    int* linfo;
+    int* isleaf;
+    int* lscan;
+    NodeVal* V;
+    int* ready;
+    // per pixel (stride N)
+    int* LP;
+    int* leaf_order;
+    int* paths;
+    int* cur;
+    int* sevent;
+    unsigned long long* sbest;
+    int* sflag;
+    int* soff;
+    int* labels;
+    // per edge (stride M)
+    int* cand;
+    double* cscore;
+    // segment tree (stride 2*P2)
+    int* seg;
+    // outputs (stride snap_cap)
+    dofs_snapshot* snaps;
+    dofs_box_record* recs;
+    int snap_cap;
+    // counters (stride kCounters)
+    int* ctr;
+    // parameters
+    LiftMats L;
+    int min_size;
+    double score_threshold;
+    double overlay_min_score;
+    double min_convexity[3];
+
+    DOFS_HD int* C(int f) const { return ctr + (int64_t)f * kCounters; }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Implicit 8-neighbour grid graph (graph.cpp:62-93): pixel p emits edge k∈{0:left, 1:up,
+// 2:up-left, 3:down-left}; emission index idx = 4p + k orders edges exactly like the reference's
+// sequential emission. start = p, end = neighbour.
+// ---------------------------------------------------------------------------------------------
+DOFS_HD inline bool edge_exists(const Dims& d, int x, int y, int k) {
+    switch (k) {
+        case 0: return x > 0;
+        case 1: return y > 0;
+        case 2: return d.nbr8 && x > 0 && y > 0;
+        default: return d.nbr8 && x > 0 && y < d.H - 1;
+    }
+}
+DOFS_HD inline int64_t edge_end(const Dims& d, int64_t p, int k) {
+    switch (k) {
+        case 0: return p - 1;
+        case 1: return p - d.W;
+        case 2: return p - d.W - 1;
+        default: return p + d.W - 1;
+    }
+}
+// diff (segment.cpp:20-32): float subtraction, double squares/sum/sqrt (correctly rounded).
+DOFS_HD inline double edge_weight(const F2* b, int64_t p, int64_t q) {
+    double dx = b[p].x - b[q].x;
+    double dy = b[p].y - b[q].y;
+    return sqrt(dx * dx + dy * dy);
+}
+DOFS_HD inline unsigned long long dbits(double w) {
+    union {
+        double d;
+        unsigned long long u;
+    } c;
+    c.d = w;
+    return c.u;
+}
+DOFS_HD inline double bitsd(unsigned long long u) {
+    union {
+        double d;
+        unsigned long long u;
+    } c;
+    c.u = u;
+    return c.d;
+}
+
+// cv::borderInterpolate(p, len, BORDER_REFLECT_101)
+DOFS_HD inline int reflect101(int p, int len) {
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        if (p < 0)
+            p = -p;
+        else
+            p = 2 * len - 2 - p;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1 — separable Gaussian blur (segment.cpp:52), OpenCV RowFilter then SymmColumnFilter order.
+// ---------------------------------------------------------------------------------------------
+struct KBlurRow {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t i) const {
+        const int W = w.d.W;
+        const int y = (int)(i / W), x = (int)(i % W);
+        const F2* row = w.flow + f * w.flow_fstride + (int64_t)y * W;
+        const int r = w.bn / 2;
+        F2 s0 = row[reflect101(x - r, W)];
+        float sx = w.bk[0] * s0.x, sy = w.bk[0] * s0.y;
+        for (int t = 1; t < w.bn; ++t) {
+            F2 v = row[reflect101(x - r + t, W)];
+            sx += w.bk[t] * v.x;
+            sy += w.bk[t] * v.y;
+        }
+        F2 o;
+        o.x = sx;
+        o.y = sy;
+        w.tmp[f * w.d.N + i] = o;
+    }
+};
+
+struct KBlurCol {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t i) const {
+        const int W = w.d.W, H = w.d.H;
+        const int y = (int)(i / W), x = (int)(i % W);
+        const F2* t = w.tmp + f * w.d.N;
+        const int r = w.bn / 2;
+        F2 c = t[i];
+        float sx = w.bk[r] * c.x + 0.0f, sy = w.bk[r] * c.y + 0.0f;
+        for (int j = 1; j <= r; ++j) {
+            F2 a = t[(int64_t)reflect101(y + j, H) * W + x];
+            F2 b = t[(int64_t)reflect101(y - j, H) * W + x];
+            sx += w.bk[r + j] * (a.x + b.x);
+            sy += w.bk[r + j] * (a.y + b.y);
+        }
+        F2 o;
+        o.x = sx;
+        o.y = sy;
+        w.blur[f * w.d.N + i] = o;
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Lock-free union-find on an int parent array (hook the larger root onto the smaller).
+// ---------------------------------------------------------------------------------------------
+DOFS_HD inline int uf_find(int* P, int x) {
+    for (;;) {
+        int p = dofs_ld(P + x);
+        if (p == x) return x;
+        int gp = dofs_ld(P + p);
+        if (gp == p) return p;
+        dofs_st(P + x, gp);  // path halving (x is not a root; P[x] only ever moves toward its root)
+        x = gp;
+    }
+}
+DOFS_HD inline void uf_union(int* P, int a, int b) {
+    for (;;) {
+        a = uf_find(P, a);
+        b = uf_find(P, b);
+        if (a == b) return;
+        if (a < b) {
+            int t = a;
+            a = b;
+            b = t;
+        }
+        if (dofs_cas(P + a, a, b) == a) return;
+    }
+}
+DOFS_HD inline int uf_root_ro(const int* P, int x) {  // read-only walk (no writer in this kernel)
+    int p = P[x];
+    while (p != x) {
+        x = p;
+        p = P[x];
+    }
+    return x;
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2 — Borůvka MST on the implicit grid graph, strict order (weight bits, idx).
+// ---------------------------------------------------------------------------------------------
+struct KBoruvkaInit {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t p) const {
+        const int64_t o = f * w.d.N + p;
+        w.comp[o] = (int)p;
+        w.uf[o] = (int)p;
+        w.mstbits[o] = 0;
+    }
+};
+
+struct KBoruvkaReset {  // round r: clear per-component minima
+    Ws w;
+    int r;
+    DOFS_HD void operator()(int f, int64_t c) const {
+        if (r > 0 && !w.C(f)[C_ACT + r - 1]) return;
+        const int64_t o = f * w.d.N + c;
+        w.bw[o] = ~0ull;
+        w.bi[o] = kNoEdge;
+    }
+};
+
+struct KBoruvkaMinW {
+    Ws w;
+    int r;
+    DOFS_HD void operator()(int f, int64_t p) const {
+        if (r > 0 && !w.C(f)[C_ACT + r - 1]) return;
+        const Dims& d = w.d;
+        const int x = (int)(p % d.W), y = (int)(p / d.W);
+        const int* comp = w.comp + f * d.N;
+        const F2* b = w.blur + f * d.N;
+        unsigned long long* bw = w.bw + f * d.N;
+        const int cp = comp[p];
+        bool any = false;
+        for (int k = 0; k < 4; ++k) {
+            if (!edge_exists(d, x, y, k)) continue;
+            const int64_t q = edge_end(d, p, k);
+            const int cq = comp[q];
+            if (cp == cq) continue;
+            const unsigned long long wb = dbits(edge_weight(b, p, q));
+            dofs_amin_u64(bw + cp, wb);
+            dofs_amin_u64(bw + cq, wb);
+            any = true;
+        }
+        if (any) w.C(f)[C_ACT + r] = 1;
+    }
+};
+
+struct KBoruvkaMinI {
+    Ws w;
+    int r;
+    DOFS_HD void operator()(int f, int64_t p) const {
+        if (!w.C(f)[C_ACT + r]) return;
+        const Dims& d = w.d;
+        const int x = (int)(p % d.W), y = (int)(p / d.W);
+        const int* comp = w.comp + f * d.N;
+        const F2* b = w.blur + f * d.N;
+        const unsigned long long* bw = w.bw + f * d.N;
+        unsigned* bi = w.bi + f * d.N;
+        const int cp = comp[p];
+        for (int k = 0; k < 4; ++k) {
+            if (!edge_exists(d, x, y, k)) continue;
+            const int64_t q = edge_end(d, p, k);
+            const int cq = comp[q];
+            if (cp == cq) continue;
+            const unsigned long long wb = dbits(edge_weight(b, p, q));
+            const unsigned idx = (unsigned)(4 * p + k);
+            if (wb == bw[cp]) dofs_amin_u32(bi + cp, idx);
+            if (wb == bw[cq]) dofs_amin_u32(bi + cq, idx);
+        }
+    }
+};
+
+struct KBoruvkaHook {  // every component root hooks along its minimum edge
+    Ws w;
+    int r;
+    DOFS_HD void operator()(int f, int64_t c) const {
+        if (!w.C(f)[C_ACT + r]) return;
+        const Dims& d = w.d;
+        const int* comp = w.comp + f * d.N;
+        if (comp[c] != (int)c) return;
+        const unsigned idx = w.bi[f * d.N + c];
+        if (idx == kNoEdge) return;
+        const int64_t p = idx >> 2;
+        const int k = idx & 3;
+        const int64_t q = edge_end(d, p, k);
+        dofs_aor(w.mstbits + f * d.N + p, 1 << k);
+        uf_union(w.uf + f * d.N, comp[p], comp[q]);
+    }
+};
+
+struct KBoruvkaCompress {  // uf[c] = root
+    Ws w;
+    int r;
+    DOFS_HD void operator()(int f, int64_t c) const {
+        if (!w.C(f)[C_ACT + r]) return;
+        int* uf = w.uf + f * w.d.N;
+        int x = (int)c;
+        int p = uf[x];
+        if (p == x) return;
+        while (true) {
+            int gp = uf[p];
+            if (gp == p) break;
+            p = gp;
+        }
+        uf[c] = p;
+    }
+};
+
+struct KBoruvkaRelabel {
+    Ws w;
+    int r;
+    DOFS_HD void operator()(int f, int64_t p) const {
+        if (!w.C(f)[C_ACT + r]) return;
+        int* comp = w.comp + f * w.d.N;
+        comp[p] = w.uf[f * w.d.N + comp[p]];
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// MST edge list in emission order, then (after the radix sort) in Kruskal order.
+// ---------------------------------------------------------------------------------------------
+struct KMstCount {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t p) const {
+        w.cnt[f * w.d.N + p] = __builtin_popcount((unsigned)w.mstbits[f * w.d.N + p]);
+    }
+};
+
+struct KMstEmit {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t p) const {
+        const Dims& d = w.d;
+        const int bits = w.mstbits[f * d.N + p];
+        if (!bits) return;
+        int64_t j = w.off[f * d.N + p];
+        const F2* b = w.blur + f * d.N;
+        for (int k = 0; k < 4; ++k) {
+            if (!(bits & (1 << k))) continue;
+            if (j < d.M) {
+                w.key_in[f * d.M + j] = dbits(edge_weight(b, p, edge_end(d, p, k)));
+                w.val_in[f * d.M + j] = (unsigned)(4 * p + k);
+            }
+            ++j;
+        }
+        if (p == d.N - 1) w.C(f)[C_MST] = (int)j;
+    }
+};
+
+struct KEdgeInit {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t i) const {
+        const Dims& d = w.d;
+        const int64_t o = f * d.M + i;
+        const unsigned idx = w.val_out[o];
+        const int64_t p = idx >> 2;
+        const int64_t q = edge_end(d, p, idx & 3);
+        w.EU[o] = (int)p;
+        w.EV[o] = (int)q;
+        w.lu[o] = (int)p;
+        w.lv[o] = (int)q;
+        w.MINR[o] = kIntMax;
+        w.parentE[o] = -1;
+        w.childA[o] = -1;
+        w.childB[o] = -1;
+        w.own[o] = 0;
+    }
+};
+
+struct KLabelInit {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t x) const {
+        const Dims& d = w.d;
+        const int64_t o = f * d.NL + x;
+        w.stamp[o] = -1;
+        if (x < d.N) {
+            const int px = (int)(x % d.W), py = (int)(x / d.W);
+            w.SZ[o] = 1;
+            I4 b;
+            b.x0 = px;
+            b.y0 = py;
+            b.x1 = px;
+            b.y1 = py;
+            w.BB[o] = b;
+            w.LP[f * d.N + x] = kIntMax;
+        } else if (x == d.NL - 1) {  // KRT root = last merge: the whole frame
+            w.SZ[o] = (int)d.N;
+            I4 b;
+            b.x0 = 0;
+            b.y0 = 0;
+            b.x1 = d.W - 1;
+            b.y1 = d.H - 1;
+            w.BB[o] = b;
+        }
+    }
+};
+
+// Leaf parent of pixel v = its smallest-rank incident MST edge; side bit = v is Edge::end.
+struct KLeafParent {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t i) const {
+        const int64_t o = f * w.d.M + i;
+        int* LP = w.LP + f * w.d.N;
+        dofs_amin(LP + w.EU[o], (int)(2 * i));
+        dofs_amin(LP + w.EV[o], (int)(2 * i + 1));
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// K3 — KRT by top-down divide and conquer over rank blocks. At depth d with
+// block size S: L = first S/2 ranks of a block, R = the rest. Labels of every edge endpoint are the
+// components at the start of its block (pixel id, or N + max edge rank of the component). The
+// L-edges of all blocks form a forest over a collision-free label space; its components get the
+// label N + (max L rank) and every L-root's KRT parent is the smallest-rank R edge touching it.
+// ---------------------------------------------------------------------------------------------
+DOFS_HD inline bool dnc_is_L(const Dims& d, int64_t i, int64_t S) {
+    const int64_t h = S >> 1;
+    const int64_t s = i & ~(S - 1);
+    return (i - s) < h && (s + h) < d.M;  // L edge of a block whose R half is non-empty
+}
+DOFS_HD inline bool dnc_is_R(int64_t i, int64_t S) { return (i & (S - 1)) >= (S >> 1); }
+
+struct KDncTouch {
+    Ws w;
+    int64_t S;
+    int depth;
+    DOFS_HD void operator()(int f, int64_t i) const {
+        const Dims& d = w.d;
+        if (!dnc_is_L(d, i, S)) return;
+        const int64_t o = f * d.M + i;
+        const int64_t lb = f * d.NL;
+        int own = 0;
+        for (int side = 0; side < 2; ++side) {
+            const int x = side ? w.lv[o] : w.lu[o];
+            if (dofs_exch(w.stamp + lb + x, depth) != depth) {
+                own |= 1 << side;
+                w.P[lb + x] = x;
+                w.CS[lb + x] = 0;
+                w.MX[lb + x] = -1;
+                I4 b;
+                b.x0 = kIntMax;
+                b.y0 = kIntMax;
+                b.x1 = -1;
+                b.y1 = -1;
+                w.BBacc[lb + x] = b;
+            }
+        }
+        w.own[o] = own;
+    }
+};
+
+struct KDncUnion {
+    Ws w;
+    int64_t S;
+    DOFS_HD void operator()(int f, int64_t i) const {
+        const Dims& d = w.d;
+        if (!dnc_is_L(d, i, S)) return;
+        const int64_t o = f * d.M + i;
+        uf_union(w.P + f * d.NL, w.lu[o], w.lv[o]);
+    }
+};
+
+struct KDncCompress {
+    Ws w;
+    int64_t S;
+    DOFS_HD void operator()(int f, int64_t i) const {
+        const Dims& d = w.d;
+        if (!dnc_is_L(d, i, S)) return;
+        const int64_t o = f * d.M + i;
+        const int64_t lb = f * d.NL;
+        int* P = w.P + lb;
+        const int own = w.own[o];
+        int ri = -1;
+        for (int side = 0; side < 2; ++side) {
+            const int x = side ? w.lv[o] : w.lu[o];
+            int r = x;
+            for (;;) {  // no union runs in this kernel: plain walk, others only shorten paths
+                int p = dofs_ld(P + r);
+                if (p == r) break;
+                r = p;
+            }
+            if (side == 0) ri = r;
+            if (own & (1 << side)) {
+                dofs_st(P + x, r);
+                dofs_aadd(w.CS + lb + r, w.SZ[lb + x]);
+                const I4 b = w.BB[lb + x];
+                I4* acc = w.BBacc + lb + r;
+                dofs_amin(&acc->x0, b.x0);
+                dofs_amin(&acc->y0, b.y0);
+                dofs_amax(&acc->x1, b.x1);
+                dofs_amax(&acc->y1, b.y1);
+            }
+        }
+        dofs_amax(w.MX + lb + ri, (int)i);
+    }
+};
+
+struct KDncLRoot {
+    Ws w;
+    int64_t S;
+    DOFS_HD void operator()(int f, int64_t i) const {
+        const Dims& d = w.d;
+        if (!dnc_is_L(d, i, S)) return;
+        const int64_t o = f * d.M + i;
+        const int64_t lb = f * d.NL;
+        const int r = w.P[lb + w.lu[o]];
+        if (w.MX[lb + r] != (int)i) return;
+        w.SZ[lb + d.N + i] = w.CS[lb + r];
+        w.BB[lb + d.N + i] = w.BBacc[lb + r];
+    }
+};
+
+struct KDncRelabelR {
+    Ws w;
+    int64_t S;
+    int depth;
+    DOFS_HD void operator()(int f, int64_t j) const {
+        const Dims& d = w.d;
+        if (!dnc_is_R(j, S)) return;
+        const int64_t o = f * d.M + j;
+        const int64_t lb = f * d.NL;
+        for (int side = 0; side < 2; ++side) {
+            int* lp = side ? (w.lv + o) : (w.lu + o);
+            const int x = *lp;
+            if (w.stamp[lb + x] != depth) continue;
+            const int li = w.MX[lb + w.P[lb + x]];
+            *lp = (int)(d.N + li);
+            dofs_amin(w.MINR + f * d.M + li, (int)(2 * j + side));
+        }
+    }
+};
+
+struct KDncParent {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t i) const {
+        const Dims& d = w.d;
+        const int64_t o = f * d.M + i;
+        const int c = w.MINR[o];
+        if (c == kIntMax) return;
+        const int p = c >> 1;
+        w.parentE[o] = p;
+        if (c & 1)
+            w.childB[f * d.M + p] = (int)(d.N + i);
+        else
+            w.childA[f * d.M + p] = (int)(d.N + i);
+    }
+};
+
+struct KLeafChild {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t v) const {
+        const Dims& d = w.d;
+        const int c = w.LP[f * d.N + v];
+        if (c == kIntMax) return;
+        const int p = c >> 1;
+        if (c & 1)
+            w.childB[f * d.M + p] = (int)v;
+        else
+            w.childA[f * d.M + p] = (int)v;
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// K4 — heavy-first preorder of the KRT (every heavy path becomes a contiguous range) via
+// pointer jumping over parent links with accumulated offsets.
+// ---------------------------------------------------------------------------------------------
+DOFS_HD inline int node_parent(const Ws& w, int f, int64_t x) {
+    const Dims& d = w.d;
+    if (x < d.N) {
+        const int c = w.LP[f * d.N + x];
+        return c == kIntMax ? -1 : (int)(d.N + (c >> 1));
+    }
+    const int p = w.parentE[f * d.M + (x - d.N)];
+    return p < 0 ? -1 : (int)(d.N + p);
+}
+// heavy child of internal node y (larger subtree; ties → start side A)
+DOFS_HD inline int heavy_child(const Ws& w, int f, int y, int* light, int* light_is_B) {
+    const Dims& d = w.d;
+    const int64_t e = f * d.M + (y - d.N);
+    const int a = w.childA[e], b = w.childB[e];
+    const int sa = w.SZ[f * d.NL + a], sb = w.SZ[f * d.NL + b];
+    if (sa >= sb) {
+        *light = b;
+        *light_is_B = 1;
+        return a;
+    }
+    *light = a;
+    *light_is_B = 0;
+    return b;
+}
+
+struct KTreeInit {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t x) const {
+        const Dims& d = w.d;
+        const int64_t o = f * d.NL + x;
+        const int p = node_parent(w, f, x);
+        int off = 0;
+        if (p >= 0) {
+            int lt, lb;
+            const int h = heavy_child(w, f, p, &lt, &lb);
+            off = (h == (int)x) ? 1 : 1 + (2 * w.SZ[f * d.NL + h] - 1);
+        }
+        w.anc0[o] = p;
+        w.acc0[o] = off;
+    }
+};
+
+struct KJump {
+    const int* anc_in;
+    const int* acc_in;
+    int* anc_out;
+    int* acc_out;
+    int64_t NL;
+    DOFS_HD void operator()(int f, int64_t x) const {
+        const int64_t o = f * NL + x;
+        const int a = anc_in[o];
+        if (a < 0) {
+            anc_out[o] = -1;
+            acc_out[o] = acc_in[o];
+            return;
+        }
+        anc_out[o] = anc_in[f * NL + a];
+        acc_out[o] = acc_in[o] + acc_in[f * NL + a];
+    }
+};
+
+struct KOrd {
+    Ws w;
+    const int* pre;
+    DOFS_HD void operator()(int f, int64_t x) const {
+        const Dims& d = w.d;
+        const int q = pre[f * d.NL + x];
+        w.ord[f * d.NL + q] = (int)x;
+        w.isleaf[f * d.NL + q] = x < d.N ? 1 : 0;
+    }
+};
+
+struct KLeafOrder {
+    Ws w;
+    const int* pre;
+    DOFS_HD void operator()(int f, int64_t v) const {
+        const Dims& d = w.d;
+        const int lp = w.lscan[f * d.NL + pre[f * d.NL + v]];
+        w.leaf_order[f * d.N + lp] = (int)v;
+    }
+};
+
+constexpr int kLinfoId = (1 << 29) - 1;
+constexpr int kLinfoB = 1 << 29;
+constexpr int kLinfoTop = 1 << 30;
+
+struct KPathInit {
+    Ws w;
+    const int* pre;
+    DOFS_HD void operator()(int f, int64_t x) const {
+        const Dims& d = w.d;
+        const int64_t lb = f * d.NL;
+        const int q = pre[lb + x];
+        const int p = node_parent(w, f, x);
+        bool top = true;
+        if (p >= 0) {
+            int lt, lB;
+            top = heavy_child(w, f, p, &lt, &lB) != (int)x;
+        }
+        if (x >= d.N) {
+            int lt, lB;
+            heavy_child(w, f, (int)x, &lt, &lB);
+            w.linfo[lb + q] = lt | (lB ? kLinfoB : 0) | (top ? kLinfoTop : 0);
+            w.ready[lb + x] = kIntMax;
+        } else {
+            const F2 v = w.blur[f * d.N + x];
+            NodeVal nv;
+            nv.mx = v.x;
+            nv.my = v.y;
+            nv.size = 1;
+            nv.root = (int)x;
+            nv.x0 = nv.x1 = (int16_t)(x % d.W);
+            nv.y0 = nv.y1 = (int16_t)(x / d.W);
+            nv.rank = 0;
+            nv.pad = 0;
+            w.V[lb + x] = nv;
+            w.ready[lb + x] = -1;
+            w.linfo[lb + q] = kLinfoTop;
+            if (!top) {  // heavy leaf = bottom of a heavy path
+                const int j = dofs_aadd(w.C(f) + C_PATHS, 1);
+                w.paths[f * d.N + j] = (int)x;
+                w.cur[f * d.N + j] = q - 1;
+            }
+        }
+    }
+};
+
+// Forest::merge (graph.cpp:170-218) on KRT values: A = start side, B = end side.
+DOFS_HD inline NodeVal merge_vals(const NodeVal& A, const NodeVal& B) {
+    NodeVal r;
+    r.size = A.size + B.size;
+    r.root = (A.rank > B.rank) ? A.root : B.root;
+    r.rank = (A.rank == B.rank) ? A.rank + 1 : (A.rank > B.rank ? A.rank : B.rank);
+    const float wax = A.mx * (float)A.size, way = A.my * (float)A.size;
+    const float wbx = B.mx * (float)B.size, wby = B.my * (float)B.size;
+    const double ia = 1. / (double)(A.size + B.size);
+    r.mx = (float)((double)(wax + wbx) * ia);
+    r.my = (float)((double)(way + wby) * ia);
+    r.x0 = A.x0 < B.x0 ? A.x0 : B.x0;
+    r.y0 = A.y0 < B.y0 ? A.y0 : B.y0;
+    r.x1 = A.x1 > B.x1 ? A.x1 : B.x1;
+    r.y1 = A.y1 > B.y1 ? A.y1 : B.y1;
+    r.pad = 0;
+    return r;
+}
+
+// K5 — sequential replay along one heavy path (bottom-up), round `round`: advances until a light
+// child not completed in an earlier round is met (resumed next round) or the path top is done.
+struct KReplay {
+    Ws w;
+    int round;
+    DOFS_HD void operator()(int f, int64_t j) const {
+        const Dims& d = w.d;
+        if (j >= w.C(f)[C_PATHS]) return;
+        int* curp = w.cur + f * d.N + j;
+        int q = *curp;
+        if (q < 0) return;
+        const int64_t lb = f * d.NL;
+        NodeVal run = w.V[lb + w.ord[lb + q + 1]];
+        for (;;) {
+            const int x = w.ord[lb + q];
+            const int info = w.linfo[lb + q];
+            const int lt = info & kLinfoId;
+            if (w.ready[lb + lt] >= round) {
+                *curp = q;
+                return;
+            }
+            const NodeVal lv = w.V[lb + lt];
+            run = (info & kLinfoB) ? merge_vals(run, lv) : merge_vals(lv, run);
+            w.V[lb + x] = run;
+            if (info & kLinfoTop) {
+                w.ready[lb + x] = round;
+                *curp = -1;
+                return;
+            }
+            --q;
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// K6 — new_merge filters + lifting (graph.cpp:280-356) and the per-slot arg-max.
+// ---------------------------------------------------------------------------------------------
+DOFS_HD inline double vec_norm(float x, float y) {  // cv::norm(Vec2f)
+    double s = 0.0;
+    s += (double)x * (double)x;
+    s += (double)y * (double)y;
+    return sqrt(s);
+}
+
+struct KFilter {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t i) const {
+        const Dims& d = w.d;
+        const NodeVal v = w.V[f * d.NL + d.N + i];
+        if (v.size < w.min_size) return;
+        const int y = v.root / d.W;
+        if (y < d.H / 10) return;
+        const double move = vec_norm(v.mx, v.my);
+        if (move < 3 * (y + 1) / (double)d.H) return;
+        const int k = dofs_aadd(w.C(f) + C_CAND, 1);
+        w.cand[f * d.M + k] = (int)i;
+    }
+};
+
+DOFS_HD inline double event_score(const Ws& w, const NodeVal& v, int* cls, dofs_solution* best) {
+    const int box[4] = {v.x0, v.y0, v.x1, v.y1};
+    return score_event(mk(v.mx, v.my), box, w.L, cls, best);
+}
+
+struct KLift {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t j) const {
+        const Dims& d = w.d;
+        if (j >= w.C(f)[C_CAND]) return;
+        const int i = w.cand[f * d.M + j];
+        const NodeVal v = w.V[f * d.NL + d.N + i];
+        double* cs = w.cscore + f * d.M + j;
+        *cs = -1.0;
+        const double rect_area = (double)((v.x1 - v.x0 + 1) * (v.y1 - v.y0 + 1));
+        const double convexity = v.size / rect_area;
+        int cls;
+        const double score = event_score(w, v, &cls, nullptr);
+        if (score == -1) return;
+        dofs_aadd(w.C(f) + C_SCORED, 1);
+        const double minc = w.min_convexity[cls];
+        if (convexity < minc) return;
+        if (!(score > w.score_threshold)) return;
+        dofs_aadd(w.C(f) + C_QUAL, 1);
+        *cs = score;
+        dofs_amax_u64(w.sbest + f * d.N + v.root, dbits(score));
+    }
+};
+
+struct KSlotInit {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t s) const {
+        w.sbest[f * w.d.N + s] = 0ull;
+        w.sevent[f * w.d.N + s] = kIntMax;
+    }
+};
+
+struct KSlotEvent {  // first event reaching the slot's maximum wins (strict '<' update, graph.cpp:352)
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t j) const {
+        const Dims& d = w.d;
+        if (j >= w.C(f)[C_CAND]) return;
+        const double s = w.cscore[f * d.M + j];
+        if (!(s > w.score_threshold)) return;
+        const int i = w.cand[f * d.M + j];
+        const int root = w.V[f * d.NL + d.N + i].root;
+        if (dbits(s) == w.sbest[f * d.N + root]) dofs_amin(w.sevent + f * d.N + root, i);
+    }
+};
+
+struct KSlotFlag {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t s) const {
+        w.sflag[f * w.d.N + s] = w.sevent[f * w.d.N + s] != kIntMax ? 1 : 0;
+    }
+};
+
+struct KSnapshot {
+    Ws w;
+    const int* pre;
+    DOFS_HD void operator()(int f, int64_t s) const {
+        const Dims& d = w.d;
+        const int i = w.sevent[f * d.N + s];
+        if (i == kIntMax) return;
+        const int k = w.soff[f * d.N + s];
+        if (k >= w.snap_cap) return;
+        const NodeVal v = w.V[f * d.NL + d.N + i];
+        dofs_snapshot sn;
+        int cls;
+        sn.score = event_score(w, v, &cls, &sn.sol);
+        sn.slot = (int)s;
+        sn.event = i;
+        sn.size = v.size;
+        sn.seg_begin = w.lscan[f * d.NL + pre[f * d.NL + d.N + i]];
+        sn.bbox[0] = v.x0;
+        sn.bbox[1] = v.y0;
+        sn.bbox[2] = v.x1;
+        sn.bbox[3] = v.y1;
+        sn.move = vec_norm(v.mx, v.my);
+        w.snaps[(int64_t)f * w.snap_cap + k] = sn;
+        dofs_box_record rec;
+        rec.frame = f;
+        rec.slot = (int)s;
+        rec.cls = sn.sol.cls;
+        rec.size = v.size;
+        rec.score = (float)sn.score;
+        rec.move = (float)sn.move;
+        for (int t = 0; t < 4; ++t) {
+            rec.lower_face[t][0] = sn.sol.lower_face[t][0];
+            rec.lower_face[t][1] = sn.sol.lower_face[t][1];
+            rec.upper_face[t][0] = sn.sol.upper_face[t][0];
+            rec.upper_face[t][1] = sn.sol.upper_face[t][1];
+        }
+        w.recs[(int64_t)f * w.snap_cap + k] = rec;
+    }
+};
+
+struct KSnapCount {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t) const {
+        const Dims& d = w.d;
+        const int64_t last = f * d.N + d.N - 1;
+        w.C(f)[C_SNAP] = w.soff[last] + w.sflag[last];
+    }
+};
+
+struct KSingle {  // H*W == 1: one leaf, no merge (segment_graph performs no union)
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t) const {
+        w.leaf_order[f * w.d.N] = 0;
+        w.labels[f * w.d.N] = -1;
+        w.C(f)[C_SNAP] = 0;
+        w.recs[(int64_t)f * w.snap_cap].slot = -1;
+    }
+};
+
+struct KRecClear {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t k) const { w.recs[(int64_t)f * w.snap_cap + k].slot = -1; }
+};
+
+// ---------------------------------------------------------------------------------------------
+// K7 — overlay labels (draw.cpp:118-147): max slot over painting snapshots containing the pixel,
+// via a segment tree over leaf-order positions (snapshot = contiguous leaf range).
+// ---------------------------------------------------------------------------------------------
+struct KSegInit {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t t) const { w.seg[f * 2 * w.d.P2 + t] = -1; }
+};
+
+struct KPaint {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t k) const {
+        const Dims& d = w.d;
+        const int n = w.C(f)[C_SNAP];
+        if (k >= n || k >= w.snap_cap) return;
+        const dofs_snapshot& sn = w.snaps[(int64_t)f * w.snap_cap + k];
+        if (!(sn.score > w.overlay_min_score)) return;
+        int* seg = w.seg + f * 2 * d.P2;
+        int64_t l = sn.seg_begin + d.P2, r = (int64_t)sn.seg_begin + sn.size + d.P2;
+        while (l < r) {
+            if (l & 1) dofs_amax(seg + l++, sn.slot);
+            if (r & 1) dofs_amax(seg + --r, sn.slot);
+            l >>= 1;
+            r >>= 1;
+        }
+    }
+};
+
+struct KLabel {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t q) const {
+        const Dims& d = w.d;
+        const int* seg = w.seg + f * 2 * d.P2;
+        int lab = -1;
+        for (int64_t t = q + d.P2; t >= 1; t >>= 1) lab = seg[t] > lab ? seg[t] : lab;
+        w.labels[f * d.N + w.leaf_order[f * d.N + q]] = lab;
+    }
+};
+
+}  // namespace dofs

@@ -1,0 +1,276 @@
+// dofs_pipeline.h — orchestration of one batch of frames through the kernels of dofs_kernels.h.
+// Templated on the execution backend: dofs_hip.hip instantiates it with the HIP backend (the
+// product); tests/emu instantiates it with a sequential host backend to model the algorithm.
+#pragma once
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "dofs_kernels.h"
+
+namespace dofs {
+
+inline int ceil_log2(int64_t n) {
+    int k = 0;
+    while (((int64_t)1 << k) < n) ++k;
+    return k;
+}
+
+// OpenCV 4.x getGaussianKernel (bit-exact variant: double arithmetic, float result) for float input:
+// ksize = cvRound(sigma*4*2+1)|1 (segment.cpp:52 → cv::GaussianBlur(..., Size(0,0), 3.0)).
+inline int gaussian_taps(double sigma, float* k) {
+    int n = ((int)nearbyint(sigma * 4 * 2 + 1)) | 1;
+    if (n > kMaxTaps - 1) n = (kMaxTaps - 1) | 1;
+    std::vector<double> v((size_t)(n / 2 + 1));
+    const double sx = sigma > 0 ? sigma : n * 0.15 + 0.35;
+    const double scale2X = (-0.5 * 0.25) / (sx * sx);
+    const int n2 = (n - 1) / 2;
+    double sum = 0;
+    for (int i = 0, x = 1 - n; i < n2; ++i, x += 2) {
+        v[i] = exp((double)(x * x) * scale2X);
+        sum += v[i];
+    }
+    sum = sum * 2 + 1;
+    const double mul1 = 1.0 / sum;
+    double sum2 = 0;
+    for (int i = 0; i < n2; ++i) {
+        v[i] *= mul1;
+        sum2 += v[i];
+    }
+    v[n2] = 1.0 - sum2 * 2;
+    for (int i = 0; i <= n2; ++i) k[i] = k[n - 1 - i] = (float)v[i];
+    return n;
+}
+
+template <class Backend>
+struct Pipeline {
+    Backend& be;
+    Ws w;
+    void* base = nullptr;
+    size_t base_bytes = 0;
+    Dims cap{};  // allocated shape
+    int* pre = nullptr;
+    int64_t snap_cap = 4096;
+
+    explicit Pipeline(Backend& b) : be(b) { memset(&w, 0, sizeof(w)); }
+    ~Pipeline() {
+        if (base) be.free(base);
+    }
+
+    static Dims dims_for(int B, int H, int W, int nbr8) {
+        Dims d;
+        d.H = H;
+        d.W = W;
+        d.N = (int64_t)H * W;
+        d.M = d.N - 1;
+        d.NL = d.N + d.M;
+        d.P2 = 1;
+        while (d.P2 < d.N) d.P2 <<= 1;
+        d.B = B;
+        d.nbr8 = nbr8;
+        return d;
+    }
+
+    // Carve every buffer from one allocation (grow-only). Returns false on allocation failure.
+    bool reserve(const Dims& d) {
+        const bool fits = base && cap.B >= d.B && cap.N == d.N && cap.W == d.W;
+        if (!fits) {
+            if (base) be.free(base);
+            base = nullptr;
+            size_t bytes = layout(d, nullptr);
+            base = be.alloc(bytes);
+            if (!base) return false;
+            base_bytes = bytes;
+            cap = d;
+            layout(d, (char*)base);
+        }
+        w.d = d;
+        return true;
+    }
+
+    size_t layout(const Dims& d, char* p) {
+        size_t off = 0;
+        auto take = [&](size_t bytes) {
+            off = (off + 255) & ~(size_t)255;
+            char* r = p ? p + off : nullptr;
+            off += bytes;
+            return r;
+        };
+        const int64_t B = d.B, N = d.N, M = std::max<int64_t>(d.M, 1), NL = d.NL;
+        w.tmp = (F2*)take(sizeof(F2) * B * N);
+        w.blur = (F2*)take(sizeof(F2) * B * N);
+        w.comp = (int*)take(4 * B * N);
+        w.bw = (unsigned long long*)take(8 * B * N);
+        w.bi = (unsigned*)take(4 * B * N);
+        w.uf = (int*)take(4 * B * N);
+        w.mstbits = (int*)take(4 * B * N);
+        w.cnt = (int*)take(4 * B * N);
+        w.off = (int*)take(4 * B * N);
+        w.key_in = (unsigned long long*)take(8 * B * M);
+        w.val_in = (unsigned*)take(4 * B * M);
+        w.key_out = (unsigned long long*)take(8 * B * M);
+        w.val_out = (unsigned*)take(4 * B * M);
+        w.EU = (int*)take(4 * B * M);
+        w.EV = (int*)take(4 * B * M);
+        w.lu = (int*)take(4 * B * M);
+        w.lv = (int*)take(4 * B * M);
+        w.own = (int*)take(4 * B * M);
+        w.MINR = (int*)take(4 * B * M);
+        w.parentE = (int*)take(4 * B * M);
+        w.childA = (int*)take(4 * B * M);
+        w.childB = (int*)take(4 * B * M);
+        w.stamp = (int*)take(4 * B * NL);
+        w.P = (int*)take(4 * B * NL);
+        w.CS = (int*)take(4 * B * NL);
+        w.MX = (int*)take(4 * B * NL);
+        w.BBacc = (I4*)take(sizeof(I4) * B * NL);
+        w.SZ = (int*)take(4 * B * NL);
+        w.BB = (I4*)take(sizeof(I4) * B * NL);
+        w.anc0 = (int*)take(4 * B * NL);
+        w.acc0 = (int*)take(4 * B * NL);
+        w.anc1 = (int*)take(4 * B * NL);
+        w.acc1 = (int*)take(4 * B * NL);
+        w.ord = (int*)take(4 * B * NL);
+        w.linfo = (int*)take(4 * B * NL);
+        w.isleaf = (int*)take(4 * B * NL);
+        w.lscan = (int*)take(4 * B * NL);
+        w.V = (NodeVal*)take(sizeof(NodeVal) * B * NL);
+        w.ready = (int*)take(4 * B * NL);
+        w.LP = (int*)take(4 * B * N);
+        w.leaf_order = (int*)take(4 * B * N);
+        w.paths = (int*)take(4 * B * N);
+        w.cur = (int*)take(4 * B * N);
+        w.sevent = (int*)take(4 * B * N);
+        w.sbest = (unsigned long long*)take(8 * B * N);
+        w.sflag = (int*)take(4 * B * N);
+        w.soff = (int*)take(4 * B * N);
+        w.labels = (int*)take(4 * B * N);
+        w.cand = (int*)take(4 * B * M);
+        w.cscore = (double*)take(8 * B * M);
+        w.seg = (int*)take(4 * B * 2 * d.P2);
+        w.snaps = (dofs_snapshot*)take(sizeof(dofs_snapshot) * B * snap_cap);
+        w.recs = (dofs_box_record*)take(sizeof(dofs_box_record) * B * snap_cap);
+        w.ctr = (int*)take(4 * B * kCounters);
+        w.snap_cap = (int)snap_cap;
+        return off + 256;
+    }
+
+    void set_params(const dofs_params& prm, const float persp[9], const float inv[9], const float inv_upper[27]) {
+        w.bn = gaussian_taps(prm.blur_sigma, w.bk);
+        memcpy(w.L.persp, persp, sizeof(w.L.persp));
+        memcpy(w.L.inv, inv, sizeof(w.L.inv));
+        memcpy(w.L.inv_upper, inv_upper, sizeof(w.L.inv_upper));
+        for (int c = 0; c < 3; ++c) {
+            w.L.obj_size[c][0] = prm.obj_size[c][0];
+            w.L.obj_size[c][1] = prm.obj_size[c][1];
+            w.min_convexity[c] = prm.min_convexity[c];
+        }
+        w.min_size = prm.min_size;
+        w.score_threshold = prm.score_threshold;
+        w.overlay_min_score = prm.overlay_min_score;
+    }
+
+    // Run the whole path on B frames of device-resident flow (frame stride fstride F2 elements).
+    void run(const F2* flow, int64_t fstride) {
+        const Dims& d = w.d;
+        const int B = d.B;
+        const int64_t N = d.N, M = d.M, NL = d.NL;
+        w.flow = flow;
+        w.flow_fstride = fstride;
+        be.memset(w.ctr, 0, sizeof(int) * (size_t)B * kCounters);
+
+        be.mark(0);
+        // K1 blur (segment.cpp:52)
+        be.launch(B, N, KBlurRow{w});
+        be.launch(B, N, KBlurCol{w});
+        if (M <= 0) {  // single pixel: no edge, no merge
+            be.launch(B, N, KLabelInit{w});
+            be.launch(B, 1, KSingle{w});
+            pre = nullptr;
+            be.mark(8);
+            return;
+        }
+
+        be.mark(1);
+        // K2 Borůvka MST under (weight, emission index)
+        be.launch(B, N, KBoruvkaInit{w});
+        const int R = std::min(ceil_log2(N) + 2, kRoundsMax - 1);
+        for (int r = 0; r < R; ++r) {
+            be.launch(B, N, KBoruvkaReset{w, r});
+            be.launch(B, N, KBoruvkaMinW{w, r});
+            be.launch(B, N, KBoruvkaMinI{w, r});
+            be.launch(B, N, KBoruvkaHook{w, r});
+            be.launch(B, N, KBoruvkaCompress{w, r});
+            be.launch(B, N, KBoruvkaRelabel{w, r});
+        }
+        be.mark(2);
+        be.launch(B, N, KMstCount{w});
+        be.scan_excl(w.cnt, w.off, N, B);
+        be.launch(B, N, KMstEmit{w});
+        be.sort_pairs(w.key_in, w.key_out, w.val_in, w.val_out, M, B);  // Kruskal order
+
+        be.mark(3);
+        // K3 Kruskal reconstruction tree
+        be.launch(B, M, KEdgeInit{w});
+        be.launch(B, NL, KLabelInit{w});
+        be.launch(B, M, KLeafParent{w});
+        int depth = 0;
+        for (int64_t S = (int64_t)1 << ceil_log2(M); S >= 2; S >>= 1, ++depth) {
+            be.launch(B, M, KDncTouch{w, S, depth});
+            be.launch(B, M, KDncUnion{w, S});
+            be.launch(B, M, KDncCompress{w, S});
+            be.launch(B, M, KDncLRoot{w, S});
+            be.launch(B, M, KDncRelabelR{w, S, depth});
+        }
+        be.launch(B, M, KDncParent{w});
+        be.launch(B, N, KLeafChild{w});
+
+        be.mark(4);
+        // K4 heavy-first preorder (pointer jumping)
+        be.launch(B, NL, KTreeInit{w});
+        int* anc_a = w.anc0;
+        int* acc_a = w.acc0;
+        int* anc_b = w.anc1;
+        int* acc_b = w.acc1;
+        const int J = ceil_log2(NL) + 1;
+        for (int t = 0; t < J; ++t) {
+            be.launch(B, NL, KJump{anc_a, acc_a, anc_b, acc_b, NL});
+            std::swap(anc_a, anc_b);
+            std::swap(acc_a, acc_b);
+        }
+        pre = acc_a;
+        be.launch(B, NL, KOrd{w, pre});
+        be.scan_excl(w.isleaf, w.lscan, NL, B);
+        be.launch(B, N, KLeafOrder{w, pre});
+        be.launch(B, NL, KPathInit{w, pre});
+
+        be.mark(5);
+        // K5 bottom-up replay of Forest::merge along heavy paths
+        const int RR = ceil_log2(N) + 2;
+        for (int r = 0; r < RR; ++r) be.launch(B, N, KReplay{w, r});
+
+        be.mark(6);
+        // K6 new_merge filters, lifting, per-slot arg-max, snapshots
+        be.launch(B, M, KFilter{w});
+        be.launch(B, N, KSlotInit{w});
+        be.launch(B, M, KLift{w});
+        be.launch(B, M, KSlotEvent{w});
+        be.launch(B, N, KSlotFlag{w});
+        be.scan_excl(w.sflag, w.soff, N, B);
+        be.launch(B, 1, KSnapCount{w});
+        be.launch(B, snap_cap, KRecClear{w});
+        be.launch(B, N, KSnapshot{w, pre});
+
+        be.mark(7);
+        // K7 overlay labels
+        be.launch(B, 2 * d.P2, KSegInit{w});
+        be.launch(B, snap_cap, KPaint{w});
+        be.launch(B, N, KLabel{w});
+        be.mark(8);
+    }
+};
+
+}  // namespace dofs

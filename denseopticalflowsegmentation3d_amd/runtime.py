@@ -1,0 +1,244 @@
+"""ctypes binding of the product C-ABI (include/dofs.h) in libdofs_hip.so.
+
+The HIP library is built in-tree (denseopticalflowsegmentation3d_amd/_build/libdofs_hip.so, see
+__graft_entry__.build()). There is no CPU fallback: loading fails loudly when the library is
+missing, and creating a context fails loudly when no gfx950 device is visible.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from .abi import (DofsBoxRecord, DofsEvent, DofsParams, DofsResult, DofsSnapshot, DofsSolution, default_params,
+                  solution_dict)
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "_build", "libdofs_hip.so")
+_LIBS: dict[str, C.CDLL] = {}
+
+_fp = C.POINTER(C.c_float)
+_ip = C.POINTER(C.c_int32)
+
+
+def load(path: str | None = None) -> C.CDLL:
+    """Load a library exporting the dofs C-ABI (default: the in-tree HIP build)."""
+    path = os.path.abspath(path or LIB_PATH)
+    if path in _LIBS:
+        return _LIBS[path]
+    if not os.path.exists(path):
+        raise RuntimeError(f"dofs HIP extension not built: {path} missing (run __graft_entry__.build())")
+    L = C.CDLL(path)
+    L.dofs_abi_version.restype = C.c_int32
+    L.dofs_default_params.argtypes = [C.POINTER(DofsParams)]
+    L.dofs_calib.argtypes = [_fp, _fp, _fp]
+    L.dofs_calib.restype = C.c_int32
+    L.dofs_intersect.argtypes = [_fp, _fp, _fp, _fp, _fp]
+    L.dofs_create.argtypes = [C.c_int32]
+    L.dofs_create.restype = C.c_void_p
+    L.dofs_destroy.argtypes = [C.c_void_p]
+    L.dofs_last_error.argtypes = [C.c_void_p]
+    L.dofs_last_error.restype = C.c_char_p
+    L.dofs_segment.argtypes = [C.c_void_p, _fp, C.c_int32, C.c_int32, C.c_size_t, _fp, _fp, _fp,
+                               C.POINTER(DofsParams), C.POINTER(DofsResult)]
+    L.dofs_segment.restype = C.c_int32
+    L.dofs_events.argtypes = [C.c_void_p, C.c_int32, C.POINTER(DofsEvent), C.c_int64]
+    L.dofs_events.restype = C.c_int32
+    L.dofs_segment_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, _fp, _fp, _fp,
+                                            C.POINTER(DofsParams), C.c_void_p]
+    L.dofs_segment_batch_device.restype = C.c_int32
+    L.dofs_batch_fetch.argtypes = [C.c_void_p, C.c_int32, C.POINTER(DofsResult)]
+    L.dofs_batch_fetch.restype = C.c_int32
+    L.dofs_batch_records_device.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _ip]
+    L.dofs_batch_records_device.restype = C.c_int32
+    L.dofs_batch_records_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+    L.dofs_batch_records_copy.restype = C.c_int32
+    L.dofs_profile.argtypes = [C.c_void_p, C.c_int32]
+    L.dofs_profile.restype = C.c_int32
+    L.dofs_profile_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), _ip]
+    L.dofs_profile_read.restype = C.c_int32
+    L.dofs_lift.argtypes = [C.c_void_p, _fp, _ip, _fp, _fp, _fp, C.c_int32, C.POINTER(DofsSolution)]
+    L.dofs_lift.restype = C.c_int32
+    L.dofs_lift_batch.argtypes = [C.c_void_p, C.c_int32, _fp, _ip, _ip, _fp, _fp, _fp, C.POINTER(DofsSolution)]
+    L.dofs_lift_batch.restype = C.c_int32
+    L.dofs_synth_flow_device.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_uint64, C.c_void_p]
+    L.dofs_synth_flow_device.restype = C.c_int32
+    if L.dofs_abi_version() != 1:
+        raise RuntimeError("dofs ABI version mismatch")
+    _LIBS[path] = L
+    return L
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _p(a, t=C.c_float):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def calib(lib: C.CDLL | None = None):
+    """get_mat() + get_mat_upper(0..2) → (persp 3x3, inv 3x3, inv_upper 3x3x3), float32."""
+    L = lib or load()
+    persp, inv, up = np.zeros(9, np.float32), np.zeros(9, np.float32), np.zeros(27, np.float32)
+    if L.dofs_calib(_p(persp), _p(inv), _p(up)) != 0:
+        raise RuntimeError("dofs_calib failed")
+    return persp.reshape(3, 3), inv.reshape(3, 3), up.reshape(3, 3, 3)
+
+
+def intersect(a1, a2, b1, b2, lib: C.CDLL | None = None) -> np.ndarray:
+    L = lib or load()
+    out = np.zeros(2, np.float32)
+    L.dofs_intersect(*[_p(_f32(v)) for v in (a1, a2, b1, b2)], _p(out))
+    return out
+
+
+@dataclass
+class FrameResult:
+    """Outputs of one frame: the non-empty Forest::segment_history slots and derived arrays."""
+    H: int
+    W: int
+    snapshots: np.ndarray          # structured (DofsSnapshot.np_dtype()), sorted by slot
+    labels: np.ndarray | None      # int32 [H*W]
+    leaf_order: np.ndarray | None  # int32 [H*W]
+    blurred: np.ndarray | None     # float32 [H, W, 2]
+    stats: dict
+
+    def members(self, snap) -> np.ndarray:
+        """SegmentData::seg of one snapshot (sorted pixel ids)."""
+        b, n = int(snap["seg_begin"]), int(snap["size"])
+        return np.sort(self.leaf_order[b:b + n])
+
+
+class Dofs:
+    """One context (one device, one stream): dofs_create / dofs_destroy."""
+
+    def __init__(self, device: int = 0, lib: C.CDLL | str | None = None):
+        self.lib = lib if isinstance(lib, C.CDLL) else load(lib)
+        self.ctx = self.lib.dofs_create(device)
+        if not self.ctx:
+            raise RuntimeError(f"dofs_create({device}) failed: no gfx950 device visible")
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.dofs_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        self.close()
+
+    def _err(self, rc: int, what: str):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed ({rc}): {self.lib.dofs_last_error(self.ctx).decode()}")
+
+    @staticmethod
+    def _mats(persp, inv, inv_upper):
+        return _f32(persp).ravel(), _f32(inv).ravel(), _f32(inv_upper).ravel()
+
+    def _result(self, H, W, cap, want_blur=True):
+        N = H * W
+        snaps = np.zeros(max(cap, 1), dtype=DofsSnapshot.np_dtype())
+        labels = np.zeros(N, np.int32)
+        leaf = np.zeros(N, np.int32)
+        blurred = np.zeros((H, W, 2), np.float32) if want_blur else None
+        r = DofsResult()
+        r.snapshots = snaps.ctypes.data_as(C.POINTER(DofsSnapshot))
+        r.snapshot_capacity = cap
+        r.labels = _p(labels, C.c_int32)
+        r.leaf_order = _p(leaf, C.c_int32)
+        r.blurred = _p(blurred) if want_blur else None
+        return r, snaps, labels, leaf, blurred
+
+    @staticmethod
+    def _stats(r: DofsResult) -> dict:
+        return {k: getattr(r.stats, k) for k, _ in r.stats._fields_}
+
+    def segment(self, flow: np.ndarray, persp, inv, inv_upper, params: DofsParams | None = None,
+                capacity: int = 65536) -> FrameResult:
+        """get_segmented_array on a host (H, W, 2) float32 flow field."""
+        flow = _f32(flow)
+        H, W = flow.shape[:2]
+        p, i, u = self._mats(persp, inv, inv_upper)
+        r, snaps, labels, leaf, blurred = self._result(H, W, capacity)
+        rc = self.lib.dofs_segment(self.ctx, _p(flow), H, W, 0, _p(p), _p(i), _p(u),
+                                   C.byref(params or default_params()), C.byref(r))
+        self._err(rc, "dofs_segment")
+        self._last_hw = (H, W)
+        return FrameResult(H, W, snaps[:r.n_snapshots].copy(), labels, leaf, blurred, self._stats(r))
+
+    def events(self, frame: int = 0) -> np.ndarray:
+        """Per-merge records (Kruskal order) of `frame` of the last batch."""
+        H, W = self._last_hw
+        n = max(H * W - 1, 0)
+        ev = np.zeros(max(n, 1), dtype=DofsEvent.np_dtype())
+        rc = self.lib.dofs_events(self.ctx, frame, ev.ctypes.data_as(C.POINTER(DofsEvent)), n)
+        self._err(rc, "dofs_events")
+        return ev[:n]
+
+    def segment_batch_device(self, d_flow: int, B: int, H: int, W: int, persp, inv, inv_upper,
+                             params: DofsParams | None = None, stream: int | None = None) -> None:
+        """Device-resident batch (d_flow = device pointer to B×H×W×2 float32). Asynchronous."""
+        p, i, u = self._mats(persp, inv, inv_upper)
+        rc = self.lib.dofs_segment_batch_device(self.ctx, C.c_void_p(d_flow), B, H, W, _p(p), _p(i), _p(u),
+                                                C.byref(params or default_params()), C.c_void_p(stream or 0))
+        self._err(rc, "dofs_segment_batch_device")
+        self._last_hw = (H, W)
+
+    def fetch(self, frame: int, capacity: int = 65536, want_blur: bool = True) -> FrameResult:
+        H, W = self._last_hw
+        r, snaps, labels, leaf, blurred = self._result(H, W, capacity, want_blur)
+        self._err(self.lib.dofs_batch_fetch(self.ctx, frame, C.byref(r)), "dofs_batch_fetch")
+        return FrameResult(H, W, snaps[:r.n_snapshots].copy(), labels, leaf, blurred, self._stats(r))
+
+    def records_device(self):
+        """(device ptr of B×cap DofsBoxRecord, device ptr of counters, cap)."""
+        rec, cnt, cap = C.c_void_p(), C.c_void_p(), C.c_int32()
+        self._err(self.lib.dofs_batch_records_device(self.ctx, C.byref(rec), C.byref(cnt), C.byref(cap)),
+                  "dofs_batch_records_device")
+        return rec.value, cnt.value, cap.value
+
+    def records_copy(self, d_dst: int, per_frame: int, stream: int | None = None) -> None:
+        """int32 counts[B] then B × per_frame DofsBoxRecord into a device buffer (stream-ordered)."""
+        self._err(self.lib.dofs_batch_records_copy(self.ctx, C.c_void_p(d_dst), per_frame, C.c_void_p(stream or 0)),
+                  "dofs_batch_records_copy")
+
+    STAGES = ("blur", "mst", "mst_sort", "krt", "preorder", "replay", "lift", "labels")
+
+    def profile(self, enable: bool = True) -> None:
+        self._err(self.lib.dofs_profile(self.ctx, 1 if enable else 0), "dofs_profile")
+
+    def profile_read(self) -> tuple[dict, int]:
+        ms = (C.c_double * 8)()
+        n = C.c_int32()
+        self._err(self.lib.dofs_profile_read(self.ctx, ms, C.byref(n)), "dofs_profile_read")
+        return {k: ms[i] for i, k in enumerate(self.STAGES)}, n.value
+
+    def lift(self, direction, box, mat, inv, inv_upper, cls: int) -> dict:
+        """get_bottom_variants on the GPU."""
+        s = DofsSolution()
+        rc = self.lib.dofs_lift(self.ctx, _p(_f32(direction)), _p(np.ascontiguousarray(box, np.int32), C.c_int32),
+                                _p(_f32(mat).ravel()), _p(_f32(inv).ravel()), _p(_f32(inv_upper).ravel()), cls,
+                                C.byref(s))
+        self._err(rc, "dofs_lift")
+        return solution_dict(s)
+
+    def lift_batch(self, dirs, boxes, cls, mat, inv, inv_upper27) -> np.ndarray:
+        dirs = _f32(dirs).reshape(-1, 2)
+        boxes = np.ascontiguousarray(boxes, np.int32).reshape(-1, 4)
+        cls = np.ascontiguousarray(cls, np.int32).ravel()
+        n = len(dirs)
+        out = np.zeros(n, dtype=DofsSolution.np_dtype())
+        rc = self.lib.dofs_lift_batch(self.ctx, n, _p(dirs), _p(boxes, C.c_int32), _p(cls, C.c_int32),
+                                      _p(_f32(mat).ravel()), _p(_f32(inv).ravel()), _p(_f32(inv_upper27).ravel()),
+                                      out.ctypes.data_as(C.POINTER(DofsSolution)))
+        self._err(rc, "dofs_lift_batch")
+        return out
+
+
+def synth_flow_device(d_out: int, B: int, H: int, W: int, seed0: int = 0, stream: int | None = None,
+                      lib: C.CDLL | None = None) -> None:
+    L = lib or load()
+    if L.dofs_synth_flow_device(C.c_void_p(d_out), B, H, W, seed0, C.c_void_p(stream or 0)) != 0:
+        raise RuntimeError("dofs_synth_flow_device failed")

@@ -168,6 +168,16 @@ int32_t dofs_batch_fetch(dofs_ctx* ctx, int32_t frame, dofs_result* out);
  * unused records have slot == -1) and per-frame counts (device int32[B]). */
 int32_t dofs_batch_records_device(dofs_ctx* ctx, void** d_records, void** d_counts, int32_t* capacity);
 
+/* Copy the batch's box records to a caller device buffer on `stream`: int32 counts[B] (snapshots per
+ * frame), then B × per_frame dofs_box_record (the first per_frame records of each frame). */
+int32_t dofs_batch_records_copy(dofs_ctx* ctx, void* d_dst, int32_t per_frame, void* stream);
+
+/* Stage timing with device events (0 = off). Stages: 0 blur, 1 MST (Borůvka), 2 MST sort, 3 KRT,
+ * 4 preorder, 5 replay, 6 lift + slots, 7 labels. dofs_profile_read returns the accumulated
+ * milliseconds per stage and the number of profiled batches, then resets. */
+int32_t dofs_profile(dofs_ctx* ctx, int32_t enable);
+int32_t dofs_profile_read(dofs_ctx* ctx, double ms[8], int32_t* batches);
+
 /* get_bottom_variants on the GPU (one candidate, or n candidates with per-candidate class). */
 int32_t dofs_lift(dofs_ctx* ctx, const float dir[2], const int32_t box[4], const float mat[9],
                   const float inv[9], const float inv_upper[9], int32_t cls, dofs_solution* out);

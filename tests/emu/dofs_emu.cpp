@@ -1,0 +1,103 @@
+// dofs_emu.cpp — TEST INFRASTRUCTURE ONLY: a sequential host backend for the product pipeline
+// (denseopticalflowsegmentation3d_amd/csrc). It runs every per-element kernel body of
+// dofs_kernels.h in a plain loop — one valid serialisation of the parallel launches — so the
+// parallel algorithm (Borůvka MST, KRT divide and conquer, heavy-path replay, ...) can be checked
+// against the oracle on a machine without a GPU. It is never loaded by the product package.
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#define DOFS_HD
+#define DOFS_HDM
+inline int dofs_ld(int* p) { return *p; }
+inline void dofs_st(int* p, int v) { *p = v; }
+inline int dofs_cas(int* p, int e, int v) {
+    int o = *p;
+    if (o == e) *p = v;
+    return o;
+}
+inline int dofs_exch(int* p, int v) {
+    int o = *p;
+    *p = v;
+    return o;
+}
+inline void dofs_amin_u64(unsigned long long* p, unsigned long long v) { *p = std::min(*p, v); }
+inline void dofs_amax_u64(unsigned long long* p, unsigned long long v) { *p = std::max(*p, v); }
+inline void dofs_amin_u32(unsigned* p, unsigned v) { *p = std::min(*p, v); }
+inline void dofs_amin(int* p, int v) { *p = std::min(*p, v); }
+inline void dofs_amax(int* p, int v) { *p = std::max(*p, v); }
+inline int dofs_aadd(int* p, int v) {
+    int o = *p;
+    *p += v;
+    return o;
+}
+inline void dofs_aor(int* p, int v) { *p |= v; }
+
+#include "../../denseopticalflowsegmentation3d_amd/csrc/dofs_common.h"
+#include "../../denseopticalflowsegmentation3d_amd/csrc/dofs_kernels.h"
+
+namespace dofs {
+struct HostBackend {
+    explicit HostBackend(int) {}
+    static bool device_ok(int) { return true; }
+    bool ok() const { return true; }
+    std::string error() const { return std::string(); }
+    void set_stream(void*) {}
+    void* alloc(size_t bytes) { return malloc(bytes); }
+    void free(void* p) { ::free(p); }
+    void memset(void* p, int v, size_t bytes) { ::memset(p, v, bytes); }
+    void h2d(void* d, const void* h, size_t bytes) { memcpy(d, h, bytes); }
+    void d2h(void* h, const void* d, size_t bytes) { memcpy(h, d, bytes); }
+    void sync() {}
+    void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height) {
+        for (size_t r = 0; r < height; ++r) memcpy((char*)dst + r * dpitch, (const char*)src + r * spitch, width);
+    }
+    void profile(bool) {}
+    void mark(int) {}
+    int profile_read(double* ms) {
+        for (int s = 0; s < 8; ++s) ms[s] = 0;
+        return 0;
+    }
+    template <class F>
+    static int launch_static(void*, int nf, int64_t n, const F& f) {
+        for (int fr = 0; fr < nf; ++fr)
+            for (int64_t i = 0; i < n; ++i) f(fr, i);
+        return DOFS_OK;
+    }
+    template <class F>
+    void launch(int nf, int64_t n, const F& f) {
+        launch_static(nullptr, nf, n, f);
+    }
+    void scan_excl(const int* in, int* out, int64_t n, int nf) {
+        for (int f = 0; f < nf; ++f) {
+            int s = 0;
+            for (int64_t i = 0; i < n; ++i) {
+                int v = in[f * n + i];
+                out[f * n + i] = s;
+                s += v;
+            }
+        }
+    }
+    void sort_pairs(const unsigned long long* kin, unsigned long long* kout, const unsigned* vin, unsigned* vout,
+                    int64_t n, int nf) {
+        std::vector<int64_t> ix((size_t)n);
+        for (int f = 0; f < nf; ++f) {
+            std::iota(ix.begin(), ix.end(), 0);
+            const unsigned long long* k = kin + f * n;
+            std::stable_sort(ix.begin(), ix.end(), [&](int64_t a, int64_t b) { return k[a] < k[b]; });
+            for (int64_t i = 0; i < n; ++i) {
+                kout[f * n + i] = k[ix[i]];
+                vout[f * n + i] = vin[f * n + ix[i]];
+            }
+        }
+    }
+};
+}  // namespace dofs
+
+using DofsBackend = dofs::HostBackend;
+#include "../../denseopticalflowsegmentation3d_amd/csrc/dofs_cabi.inc.h"

@@ -1,0 +1,66 @@
+"""Shared parity checks: product result (GPU or emulator) vs the CPU oracle on the same input."""
+import numpy as np
+
+from denseopticalflowsegmentation3d_amd.abi import default_params
+from oracle import binding as ob
+
+EVENT_FIELDS = ("start", "end", "weight", "root", "size", "rank", "bbox", "mean")
+SNAP_EXACT = ("slot", "event", "size", "bbox")
+
+
+def _b(a):
+    return np.ascontiguousarray(a).tobytes()
+
+
+def params(min_size=500, neighbor=8):
+    p = default_params()
+    p.min_size = min_size
+    p.neighbor = neighbor
+    return p
+
+
+def run_both(ctx, flow, calib, prm):
+    persp, inv, up = calib
+    o = ob.segment(flow, persp, inv, up, params=prm, mode=0, events=True)
+    g = ctx.segment(flow, persp, inv, up, params=prm)
+    ev = ctx.events(0)
+    return o, g, ev
+
+
+def check_exact(o, g, ev, lift_exact=True):
+    """Bit-exact: blurred field, per-merge events, snapshot slots/events/sizes/bboxes/member sets,
+    labels. Scores, moves and solutions bit-exact when lift_exact (host emulator), else within the
+    stated float tolerance (GPU transcendentals)."""
+    assert _b(o.blurred) == _b(g.blurred), "blurred flow differs"
+    for k in EVENT_FIELDS:
+        a, b = o.events[k], ev[k]
+        if _b(a) != _b(b):
+            bad = np.nonzero((np.asarray(a) != np.asarray(b)).reshape(len(a), -1).any(1))[0]
+            raise AssertionError(f"event field {k}: first mismatch at merge {bad[0]} ({len(bad)} total)")
+    assert len(o.snapshots) == len(g.snapshots), (len(o.snapshots), len(g.snapshots))
+    for k in SNAP_EXACT:
+        assert _b(o.snapshots[k]) == _b(g.snapshots[k]), f"snapshot field {k}"
+    for a, b in zip(o.snapshots, g.snapshots):
+        assert np.array_equal(o.members(a), g.members(b)), "snapshot member set"
+        assert a["sol"]["cls"] == b["sol"]["cls"]
+        if lift_exact:
+            assert a["sol"].tobytes() == b["sol"].tobytes()
+            assert a["score"] == b["score"] and a["move"] == b["move"]
+        else:
+            check_solution_close(a["sol"], b["sol"])
+            assert abs(a["score"] - b["score"]) <= 1e-6
+            assert a["move"] == b["move"]  # no transcendental on this path
+    assert np.array_equal(o.labels, g.labels), "labels"
+    assert o.stats == g.stats, (o.stats, g.stats)
+
+
+# Box corners: float32 geometry fed by double atan2/sin/cos of the device math library
+# (≤ 1-2 ulp from glibc). Stated tolerance: 1e-3 px relative to the coordinate magnitude + 1e-3 px,
+# errors/orientation within 1e-6 absolute.
+def check_solution_close(a, b):
+    assert a["valid"] == b["valid"] and a["cls"] == b["cls"]
+    for k in ("ps_bev", "lower_face", "upper_face", "rectangle"):
+        x, y = np.asarray(a[k], np.float64), np.asarray(b[k], np.float64)
+        assert np.all(np.abs(x - y) <= 1e-3 + 1e-5 * np.abs(x)), (k, x, y)
+    for k in ("w_error", "h_error", "orient"):
+        assert abs(float(a[k]) - float(b[k])) <= 1e-6, (k, a[k], b[k])
