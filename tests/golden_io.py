@@ -1,0 +1,27 @@
+"""Load the committed golden fixtures (numpy .npz, allow_pickle=False)."""
+import glob
+import os
+
+import numpy as np
+
+from denseopticalflowsegmentation3d_amd.abi import DofsEvent, DofsSnapshot, default_params
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def names():
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+def load(name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    c = z["calib"]
+    ms, nbr = (int(v) for v in z["params"])
+    prm = default_params()
+    prm.min_size, prm.neighbor = ms, nbr
+    ev = np.ascontiguousarray(z["events"]).view(DofsEvent.np_dtype()).ravel()
+    sn = np.ascontiguousarray(z["snapshots"]).view(DofsSnapshot.np_dtype()).ravel()
+    off = z["member_off"]
+    members = [z["members"][off[i]:off[i + 1]] for i in range(len(off) - 1)]
+    return dict(flow=z["flow"], prm=prm, calib=(c[:9].reshape(3, 3), c[9:18].reshape(3, 3), c[18:].reshape(3, 3, 3)),
+                blurred=z["blurred"], events=ev, snapshots=sn, members=members, labels=z["labels"])
