@@ -48,7 +48,9 @@ enum Counter {
     C_QUAL = 3,
     C_SNAP = 4,
     C_MST = 5,
-    C_ACT = 8  // C_ACT + r: Borůvka round r found a cross-component edge
+    C_SHORT = 6,
+    C_LONG = 7,
+    C_ACT = 16  // C_ACT + r: Borůvka round r found a cross-component edge
 };
 
 constexpr uint32_t kNoEdge = 0xFFFFFFFFu;

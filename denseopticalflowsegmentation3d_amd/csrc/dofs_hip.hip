@@ -45,6 +45,146 @@ __global__ __launch_bounds__(kBlock) void k_generic(F f, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += step) f(fr, i);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// K5 (long heavy paths): one wave64 per path. The running union-find state (float mean x/y,
+// rank, root) is a strictly sequential recurrence (Forest::merge, graph.cpp:184-190): its float
+// roundings must be replayed in Kruskal order. Lane l gathers the inputs of position q-l (light
+// child value, node size/bbox) for a 64-step chunk while the previous chunk is being consumed;
+// every lane then runs the same 64 dependent steps, reading step k's inputs with v_readlane
+// (wave-uniform scalars), and lane k keeps step k's result for one coalesced store.
+// ---------------------------------------------------------------------------------------------
+struct LongIn {
+    int x;        // node at this position
+    int ok;       // position on the path and its light child completed in an earlier round
+    int top;      // this position is the path top
+    int lside;    // light child is the end side (B)
+    int lrank, lroot;
+    float fs;     // (float) heavy-child size
+    float wbx, wby;  // light child's weighted flow, float(m * (float)size)
+    double r;     // 1 / (double)(size of the merged set)
+    int sz;
+    I4 bb;
+};
+
+__device__ inline LongIn long_load(const Ws& w, int64_t lb, int p, int top, int round) {
+    LongIn in;
+    in.ok = 0;
+    in.top = 0;
+    in.x = 0;
+    in.sz = 0;
+    if (p < top) return in;
+    const int x = w.ord[lb + p];
+    const int info = w.linfo[lb + p];
+    const int lt = info & kLinfoId;
+    const int rd = w.ready[lb + lt];
+    const NodeVal lv = w.V[lb + lt];
+    const int sz = w.SZ[lb + x];
+    in.x = x;
+    in.ok = rd < round;
+    in.top = (info & kLinfoTop) ? 1 : 0;
+    in.lside = (info & kLinfoB) ? 1 : 0;
+    in.lrank = lv.rank;
+    in.lroot = lv.root;
+    in.fs = (float)(sz - lv.size);
+    in.wbx = lv.mx * (float)lv.size;
+    in.wby = lv.my * (float)lv.size;
+    in.r = 1. / (double)sz;
+    in.sz = sz;
+    in.bb = w.BB[lb + x];
+    return in;
+}
+
+__device__ inline int rl_i(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+__device__ inline float rl_f(float v, int k) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k)); }
+__device__ inline double rl_d(double v, int k) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), k);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ void replay_long_path(const Ws& w, int f, int jj, int round) {
+    const Dims& d = w.d;
+    const int j = w.list_long[f * d.N + jj];
+    int* curp = w.cur + f * d.N + j;
+    int q = *curp;
+    if (q < 0) return;
+    const int top = w.ptop[f * d.N + j];
+    const int lane = threadIdx.x;
+    const int64_t lb = f * d.NL;
+    const NodeVal run = w.V[lb + w.ord[lb + q + 1]];
+    float mx = run.mx, my = run.my;
+    int rank = run.rank, root = run.root;
+    LongIn in = long_load(w, lb, q - lane, top, round);
+    for (;;) {
+        const LongIn nx = long_load(w, lb, q - 64 - lane, top, round);  // prefetch the next chunk
+        float rx = 0.f, ry = 0.f;
+        int rrank = 0, rroot = 0;
+        int done = 64, finished = 0;
+#pragma unroll
+        for (int k = 0; k < 64; ++k) {
+            if (!rl_i(in.ok, k)) {
+                done = k;
+                break;
+            }
+            const float fs = rl_f(in.fs, k);
+            const float tx = mx * fs, ty = my * fs;
+            const float ux = tx + rl_f(in.wbx, k), uy = ty + rl_f(in.wby, k);
+            const double r = rl_d(in.r, k);
+            mx = (float)((double)ux * r);
+            my = (float)((double)uy * r);
+            const int lrank = rl_i(in.lrank, k), lroot = rl_i(in.lroot, k);
+            // root = rank(A) > rank(B) ? root(A) : root(B); A = start side (graph.cpp:177-182)
+            const int nroot = rl_i(in.lside, k) ? (rank > lrank ? root : lroot) : (lrank > rank ? lroot : root);
+            rank = (rank == lrank) ? rank + 1 : (rank > lrank ? rank : lrank);
+            root = nroot;
+            if (lane == k) {
+                rx = mx;
+                ry = my;
+                rrank = rank;
+                rroot = root;
+            }
+            if (rl_i(in.top, k)) {
+                done = k + 1;
+                finished = 1;
+                break;
+            }
+        }
+        if (lane < done) {
+            NodeVal v;
+            v.mx = rx;
+            v.my = ry;
+            v.size = in.sz;
+            v.root = rroot;
+            v.x0 = (int16_t)in.bb.x0;
+            v.y0 = (int16_t)in.bb.y0;
+            v.x1 = (int16_t)in.bb.x1;
+            v.y1 = (int16_t)in.bb.y1;
+            v.rank = rrank;
+            v.pad = 0;
+            w.V[lb + in.x] = v;
+            if (finished && lane == done - 1) w.ready[lb + in.x] = round;
+        }
+        if (finished) {
+            if (lane == 0) *curp = -1;
+            return;
+        }
+        if (done < 64) {
+            if (lane == 0) *curp = q - done;
+            return;
+        }
+        q -= 64;
+        in = nx;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_replay_long(Ws w, int round) {
+    const int f = blockIdx.y;
+    const int n = w.C(f)[C_LONG];
+    for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path(w, f, jj, round);
+}
+
 struct HipBackend {
     int device = 0;
     hipStream_t own = nullptr;
@@ -179,6 +319,11 @@ struct HipBackend {
     template <class F>
     void launch(int nf, int64_t n, const F& f) {
         if (launch_on(stream, nf, n, f) != DOFS_OK) note(hipErrorLaunchFailure, "kernel launch");
+    }
+
+    void replay_long(const Ws& w, int round) {
+        hipLaunchKernelGGL(k_replay_long, dim3(1024u, (unsigned)w.d.B), dim3(64), 0, stream, w, round);
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_replay_long launch");
     }
 
     void* temp(size_t bytes) {

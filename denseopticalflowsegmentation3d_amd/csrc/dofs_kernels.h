@@ -78,8 +78,10 @@ struct Ws {
     // per pixel (stride N)
     int* LP;
     int* leaf_order;
-    int* paths;
     int* cur;
+    int* ptop;
+    int* list_short;
+    int* list_long;
     int* sevent;
     unsigned long long* sbest;
     int* sflag;
@@ -210,7 +212,7 @@ struct KBlurCol {
 };
 
 // ---------------------------------------------------------------------------------------------
-// Lock-free union-find on an int parent array (hook the larger root onto the smaller).
+// Lock-free union-find on an int parent array.
 // ---------------------------------------------------------------------------------------------
 DOFS_HD inline int uf_find(int* P, int x) {
     for (;;) {
@@ -222,12 +224,25 @@ DOFS_HD inline int uf_find(int* P, int x) {
         x = gp;
     }
 }
+// Randomised linking: the root with the larger hash priority is hooked onto the other, so trees
+// stay O(log n) deep in expectation even when unions arrive in monotone (chain) order.
+DOFS_HD inline unsigned uf_prio(int x) {
+    unsigned h = (unsigned)x * 0x9E3779B1u;
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    return h;
+}
+DOFS_HD inline bool uf_above(int a, int b) {  // a is hooked below b
+    const unsigned pa = uf_prio(a), pb = uf_prio(b);
+    return pa > pb || (pa == pb && a > b);
+}
 DOFS_HD inline void uf_union(int* P, int a, int b) {
     for (;;) {
         a = uf_find(P, a);
         b = uf_find(P, b);
         if (a == b) return;
-        if (a < b) {
+        if (!uf_above(a, b)) {
             int t = a;
             a = b;
             b = t;
@@ -522,10 +537,15 @@ struct KDncCompress {
         for (int side = 0; side < 2; ++side) {
             const int x = side ? w.lv[o] : w.lu[o];
             int r = x;
-            for (;;) {  // no union runs in this kernel: plain walk, others only shorten paths
+            for (;;) {  // no union runs in this kernel: roots are final, others only shorten paths
                 int p = dofs_ld(P + r);
                 if (p == r) break;
                 r = p;
+            }
+            for (int y = x; y != r;) {  // full path compression: later walks are one hop
+                int p = dofs_ld(P + y);
+                if (p != r) dofs_st(P + y, r);
+                y = p;
             }
             if (side == 0) ri = r;
             if (own & (1 << side)) {
@@ -698,6 +718,8 @@ constexpr int kLinfoId = (1 << 29) - 1;
 constexpr int kLinfoB = 1 << 29;
 constexpr int kLinfoTop = 1 << 30;
 
+constexpr int kLongPath = 256;  // heavy paths at least this long go to the wave-cooperative replay
+
 struct KPathInit {
     Ws w;
     const int* pre;
@@ -716,6 +738,17 @@ struct KPathInit {
             heavy_child(w, f, (int)x, &lt, &lB);
             w.linfo[lb + q] = lt | (lB ? kLinfoB : 0) | (top ? kLinfoTop : 0);
             w.ready[lb + x] = kIntMax;
+            if (top) {  // heavy path [q, bottom): its bottom leaf is the first leaf after q in preorder
+                const int leaf = w.leaf_order[f * d.N + w.lscan[lb + q]];
+                const int qb = pre[lb + leaf];
+                const int j = dofs_aadd(w.C(f) + C_PATHS, 1);
+                w.cur[f * d.N + j] = qb - 1;
+                w.ptop[f * d.N + j] = q;
+                if (qb - q >= kLongPath)
+                    w.list_long[f * d.N + dofs_aadd(w.C(f) + C_LONG, 1)] = j;
+                else
+                    w.list_short[f * d.N + dofs_aadd(w.C(f) + C_SHORT, 1)] = j;
+            }
         } else {
             const F2 v = w.blur[f * d.N + x];
             NodeVal nv;
@@ -730,11 +763,6 @@ struct KPathInit {
             w.V[lb + x] = nv;
             w.ready[lb + x] = -1;
             w.linfo[lb + q] = kLinfoTop;
-            if (!top) {  // heavy leaf = bottom of a heavy path
-                const int j = dofs_aadd(w.C(f) + C_PATHS, 1);
-                w.paths[f * d.N + j] = (int)x;
-                w.cur[f * d.N + j] = q - 1;
-            }
         }
     }
 };
@@ -760,12 +788,17 @@ DOFS_HD inline NodeVal merge_vals(const NodeVal& A, const NodeVal& B) {
 
 // K5 — sequential replay along one heavy path (bottom-up), round `round`: advances until a light
 // child not completed in an earlier round is met (resumed next round) or the path top is done.
+// `list`/`count` select the short-path or the long-path list (the HIP build replays long paths
+// with the wave-cooperative kernel of dofs_hip.hip instead; same state, same results).
 struct KReplay {
     Ws w;
     int round;
-    DOFS_HD void operator()(int f, int64_t j) const {
+    const int* list;
+    int count;
+    DOFS_HD void operator()(int f, int64_t jj) const {
         const Dims& d = w.d;
-        if (j >= w.C(f)[C_PATHS]) return;
+        if (jj >= w.C(f)[count]) return;
+        const int j = list[f * d.N + jj];
         int* curp = w.cur + f * d.N + j;
         int q = *curp;
         if (q < 0) return;

@@ -141,8 +141,10 @@ struct Pipeline {
         w.ready = (int*)take(4 * B * NL);
         w.LP = (int*)take(4 * B * N);
         w.leaf_order = (int*)take(4 * B * N);
-        w.paths = (int*)take(4 * B * N);
         w.cur = (int*)take(4 * B * N);
+        w.ptop = (int*)take(4 * B * N);
+        w.list_short = (int*)take(4 * B * N);
+        w.list_long = (int*)take(4 * B * N);
         w.sevent = (int*)take(4 * B * N);
         w.sbest = (unsigned long long*)take(8 * B * N);
         w.sflag = (int*)take(4 * B * N);
@@ -250,7 +252,10 @@ struct Pipeline {
         be.mark(5);
         // K5 bottom-up replay of Forest::merge along heavy paths
         const int RR = ceil_log2(N) + 2;
-        for (int r = 0; r < RR; ++r) be.launch(B, N, KReplay{w, r});
+        for (int r = 0; r < RR; ++r) {
+            be.launch(B, N, KReplay{w, r, w.list_short, C_SHORT});
+            be.replay_long(w, r);
+        }
 
         be.mark(6);
         // K6 new_merge filters, lifting, per-slot arg-max, snapshots

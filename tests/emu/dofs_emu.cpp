@@ -57,6 +57,7 @@ struct HostBackend {
     void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height) {
         for (size_t r = 0; r < height; ++r) memcpy((char*)dst + r * dpitch, (const char*)src + r * spitch, width);
     }
+    void replay_long(const Ws& w, int r) { launch(w.d.B, w.d.N, KReplay{w, r, w.list_long, C_LONG}); }
     void profile(bool) {}
     void mark(int) {}
     int profile_read(double* ms) {

@@ -31,3 +31,11 @@ def test_adversarial_parity(gpu, calib, kind):
             "ints": np.round(rng.normal(size=(H, W, 2)) * 4) + 2.0}[kind].astype(np.float32)
     o, g, ev = run_both(gpu, flow, calib, params(50, 8))
     check_exact(o, g, ev, lift_exact=False)
+
+
+@pytest.mark.parametrize("H,W,seed", [(720, 1280, 3), (1080, 1920, 0)])
+def test_full_size_parity(gpu, calib, H, W, seed):
+    """BASELINE configs 2/3 shapes: every merge event, snapshot and label bit-exact vs the oracle."""
+    flow = ob.synth_flow(H, W, seed)
+    o, g, ev = run_both(gpu, flow, calib, params(500, 8))
+    check_exact(o, g, ev, lift_exact=False)
