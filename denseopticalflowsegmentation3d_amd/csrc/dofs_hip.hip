@@ -32,6 +32,82 @@ __device__ inline int dofs_aadd(int* p, int v) { return atomicAdd(p, v); }
 __device__ inline void dofs_aor(int* p, int v) { atomicOr(p, v); }
 
 #include "dofs_common.h"
+
+// Keyed atomic updates aggregated across the wave: when all 64 lanes are present, the lanes whose
+// key equals the first active lane's key are reduced with cross-lane shuffles and updated by one
+// atomic; the other active lanes update directly (min/max read first: monotone, often skipped).
+// A big union-find component is the key of most lanes at the top divide-and-conquer levels, so
+// this turns ~one atomic per lane on a single address into ~one per wave.
+__device__ inline int wave_lane() { return __lane_id(); }
+template <class T, class Op>
+__device__ inline T wave_reduce(T v, Op op) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = op(v, __shfl_xor(v, m, 64));
+    return v;
+}
+__device__ inline void dofs_amin(int* p, int v);
+__device__ inline void dofs_amax(int* p, int v);
+__device__ inline int dofs_aadd(int* p, int v);
+template <class B4>
+__device__ inline void dofs_agg_size_bbox(int* cs, B4* bb, int key, int val, const B4& b, bool act) {
+    const unsigned long long present = __ballot(1);
+    const unsigned long long on = __ballot(act);
+    if (!on) return;
+    bool done = false;
+    if (present == ~0ull) {
+        const int leader = __ffsll((long long)on) - 1;
+        const int k0 = __shfl(key, leader, 64);
+        const bool same = act && key == k0;
+        const int s = wave_reduce(same ? val : 0, [](int a, int c) { return a + c; });
+        const int x0 = wave_reduce(same ? b.x0 : 0x7fffffff, [](int a, int c) { return a < c ? a : c; });
+        const int y0 = wave_reduce(same ? b.y0 : 0x7fffffff, [](int a, int c) { return a < c ? a : c; });
+        const int x1 = wave_reduce(same ? b.x1 : -1, [](int a, int c) { return a > c ? a : c; });
+        const int y1 = wave_reduce(same ? b.y1 : -1, [](int a, int c) { return a > c ? a : c; });
+        if (wave_lane() == leader) {
+            atomicAdd(cs + k0, s);
+            B4* a = bb + k0;
+            if (__hip_atomic_load(&a->x0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > x0) atomicMin(&a->x0, x0);
+            if (__hip_atomic_load(&a->y0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > y0) atomicMin(&a->y0, y0);
+            if (__hip_atomic_load(&a->x1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < x1) atomicMax(&a->x1, x1);
+            if (__hip_atomic_load(&a->y1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < y1) atomicMax(&a->y1, y1);
+        }
+        done = same;
+    }
+    if (act && !done) {
+        atomicAdd(cs + key, val);
+        B4* a = bb + key;
+        atomicMin(&a->x0, b.x0);
+        atomicMin(&a->y0, b.y0);
+        atomicMax(&a->x1, b.x1);
+        atomicMax(&a->y1, b.y1);
+    }
+}
+template <bool kMax>
+__device__ inline void agg_minmax(int* base, int key, int val, bool act) {
+    const unsigned long long present = __ballot(1);
+    const unsigned long long on = __ballot(act);
+    if (!on) return;
+    bool done = false;
+    if (present == ~0ull) {
+        const int leader = __ffsll((long long)on) - 1;
+        const int k0 = __shfl(key, leader, 64);
+        const bool same = act && key == k0;
+        const int v = kMax ? wave_reduce(same ? val : (int)0x80000000, [](int a, int c) { return a > c ? a : c; })
+                           : wave_reduce(same ? val : 0x7fffffff, [](int a, int c) { return a < c ? a : c; });
+        if (wave_lane() == leader) {
+            const int cur = __hip_atomic_load(base + k0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (kMax ? cur < v : cur > v) kMax ? atomicMax(base + k0, v) : atomicMin(base + k0, v);
+        }
+        done = same;
+    }
+    if (act && !done) {
+        const int cur = __hip_atomic_load(base + key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (kMax ? cur < val : cur > val) kMax ? atomicMax(base + key, val) : atomicMin(base + key, val);
+    }
+}
+__device__ inline void dofs_agg_max(int* base, int key, int val, bool act) { agg_minmax<true>(base, key, val, act); }
+__device__ inline void dofs_agg_min(int* base, int key, int val, bool act) { agg_minmax<false>(base, key, val, act); }
+
 #include "dofs_kernels.h"
 
 namespace dofs {

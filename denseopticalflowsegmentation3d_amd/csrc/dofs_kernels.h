@@ -495,7 +495,8 @@ struct KDncTouch {
         int own = 0;
         for (int side = 0; side < 2; ++side) {
             const int x = side ? w.lv[o] : w.lu[o];
-            if (dofs_exch(w.stamp + lb + x, depth) != depth) {
+            // high-degree labels (big components) are shared by many edges: read before exchanging
+            if (dofs_ld(w.stamp + lb + x) != depth && dofs_exch(w.stamp + lb + x, depth) != depth) {
                 own |= 1 << side;
                 w.P[lb + x] = x;
                 w.CS[lb + x] = 0;
@@ -528,12 +529,12 @@ struct KDncCompress {
     int64_t S;
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
-        if (!dnc_is_L(d, i, S)) return;
+        if (!dnc_is_L(d, i, S)) return;  // uniform per wave while S/2 >= 64 (aggregation below)
         const int64_t o = f * d.M + i;
         const int64_t lb = f * d.NL;
         int* P = w.P + lb;
         const int own = w.own[o];
-        int ri = -1;
+        int root[2];
         for (int side = 0; side < 2; ++side) {
             const int x = side ? w.lv[o] : w.lu[o];
             int r = x;
@@ -547,19 +548,18 @@ struct KDncCompress {
                 if (p != r) dofs_st(P + y, r);
                 y = p;
             }
-            if (side == 0) ri = r;
-            if (own & (1 << side)) {
-                dofs_st(P + x, r);
-                dofs_aadd(w.CS + lb + r, w.SZ[lb + x]);
-                const I4 b = w.BB[lb + x];
-                I4* acc = w.BBacc + lb + r;
-                dofs_amin(&acc->x0, b.x0);
-                dofs_amin(&acc->y0, b.y0);
-                dofs_amax(&acc->x1, b.x1);
-                dofs_amax(&acc->y1, b.y1);
-            }
+            root[side] = r;
         }
-        dofs_amax(w.MX + lb + ri, (int)i);
+        // component aggregates: size, bbox (owned labels only: each label counted once) and the
+        // max L-edge rank; wave-aggregated because a big component's root is shared by most lanes
+        for (int side = 0; side < 2; ++side) {
+            const int x = side ? w.lv[o] : w.lu[o];
+            const bool act = (own >> side) & 1;
+            I4 b = w.BB[lb + x];
+            dofs_agg_size_bbox(w.CS + lb, w.BBacc + lb, root[side], act ? w.SZ[lb + x] : 0, b, act);
+            if (act) dofs_st(P + x, root[side]);
+        }
+        dofs_agg_max(w.MX + lb, root[0], (int)i, true);
     }
 };
 
@@ -587,13 +587,14 @@ struct KDncRelabelR {
         if (!dnc_is_R(j, S)) return;
         const int64_t o = f * d.M + j;
         const int64_t lb = f * d.NL;
-        for (int side = 0; side < 2; ++side) {
+        for (int side = 0; side < 2; ++side) {  // uniform per wave while S/2 >= 64 (aggregation)
             int* lp = side ? (w.lv + o) : (w.lu + o);
             const int x = *lp;
-            if (w.stamp[lb + x] != depth) continue;
-            const int li = w.MX[lb + w.P[lb + x]];
-            *lp = (int)(d.N + li);
-            dofs_amin(w.MINR + f * d.M + li, (int)(2 * j + side));
+            const bool act = w.stamp[lb + x] == depth;
+            const int li = act ? w.MX[lb + w.P[lb + x]] : 0;
+            if (act) *lp = (int)(d.N + li);
+            // smallest-rank R edge touching the L component li (many R edges touch a big one)
+            dofs_agg_min(w.MINR + f * d.M, li, (int)(2 * j + side), act);
         }
     }
 };

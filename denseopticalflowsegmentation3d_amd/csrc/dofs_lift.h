@@ -51,10 +51,10 @@ DOFS_HDM inline P2 warp(P2 p, const float* m) {
 }
 
 // lifting_3d.cpp:162-217; false <=> the reference returns an empty corner vector.
-DOFS_HDM inline bool bottom(const P2 wc[4], double orient, double w, double h, double* err, P2 out[4]) {
+// co/si = cos(orient), sin(orient) (the reference evaluates them at every use; same values).
+DOFS_HDM inline bool bottom(const P2 wc[4], double co, double si, double w, double h, double* err, P2 out[4]) {
     const float inf = __builtin_inff();
     P2 a0 = p_iv(wc[0]), a1 = p_iv(wc[1]), a2 = p_iv(wc[2]), a3 = p_iv(wc[3]);
-    const double co = cos(orient), si = sin(orient);
     P2 k = intersect(a3, mk((float)(a3.x + co), (float)(a3.y + si)), a0, a1);
     if (k.x == inf || k.y == inf) return false;
     double l = p_norm(p_sub(a3, k));
@@ -108,28 +108,44 @@ struct LiftMats {
     int obj_size[3][2];
 };
 
-// get_bottom_variants (lifting_3d.cpp:350-439) given the motion angle (class independent, :358).
-DOFS_HDM inline void bottom_variant(double mov_angle, const int box[4], const LiftMats& L, int cls,
-                                   dofs_solution* s) {
-    s->cls = cls;
-    P2 ps[4] = {mk((float)box[0], (float)box[3]), mk((float)box[0], (float)box[1]), mk((float)box[2], (float)box[1]),
-                mk((float)box[2], (float)box[3])};
+// Class-independent part of get_bottom_variants for one box: motion angle (:358, computed from the
+// box and direction only), its cos/sin, and the BEV corners ps_bev (:373-378).
+struct LiftPre {
+    double ang, co, si;
     P2 ps_bev[4];
-    for (int i = 0; i < 4; ++i) ps_bev[i] = warp(ps[i], L.persp);
+};
+
+DOFS_HDM inline void lift_pre(P2 dir, const int box[4], const LiftMats& L, LiftPre* pre) {
+    pre->ang = motion_direction(dir, box, L.persp);
+    pre->co = cos(pre->ang);
+    pre->si = sin(pre->ang);
+    const P2 ps[4] = {mk((float)box[0], (float)box[3]), mk((float)box[0], (float)box[1]),
+                      mk((float)box[2], (float)box[1]), mk((float)box[2], (float)box[3])};
+    for (int i = 0; i < 4; ++i) pre->ps_bev[i] = warp(ps[i], L.persp);
+}
+
+// get_bottom_variants (lifting_3d.cpp:350-439) for one class. With s == NULL only the errors are
+// produced (the scoring pass needs (w_error + h_error)/2 and validity only).
+DOFS_HDM inline bool bottom_variant(const LiftPre& pre, const int box[4], const LiftMats& L, int cls,
+                                    double* w_error, double* h_error, dofs_solution* s) {
     double err = 0.0;
     P2 corners[4];
-    if (!bottom(ps_bev, mov_angle, (double)L.obj_size[cls][0], (double)L.obj_size[cls][1], &err, corners)) {
-        s->valid = 0;
-        s->w_error = 0.0;
-        s->h_error = 0.0;
-        s->orient = 0.0;
-        for (int i = 0; i < 4; ++i) {
-            s->ps_bev[i][0] = s->ps_bev[i][1] = 0.0f;
-            s->lower_face[i][0] = s->lower_face[i][1] = 0.0f;
-            s->upper_face[i][0] = s->upper_face[i][1] = 0.0f;
-            s->rectangle[i][0] = s->rectangle[i][1] = 0.0f;
+    if (!bottom(pre.ps_bev, pre.co, pre.si, (double)L.obj_size[cls][0], (double)L.obj_size[cls][1], &err,
+                corners)) {
+        if (s) {
+            s->cls = cls;
+            s->valid = 0;
+            s->w_error = 0.0;
+            s->h_error = 0.0;
+            s->orient = 0.0;
+            for (int i = 0; i < 4; ++i) {
+                s->ps_bev[i][0] = s->ps_bev[i][1] = 0.0f;
+                s->lower_face[i][0] = s->lower_face[i][1] = 0.0f;
+                s->upper_face[i][0] = s->upper_face[i][1] = 0.0f;
+                s->rectangle[i][0] = s->rectangle[i][1] = 0.0f;
+            }
         }
-        return;
+        return false;
     }
     P2 untop[4];
     for (int i = 0; i < 4; ++i) untop[i] = warp(corners[i], L.inv);
@@ -138,25 +154,32 @@ DOFS_HDM inline void bottom_variant(double mov_angle, const int box[4], const Li
     P2 expected_edge = warp(corners[0], L.inv_upper + 9 * cls);
     double expected_h = p_norm(p_sub(untop[0], expected_edge));
     double computed_h = p_norm(p_sub(uf[0], untop[0]));
-    s->valid = 1;
-    for (int i = 0; i < 4; ++i) {
-        s->ps_bev[i][0] = ps_bev[i].x;
-        s->ps_bev[i][1] = ps_bev[i].y;
-        s->lower_face[i][0] = untop[i].x;
-        s->lower_face[i][1] = untop[i].y;
-        s->upper_face[i][0] = uf[i].x;
-        s->upper_face[i][1] = uf[i].y;
-        s->rectangle[i][0] = corners[i].x;
-        s->rectangle[i][1] = corners[i].y;
+    *w_error = err;
+    *h_error = (computed_h < expected_h) ? (computed_h / expected_h) : (expected_h / computed_h);
+    if (s) {
+        s->cls = cls;
+        s->valid = 1;
+        for (int i = 0; i < 4; ++i) {
+            s->ps_bev[i][0] = pre.ps_bev[i].x;
+            s->ps_bev[i][1] = pre.ps_bev[i].y;
+            s->lower_face[i][0] = untop[i].x;
+            s->lower_face[i][1] = untop[i].y;
+            s->upper_face[i][0] = uf[i].x;
+            s->upper_face[i][1] = uf[i].y;
+            s->rectangle[i][0] = corners[i].x;
+            s->rectangle[i][1] = corners[i].y;
+        }
+        s->w_error = err;
+        s->h_error = *h_error;
+        s->orient = pre.ang;
     }
-    s->w_error = err;
-    s->h_error = (computed_h < expected_h) ? (computed_h / expected_h) : (expected_h / computed_h);
-    s->orient = mov_angle;
+    return true;
 }
 
 DOFS_HDM inline void lift_one(P2 dir, const int box[4], const LiftMats& L, int cls, dofs_solution* s) {
-    double ang = motion_direction(dir, box, L.persp);
-    if (__builtin_isinf(ang)) {  // :360-364 (unreachable: atan2 is finite)
+    LiftPre pre;
+    lift_pre(dir, box, L, &pre);
+    if (__builtin_isinf(pre.ang)) {  // :360-364 (unreachable: atan2 is finite)
         s->cls = -1;
         s->valid = 0;
         s->w_error = -1.0;
@@ -164,23 +187,27 @@ DOFS_HDM inline void lift_one(P2 dir, const int box[4], const LiftMats& L, int c
         s->orient = 0.0;
         return;
     }
-    bottom_variant(ang, box, L, cls, s);
+    double we, he;
+    bottom_variant(pre, box, L, cls, &we, &he, s);
 }
 
 // get_score (graph.cpp:241-270): best class by (w_error + h_error)/2, -1 when no rectangle.
 // best may be NULL when only the score and class are needed.
 DOFS_HDM inline double score_event(P2 dir, const int box[4], const LiftMats& L, int* best_cls, dofs_solution* best) {
-    double ang = motion_direction(dir, box, L.persp);
+    LiftPre pre;
+    lift_pre(dir, box, L, &pre);
     double max_score = -1.0;
     *best_cls = -1;
     for (int cls = 0; cls < 3; ++cls) {
-        dofs_solution sol;
-        bottom_variant(ang, box, L, cls, &sol);
-        if (sol.valid && max_score < (sol.w_error + sol.h_error) / 2) {
-            max_score = (sol.w_error + sol.h_error) / 2;
+        double we, he;
+        if (bottom_variant(pre, box, L, cls, &we, &he, nullptr) && max_score < (we + he) / 2) {
+            max_score = (we + he) / 2;
             *best_cls = cls;
-            if (best) *best = sol;
         }
+    }
+    if (best && *best_cls >= 0) {
+        double we, he;
+        bottom_variant(pre, box, L, *best_cls, &we, &he, best);
     }
     return max_score;
 }
