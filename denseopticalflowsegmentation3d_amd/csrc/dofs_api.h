@@ -254,28 +254,38 @@ int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity
     if (capacity < d.M) return cx->fail(DOFS_ERR_CAPACITY, "event capacity");
     if (d.M <= 0) return DOFS_OK;
     Backend& be = cx->be;
-    std::vector<int> eu((size_t)d.M), evv((size_t)d.M);
+    std::vector<int> eu((size_t)d.M), evv((size_t)d.M), pre((size_t)d.M), rrank((size_t)d.NL), rroot((size_t)d.NL),
+        sz((size_t)d.M);
+    std::vector<float> rmx((size_t)d.NL), rmy((size_t)d.NL);
+    std::vector<I4> bb((size_t)d.M);
     std::vector<unsigned long long> key((size_t)d.M);
-    std::vector<NodeVal> v((size_t)d.M);
+    const int64_t fo = (int64_t)frame * d.NL;
     be.d2h(eu.data(), w.EU + (int64_t)frame * d.M, 4 * (size_t)d.M);
     be.d2h(evv.data(), w.EV + (int64_t)frame * d.M, 4 * (size_t)d.M);
     be.d2h(key.data(), w.key_out + (int64_t)frame * d.M, 8 * (size_t)d.M);
-    be.d2h(v.data(), w.V + (int64_t)frame * d.NL + d.N, sizeof(NodeVal) * (size_t)d.M);
+    be.d2h(pre.data(), cx->pipe.pre + fo + d.N, 4 * (size_t)d.M);
+    be.d2h(rmx.data(), w.Rmx + fo, 4 * (size_t)d.NL);
+    be.d2h(rmy.data(), w.Rmy + fo, 4 * (size_t)d.NL);
+    be.d2h(rrank.data(), w.Rrank + fo, 4 * (size_t)d.NL);
+    be.d2h(rroot.data(), w.Rroot + fo, 4 * (size_t)d.NL);
+    be.d2h(sz.data(), w.SZ + fo + d.N, 4 * (size_t)d.M);
+    be.d2h(bb.data(), w.BB + fo + d.N, sizeof(I4) * (size_t)d.M);
     be.sync();
     for (int64_t i = 0; i < d.M; ++i) {
         dofs_event& e = ev[i];
+        const int q = pre[i];
         e.start = eu[i];
         e.end = evv[i];
         memcpy(&e.weight, &key[i], sizeof(double));
-        e.root = v[i].root;
-        e.size = v[i].size;
-        e.rank = v[i].rank;
-        e.bbox[0] = v[i].x0;
-        e.bbox[1] = v[i].y0;
-        e.bbox[2] = v[i].x1;
-        e.bbox[3] = v[i].y1;
-        e.mean[0] = v[i].mx;
-        e.mean[1] = v[i].my;
+        e.root = rroot[q];
+        e.size = sz[i];
+        e.rank = rrank[q];
+        e.bbox[0] = bb[i].x0;
+        e.bbox[1] = bb[i].y0;
+        e.bbox[2] = bb[i].x1;
+        e.bbox[3] = bb[i].y1;
+        e.mean[0] = rmx[q];
+        e.mean[1] = rmy[q];
     }
     return cx->check();
 }

@@ -123,142 +123,141 @@ __global__ __launch_bounds__(kBlock) void k_generic(F f, int64_t n) {
 
 
 // ---------------------------------------------------------------------------------------------
-// K5 (long heavy paths): one wave64 per path. The running union-find state (float mean x/y,
-// rank, root) is a strictly sequential recurrence (Forest::merge, graph.cpp:184-190): its float
-// roundings must be replayed in Kruskal order. Lane l gathers the inputs of position q-l (light
-// child value, node size/bbox) for a 64-step chunk while the previous chunk is being consumed;
-// every lane then runs the same 64 dependent steps, reading step k's inputs with v_readlane
-// (wave-uniform scalars), and lane k keeps step k's result for one coalesced store.
+// K5 (long heavy paths): two wave64s per path, one per mean channel (wave 0 also carries rank and
+// root on the side). The float running mean of Forest::merge (graph.cpp:184-190) is a strictly
+// sequential recurrence — mul, add (f32), cvt, mul (f64), cvt per merge — whose roundings must be
+// replayed in Kruskal order; splitting the two channels over two SIMDs halves the issue load of the
+// latency-bound chain (tools/replay_micro.hip: 41 vs 54 ns per step for one wave doing both).
+// Per 64-step chunk every lane resolves one position's inputs (StepIn, plus the light child's
+// replay output when it is a merge node) into LDS while the previous chunk is consumed; the chain
+// reads step k with uniform LDS loads and writes step k's output to LDS; one coalesced store per
+// chunk writes the outputs back by preorder position.
 // ---------------------------------------------------------------------------------------------
-struct LongIn {
-    int x;        // node at this position
-    int ok;       // position on the path and its light child completed in an earlier round
-    int top;      // this position is the path top
-    int lside;    // light child is the end side (B)
-    int lrank, lroot;
-    float fs;     // (float) heavy-child size
-    float wbx, wby;  // light child's weighted flow, float(m * (float)size)
-    double r;     // 1 / (double)(size of the merged set)
-    int sz;
-    I4 bb;
+struct LongStep {  // resolved inputs of one step, one channel (32 B)
+    float fs;
+    float wb;
+    int meta;  // StepIn meta | kLongOk (inputs ready)
+    int pad;
+    double r;
+    int lrank;
+    int lroot;
 };
+constexpr int kLongOk = 8;
 
-__device__ inline LongIn long_load(const Ws& w, int64_t lb, int p, int top, int round) {
-    LongIn in;
-    in.ok = 0;
-    in.top = 0;
-    in.x = 0;
-    in.sz = 0;
-    if (p < top) return in;
-    const int x = w.ord[lb + p];
-    const int info = w.linfo[lb + p];
-    const int lt = info & kLinfoId;
-    const int rd = w.ready[lb + lt];
-    const NodeVal lv = w.V[lb + lt];
-    const int sz = w.SZ[lb + x];
-    in.x = x;
-    in.ok = rd < round;
-    in.top = (info & kLinfoTop) ? 1 : 0;
-    in.lside = (info & kLinfoB) ? 1 : 0;
-    in.lrank = lv.rank;
-    in.lroot = lv.root;
-    in.fs = (float)(sz - lv.size);
-    in.wbx = lv.mx * (float)lv.size;
-    in.wby = lv.my * (float)lv.size;
-    in.r = 1. / (double)sz;
-    in.sz = sz;
-    in.bb = w.BB[lb + x];
-    return in;
+__device__ inline LongStep long_resolve(const Ws& w, int64_t lb, int p, int top, int round, int ch) {
+    LongStep s;
+    s.meta = 0;
+    s.fs = 0.f;
+    s.wb = 0.f;
+    s.r = 0.0;
+    s.lrank = 0;
+    s.lroot = 0;
+    s.pad = 0;
+    if (p < top) return s;
+    const StepIn in = w.In[lb + p];
+    s.fs = in.fs;
+    s.r = in.r;
+    s.meta = in.meta;
+    if (in.meta & kStepDyn) {
+        const int lq = in.lroot;
+        if (w.ready[lb + lq] >= round) return s;  // not ok: light child completes in a later round
+        s.wb = (ch ? w.Rmy[lb + lq] : w.Rmx[lb + lq]) * (float)in.lrank;
+        s.lrank = w.Rrank[lb + lq];
+        s.lroot = w.Rroot[lb + lq];
+    } else {
+        s.wb = ch ? in.wby : in.wbx;
+        s.lrank = in.lrank;
+        s.lroot = in.lroot;
+    }
+    s.meta |= kLongOk;
+    return s;
 }
 
-__device__ inline int rl_i(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
-__device__ inline float rl_f(float v, int k) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k)); }
-__device__ inline double rl_d(double v, int k) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), k);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-__device__ void replay_long_path(const Ws& w, int f, int jj, int round) {
+__device__ void replay_long_path(const Ws& w, int f, int jj, int round, LongStep (*buf)[2][64], float (*res)[64],
+                                 int (*resi)[2][64]) {
     const Dims& d = w.d;
     const int j = w.list_long[f * d.N + jj];
     int* curp = w.cur + f * d.N + j;
+    const int wv = threadIdx.x >> 6;  // channel
+    const int lane = threadIdx.x & 63;
     int q = *curp;
-    if (q < 0) return;
     const int top = w.ptop[f * d.N + j];
-    const int lane = threadIdx.x;
+    __syncthreads();  // both waves have read the cursor before wave 0 may rewrite it
+    if (q < 0) return;
     const int64_t lb = f * d.NL;
-    const NodeVal run = w.V[lb + w.ord[lb + q + 1]];
-    float mx = run.mx, my = run.my;
-    int rank = run.rank, root = run.root;
-    LongIn in = long_load(w, lb, q - lane, top, round);
+    float m = wv ? w.Rmy[lb + q + 1] : w.Rmx[lb + q + 1];
+    int rank = w.Rrank[lb + q + 1], root = w.Rroot[lb + q + 1];
+    int cb = 0;
+    buf[wv][cb][lane] = long_resolve(w, lb, q - lane, top, round, wv);
     for (;;) {
-        const LongIn nx = long_load(w, lb, q - 64 - lane, top, round);  // prefetch the next chunk
-        float rx = 0.f, ry = 0.f;
-        int rrank = 0, rroot = 0;
+        const LongStep nx = long_resolve(w, lb, q - 64 - lane, top, round, wv);  // next chunk in flight
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS staging is visible
+        __builtin_amdgcn_wave_barrier();
+        const LongStep* b = buf[wv][cb];
         int done = 64, finished = 0;
-#pragma unroll
+#pragma unroll 8
         for (int k = 0; k < 64; ++k) {
-            if (!rl_i(in.ok, k)) {
+            const LongStep st = b[k];
+            if (!(st.meta & kLongOk)) {
                 done = k;
                 break;
             }
-            const float fs = rl_f(in.fs, k);
-            const float tx = mx * fs, ty = my * fs;
-            const float ux = tx + rl_f(in.wbx, k), uy = ty + rl_f(in.wby, k);
-            const double r = rl_d(in.r, k);
-            mx = (float)((double)ux * r);
-            my = (float)((double)uy * r);
-            const int lrank = rl_i(in.lrank, k), lroot = rl_i(in.lroot, k);
-            // root = rank(A) > rank(B) ? root(A) : root(B); A = start side (graph.cpp:177-182)
-            const int nroot = rl_i(in.lside, k) ? (rank > lrank ? root : lroot) : (lrank > rank ? lroot : root);
-            rank = (rank == lrank) ? rank + 1 : (rank > lrank ? rank : lrank);
-            root = nroot;
-            if (lane == k) {
-                rx = mx;
-                ry = my;
-                rrank = rank;
-                rroot = root;
+            const float t = m * st.fs;
+            m = (float)((double)(t + st.wb) * st.r);
+            res[wv][k] = m;
+            if (wv == 0) {
+                const int nroot = (st.meta & kStepB) ? (rank > st.lrank ? root : st.lroot)
+                                                     : (st.lrank > rank ? st.lroot : root);
+                rank = (rank == st.lrank) ? rank + 1 : (rank > st.lrank ? rank : st.lrank);
+                root = nroot;
+                resi[0][0][k] = rank;
+                resi[0][1][k] = root;
             }
-            if (rl_i(in.top, k)) {
+            if (st.meta & kStepTop) {
                 done = k + 1;
                 finished = 1;
                 break;
             }
         }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
         if (lane < done) {
-            NodeVal v;
-            v.mx = rx;
-            v.my = ry;
-            v.size = in.sz;
-            v.root = rroot;
-            v.x0 = (int16_t)in.bb.x0;
-            v.y0 = (int16_t)in.bb.y0;
-            v.x1 = (int16_t)in.bb.x1;
-            v.y1 = (int16_t)in.bb.y1;
-            v.rank = rrank;
-            v.pad = 0;
-            w.V[lb + in.x] = v;
-            if (finished && lane == done - 1) w.ready[lb + in.x] = round;
+            const int p = q - lane;
+            if (wv) {
+                w.Rmy[lb + p] = res[1][lane];
+            } else {
+                w.Rmx[lb + p] = res[0][lane];
+                w.Rrank[lb + p] = resi[0][0][lane];
+                w.Rroot[lb + p] = resi[0][1][lane];
+            }
         }
-        if (finished) {
-            if (lane == 0) *curp = -1;
-            return;
-        }
-        if (done < 64) {
-            if (lane == 0) *curp = q - done;
+        if (finished || done < 64) {
+            // both waves stop at the same step (same inputs); the top's readiness is read only in
+            // later rounds (kernel boundary), so either wave may publish it
+            if (wv == 0 && lane == 0) {
+                if (finished) {
+                    w.ready[lb + q - done + 1] = round;
+                    *curp = -1;
+                } else {
+                    *curp = q - done;
+                }
+            }
+            __syncthreads();
             return;
         }
         q -= 64;
-        in = nx;
+        cb ^= 1;
+        buf[wv][cb][lane] = nx;
     }
 }
 
-__global__ __launch_bounds__(64) void k_replay_long(Ws w, int round) {
+__global__ __launch_bounds__(128) void k_replay_long(Ws w, int round) {
+    __shared__ LongStep buf[2][2][64];
+    __shared__ float res[2][64];
+    __shared__ int resi[1][2][64];
     const int f = blockIdx.y;
     const int n = w.C(f)[C_LONG];
-    for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path(w, f, jj, round);
+    for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path(w, f, jj, round, buf, res, resi);
 }
 
 struct HipBackend {
@@ -398,7 +397,7 @@ struct HipBackend {
     }
 
     void replay_long(const Ws& w, int round) {
-        hipLaunchKernelGGL(k_replay_long, dim3(1024u, (unsigned)w.d.B), dim3(64), 0, stream, w, round);
+        hipLaunchKernelGGL(k_replay_long, dim3(256u, (unsigned)w.d.B), dim3(128), 0, stream, w, round);
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_replay_long launch");
     }
 

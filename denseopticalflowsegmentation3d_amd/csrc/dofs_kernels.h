@@ -24,6 +24,25 @@
 
 namespace dofs {
 
+// Inputs of the merge at preorder position q (node x, heavy child h, light child l), precomputed in
+// parallel; the replay then only carries the order-dependent state (mean, rank, root).
+//   fs = (float)size(h)      r = 1 / (double)size(x)
+//   wb = float(mean(l) * (float)size(l))  — static when l is a pixel; when l is a merge node
+//        (kStepDyn) its mean is produced by the replay itself: lrank holds size(l) and lroot its
+//        preorder position, and wb / rank / root are read once l's path has completed.
+struct StepIn {
+    float fs;
+    float wbx, wby;
+    int meta;
+    double r;
+    int lrank;
+    int lroot;
+};
+static_assert(sizeof(StepIn) == 32, "StepIn is one 32-byte record");
+constexpr int kStepB = 1;    // light child is the end side (B) of the merge
+constexpr int kStepTop = 2;  // x is the top of its heavy path
+constexpr int kStepDyn = 4;  // light child is a merge node (value produced by the replay)
+
 // Workspace: device pointers (frame-major; per-frame strides by size class) + constants.
 struct Ws {
     Dims d;
@@ -53,12 +72,12 @@ struct Ws {
     int* lu;
     int* lv;
     int* own;
+    int* lrr;
     int* MINR;
     int* parentE;
     int* childA;
     int* childB;
     // label / node space (stride NL)
-    int* stamp;
     int* P;
     int* CS;
     int* MX;
@@ -70,10 +89,13 @@ struct Ws {
     int* anc1;
     int* acc1;
     int* ord;
-    int* linfo;
     int* isleaf;
     int* lscan;
-    NodeVal* V;
+    StepIn* In;
+    float* Rmx;
+    float* Rmy;
+    int* Rrank;
+    int* Rroot;
     int* ready;
     // per pixel (stride N)
     int* LP;
@@ -435,7 +457,15 @@ struct KLabelInit {
     DOFS_HD void operator()(int f, int64_t x) const {
         const Dims& d = w.d;
         const int64_t o = f * d.NL + x;
-        w.stamp[o] = -1;
+        w.P[o] = (int)x;
+        w.MX[o] = -1;
+        w.CS[o] = 0;
+        I4 e;
+        e.x0 = kIntMax;
+        e.y0 = kIntMax;
+        e.x1 = -1;
+        e.y1 = -1;
+        w.BBacc[o] = e;
         if (x < d.N) {
             const int px = (int)(x % d.W), py = (int)(x / d.W);
             w.SZ[o] = 1;
@@ -483,35 +513,39 @@ DOFS_HD inline bool dnc_is_L(const Dims& d, int64_t i, int64_t S) {
 }
 DOFS_HD inline bool dnc_is_R(int64_t i, int64_t S) { return (i & (S - 1)) >= (S >> 1); }
 
-struct KDncTouch {
-    Ws w;
-    int64_t S;
-    int depth;
-    DOFS_HD void operator()(int f, int64_t i) const {
-        const Dims& d = w.d;
-        if (!dnc_is_L(d, i, S)) return;
-        const int64_t o = f * d.M + i;
-        const int64_t lb = f * d.NL;
-        int own = 0;
-        for (int side = 0; side < 2; ++side) {
-            const int x = side ? w.lv[o] : w.lu[o];
-            // high-degree labels (big components) are shared by many edges: read before exchanging
-            if (dofs_ld(w.stamp + lb + x) != depth && dofs_exch(w.stamp + lb + x, depth) != depth) {
-                own |= 1 << side;
-                w.P[lb + x] = x;
-                w.CS[lb + x] = 0;
-                w.MX[lb + x] = -1;
-                I4 b;
-                b.x0 = kIntMax;
-                b.y0 = kIntMax;
-                b.x1 = -1;
-                b.y1 = -1;
-                w.BBacc[lb + x] = b;
-            }
+// Union-find over the label space of one depth, linking by component size (big components stay
+// roots, so the many small components touching one big component hook onto it without CAS
+// contention on its root), ties by hash. Returns the label whose parent pointer this union set:
+// in a forest every edge hooks exactly one label and every non-root label is hooked by exactly one
+// edge, which gives each label a unique owner without atomics.
+DOFS_HD inline bool dnc_above(const int* SZ, int a, int b) {  // a is hooked below b
+    const int sa = SZ[a], sb = SZ[b];
+    if (sa != sb) return sa < sb;
+    return uf_above(a, b);
+}
+DOFS_HD inline int dnc_union(int* P, const int* SZ, int a, int b) {
+    for (;;) {
+        a = uf_find(P, a);
+        b = uf_find(P, b);
+        if (a == b) return -1;  // unreachable: L-edges form a forest over the labels
+        if (!dnc_above(SZ, a, b)) {
+            int t = a;
+            a = b;
+            b = t;
         }
-        w.own[o] = own;
+        if (dofs_cas(P + a, a, b) == a) return a;
     }
-};
+}
+DOFS_HD inline int walk_compress(int* P, int x) {  // no union runs concurrently: plain loads
+    int r = x;
+    for (int p = P[r]; p != r; p = P[r]) r = p;
+    for (int y = x; y != r;) {
+        const int p = P[y];
+        if (p != r) P[y] = r;
+        y = p;
+    }
+    return r;
+}
 
 struct KDncUnion {
     Ws w;
@@ -520,7 +554,8 @@ struct KDncUnion {
         const Dims& d = w.d;
         if (!dnc_is_L(d, i, S)) return;
         const int64_t o = f * d.M + i;
-        uf_union(w.P + f * d.NL, w.lu[o], w.lv[o]);
+        const int64_t lb = f * d.NL;
+        w.own[o] = dnc_union(w.P + lb, w.SZ + lb, w.lu[o], w.lv[o]);
     }
 };
 
@@ -532,34 +567,13 @@ struct KDncCompress {
         if (!dnc_is_L(d, i, S)) return;  // uniform per wave while S/2 >= 64 (aggregation below)
         const int64_t o = f * d.M + i;
         const int64_t lb = f * d.NL;
-        int* P = w.P + lb;
-        const int own = w.own[o];
-        int root[2];
-        for (int side = 0; side < 2; ++side) {
-            const int x = side ? w.lv[o] : w.lu[o];
-            int r = x;
-            for (;;) {  // no union runs in this kernel: roots are final, others only shorten paths
-                int p = dofs_ld(P + r);
-                if (p == r) break;
-                r = p;
-            }
-            for (int y = x; y != r;) {  // full path compression: later walks are one hop
-                int p = dofs_ld(P + y);
-                if (p != r) dofs_st(P + y, r);
-                y = p;
-            }
-            root[side] = r;
-        }
-        // component aggregates: size, bbox (owned labels only: each label counted once) and the
-        // max L-edge rank; wave-aggregated because a big component's root is shared by most lanes
-        for (int side = 0; side < 2; ++side) {
-            const int x = side ? w.lv[o] : w.lu[o];
-            const bool act = (own >> side) & 1;
-            I4 b = w.BB[lb + x];
-            dofs_agg_size_bbox(w.CS + lb, w.BBacc + lb, root[side], act ? w.SZ[lb + x] : 0, b, act);
-            if (act) dofs_st(P + x, root[side]);
-        }
-        dofs_agg_max(w.MX + lb, root[0], (int)i, true);
+        const int h = w.own[o];
+        const int r = walk_compress(w.P + lb, h);
+        // component size / bbox over the labels hooked in it (the root label is added by the
+        // L-root edge) and the max L-edge rank; wave-aggregated: a big component's root is the
+        // key of most lanes at the top levels
+        dofs_agg_size_bbox(w.CS + lb, w.BBacc + lb, r, w.SZ[lb + h], w.BB[lb + h], true);
+        dofs_agg_max(w.MX + lb, r, (int)i, true);
     }
 };
 
@@ -571,17 +585,26 @@ struct KDncLRoot {
         if (!dnc_is_L(d, i, S)) return;
         const int64_t o = f * d.M + i;
         const int64_t lb = f * d.NL;
-        const int r = w.P[lb + w.lu[o]];
-        if (w.MX[lb + r] != (int)i) return;
-        w.SZ[lb + d.N + i] = w.CS[lb + r];
-        w.BB[lb + d.N + i] = w.BBacc[lb + r];
+        const int r = w.P[lb + w.own[o]];  // hooked labels point at their root after KDncCompress
+        if (w.MX[lb + r] != (int)i) {
+            w.lrr[o] = -1;
+            return;
+        }
+        w.lrr[o] = r;
+        w.SZ[lb + d.N + i] = w.CS[lb + r] + w.SZ[lb + r];
+        const I4 a = w.BBacc[lb + r], b = w.BB[lb + r];
+        I4 m;
+        m.x0 = a.x0 < b.x0 ? a.x0 : b.x0;
+        m.y0 = a.y0 < b.y0 ? a.y0 : b.y0;
+        m.x1 = a.x1 > b.x1 ? a.x1 : b.x1;
+        m.y1 = a.y1 > b.y1 ? a.y1 : b.y1;
+        w.BB[lb + d.N + i] = m;
     }
 };
 
 struct KDncRelabelR {
     Ws w;
     int64_t S;
-    int depth;
     DOFS_HD void operator()(int f, int64_t j) const {
         const Dims& d = w.d;
         if (!dnc_is_R(j, S)) return;
@@ -590,11 +613,37 @@ struct KDncRelabelR {
         for (int side = 0; side < 2; ++side) {  // uniform per wave while S/2 >= 64 (aggregation)
             int* lp = side ? (w.lv + o) : (w.lu + o);
             const int x = *lp;
-            const bool act = w.stamp[lb + x] == depth;
-            const int li = act ? w.MX[lb + w.P[lb + x]] : 0;
+            const int r = w.P[lb + x];
+            // x is a label of this block's L forest <=> hooked (P[x] != x) or a touched root (MX set)
+            const int li = w.MX[lb + r];
+            const bool act = (r != x) || li >= 0;
             if (act) *lp = (int)(d.N + li);
             // smallest-rank R edge touching the L component li (many R edges touch a big one)
-            dofs_agg_min(w.MINR + f * d.M, li, (int)(2 * j + side), act);
+            dofs_agg_min(w.MINR + f * d.M, act ? li : 0, (int)(2 * j + side), act);
+        }
+    }
+};
+
+struct KDncCleanup {  // restore the clean label state (P[x] = x, MX = -1, CS = 0, BBacc = empty)
+    Ws w;
+    int64_t S;
+    DOFS_HD void operator()(int f, int64_t i) const {
+        const Dims& d = w.d;
+        if (!dnc_is_L(d, i, S)) return;
+        const int64_t o = f * d.M + i;
+        const int64_t lb = f * d.NL;
+        const int h = w.own[o];
+        w.P[lb + h] = h;
+        const int r = w.lrr[o];
+        if (r >= 0) {
+            w.MX[lb + r] = -1;
+            w.CS[lb + r] = 0;
+            I4 e;
+            e.x0 = kIntMax;
+            e.y0 = kIntMax;
+            e.x1 = -1;
+            e.y1 = -1;
+            w.BBacc[lb + r] = e;
         }
     }
 };
@@ -715,11 +764,8 @@ struct KLeafOrder {
     }
 };
 
-constexpr int kLinfoId = (1 << 29) - 1;
-constexpr int kLinfoB = 1 << 29;
-constexpr int kLinfoTop = 1 << 30;
-
 constexpr int kLongPath = 256;  // heavy paths at least this long go to the wave-cooperative replay
+
 
 struct KPathInit {
     Ws w;
@@ -736,9 +782,25 @@ struct KPathInit {
         }
         if (x >= d.N) {
             int lt, lB;
-            heavy_child(w, f, (int)x, &lt, &lB);
-            w.linfo[lb + q] = lt | (lB ? kLinfoB : 0) | (top ? kLinfoTop : 0);
-            w.ready[lb + x] = kIntMax;
+            const int h = heavy_child(w, f, (int)x, &lt, &lB);
+            StepIn in;
+            in.fs = (float)w.SZ[lb + h];
+            in.r = 1. / (double)w.SZ[lb + x];
+            in.meta = (lB ? kStepB : 0) | (top ? kStepTop : 0);
+            if (lt < d.N) {
+                const F2 v = w.blur[f * d.N + lt];
+                in.wbx = v.x * (float)1;
+                in.wby = v.y * (float)1;
+                in.lrank = 0;
+                in.lroot = lt;
+            } else {
+                in.meta |= kStepDyn;
+                in.wbx = in.wby = 0.f;
+                in.lrank = w.SZ[lb + lt];
+                in.lroot = pre[lb + lt];
+            }
+            w.In[lb + q] = in;
+            w.ready[lb + q] = kIntMax;
             if (top) {  // heavy path [q, bottom): its bottom leaf is the first leaf after q in preorder
                 const int leaf = w.leaf_order[f * d.N + w.lscan[lb + q]];
                 const int qb = pre[lb + leaf];
@@ -752,45 +814,36 @@ struct KPathInit {
             }
         } else {
             const F2 v = w.blur[f * d.N + x];
-            NodeVal nv;
-            nv.mx = v.x;
-            nv.my = v.y;
-            nv.size = 1;
-            nv.root = (int)x;
-            nv.x0 = nv.x1 = (int16_t)(x % d.W);
-            nv.y0 = nv.y1 = (int16_t)(x / d.W);
-            nv.rank = 0;
-            nv.pad = 0;
-            w.V[lb + x] = nv;
-            w.ready[lb + x] = -1;
-            w.linfo[lb + q] = kLinfoTop;
+            w.Rmx[lb + q] = v.x;
+            w.Rmy[lb + q] = v.y;
+            w.Rrank[lb + q] = 0;
+            w.Rroot[lb + q] = (int)x;
+            w.ready[lb + q] = -1;
         }
     }
 };
 
-// Forest::merge (graph.cpp:170-218) on KRT values: A = start side, B = end side.
-DOFS_HD inline NodeVal merge_vals(const NodeVal& A, const NodeVal& B) {
-    NodeVal r;
-    r.size = A.size + B.size;
-    r.root = (A.rank > B.rank) ? A.root : B.root;
-    r.rank = (A.rank == B.rank) ? A.rank + 1 : (A.rank > B.rank ? A.rank : B.rank);
-    const float wax = A.mx * (float)A.size, way = A.my * (float)A.size;
-    const float wbx = B.mx * (float)B.size, wby = B.my * (float)B.size;
-    const double ia = 1. / (double)(A.size + B.size);
-    r.mx = (float)((double)(wax + wbx) * ia);
-    r.my = (float)((double)(way + wby) * ia);
-    r.x0 = A.x0 < B.x0 ? A.x0 : B.x0;
-    r.y0 = A.y0 < B.y0 ? A.y0 : B.y0;
-    r.x1 = A.x1 > B.x1 ? A.x1 : B.x1;
-    r.y1 = A.y1 > B.y1 ? A.y1 : B.y1;
-    r.pad = 0;
-    return r;
+// Forest::merge (graph.cpp:170-218) of the running (heavy) set with a light child:
+//   mean = ((m_h * (float)s_h) + (m_l * (float)s_l)) * (1. / (s_h + s_l))  [float, float, double→float]
+//   root = rank(A) > rank(B) ? root(A) : root(B), A = start side;  rank += (rank(A) == rank(B))
+struct RunState {
+    float mx, my;
+    int rank, root;
+};
+DOFS_HD inline void step_merge(RunState& s, float fs, float wbx, float wby, double r, int meta, int lrank,
+                               int lroot) {
+    const float tx = s.mx * fs, ty = s.my * fs;
+    s.mx = (float)((double)(tx + wbx) * r);
+    s.my = (float)((double)(ty + wby) * r);
+    const int nroot = (meta & kStepB) ? (s.rank > lrank ? s.root : lroot) : (lrank > s.rank ? lroot : s.root);
+    s.rank = (s.rank == lrank) ? s.rank + 1 : (s.rank > lrank ? s.rank : lrank);
+    s.root = nroot;
 }
 
 // K5 — sequential replay along one heavy path (bottom-up), round `round`: advances until a light
 // child not completed in an earlier round is met (resumed next round) or the path top is done.
 // `list`/`count` select the short-path or the long-path list (the HIP build replays long paths
-// with the wave-cooperative kernel of dofs_hip.hip instead; same state, same results).
+// with the two-wave kernel of dofs_hip.hip instead; same state, same results).
 struct KReplay {
     Ws w;
     int round;
@@ -804,20 +857,33 @@ struct KReplay {
         int q = *curp;
         if (q < 0) return;
         const int64_t lb = f * d.NL;
-        NodeVal run = w.V[lb + w.ord[lb + q + 1]];
+        RunState s;
+        s.mx = w.Rmx[lb + q + 1];
+        s.my = w.Rmy[lb + q + 1];
+        s.rank = w.Rrank[lb + q + 1];
+        s.root = w.Rroot[lb + q + 1];
         for (;;) {
-            const int x = w.ord[lb + q];
-            const int info = w.linfo[lb + q];
-            const int lt = info & kLinfoId;
-            if (w.ready[lb + lt] >= round) {
-                *curp = q;
-                return;
+            const StepIn in = w.In[lb + q];
+            float wbx = in.wbx, wby = in.wby;
+            int lrank = in.lrank, lroot = in.lroot;
+            if (in.meta & kStepDyn) {
+                const int lq = in.lroot;
+                if (w.ready[lb + lq] >= round) {
+                    *curp = q;
+                    return;
+                }
+                wbx = w.Rmx[lb + lq] * (float)in.lrank;
+                wby = w.Rmy[lb + lq] * (float)in.lrank;
+                lrank = w.Rrank[lb + lq];
+                lroot = w.Rroot[lb + lq];
             }
-            const NodeVal lv = w.V[lb + lt];
-            run = (info & kLinfoB) ? merge_vals(run, lv) : merge_vals(lv, run);
-            w.V[lb + x] = run;
-            if (info & kLinfoTop) {
-                w.ready[lb + x] = round;
+            step_merge(s, in.fs, wbx, wby, in.r, in.meta, lrank, lroot);
+            w.Rmx[lb + q] = s.mx;
+            w.Rmy[lb + q] = s.my;
+            w.Rrank[lb + q] = s.rank;
+            w.Rroot[lb + q] = s.root;
+            if (in.meta & kStepTop) {
+                w.ready[lb + q] = round;
                 *curp = -1;
                 return;
             }
@@ -825,6 +891,26 @@ struct KReplay {
         }
     }
 };
+
+// State of merge node x after its merge: replay outputs (by preorder position) + size/bbox (KRT).
+DOFS_HD inline NodeVal node_val(const Ws& w, const int* pre, int f, int64_t x) {
+    const Dims& d = w.d;
+    const int64_t lb = f * d.NL;
+    const int q = pre[lb + x];
+    NodeVal v;
+    v.mx = w.Rmx[lb + q];
+    v.my = w.Rmy[lb + q];
+    v.rank = w.Rrank[lb + q];
+    v.root = w.Rroot[lb + q];
+    v.size = w.SZ[lb + x];
+    const I4 b = w.BB[lb + x];
+    v.x0 = (int16_t)b.x0;
+    v.y0 = (int16_t)b.y0;
+    v.x1 = (int16_t)b.x1;
+    v.y1 = (int16_t)b.y1;
+    v.pad = 0;
+    return v;
+}
 
 // ---------------------------------------------------------------------------------------------
 // K6 — new_merge filters + lifting (graph.cpp:280-356) and the per-slot arg-max.
@@ -838,9 +924,10 @@ DOFS_HD inline double vec_norm(float x, float y) {  // cv::norm(Vec2f)
 
 struct KFilter {
     Ws w;
+    const int* pre;
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
-        const NodeVal v = w.V[f * d.NL + d.N + i];
+        const NodeVal v = node_val(w, pre, f, d.N + i);
         if (v.size < w.min_size) return;
         const int y = v.root / d.W;
         if (y < d.H / 10) return;
@@ -858,11 +945,12 @@ DOFS_HD inline double event_score(const Ws& w, const NodeVal& v, int* cls, dofs_
 
 struct KLift {
     Ws w;
+    const int* pre;
     DOFS_HD void operator()(int f, int64_t j) const {
         const Dims& d = w.d;
         if (j >= w.C(f)[C_CAND]) return;
         const int i = w.cand[f * d.M + j];
-        const NodeVal v = w.V[f * d.NL + d.N + i];
+        const NodeVal v = node_val(w, pre, f, d.N + i);
         double* cs = w.cscore + f * d.M + j;
         *cs = -1.0;
         const double rect_area = (double)((v.x1 - v.x0 + 1) * (v.y1 - v.y0 + 1));
@@ -890,13 +978,14 @@ struct KSlotInit {
 
 struct KSlotEvent {  // first event reaching the slot's maximum wins (strict '<' update, graph.cpp:352)
     Ws w;
+    const int* pre;
     DOFS_HD void operator()(int f, int64_t j) const {
         const Dims& d = w.d;
         if (j >= w.C(f)[C_CAND]) return;
         const double s = w.cscore[f * d.M + j];
         if (!(s > w.score_threshold)) return;
         const int i = w.cand[f * d.M + j];
-        const int root = w.V[f * d.NL + d.N + i].root;
+        const int root = w.Rroot[f * d.NL + pre[f * d.NL + d.N + i]];
         if (dbits(s) == w.sbest[f * d.N + root]) dofs_amin(w.sevent + f * d.N + root, i);
     }
 };
@@ -917,7 +1006,7 @@ struct KSnapshot {
         if (i == kIntMax) return;
         const int k = w.soff[f * d.N + s];
         if (k >= w.snap_cap) return;
-        const NodeVal v = w.V[f * d.NL + d.N + i];
+        const NodeVal v = node_val(w, pre, f, d.N + i);
         dofs_snapshot sn;
         int cls;
         sn.score = event_score(w, v, &cls, &sn.sol);

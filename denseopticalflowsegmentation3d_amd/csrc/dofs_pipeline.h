@@ -118,11 +118,11 @@ struct Pipeline {
         w.lu = (int*)take(4 * B * M);
         w.lv = (int*)take(4 * B * M);
         w.own = (int*)take(4 * B * M);
+        w.lrr = (int*)take(4 * B * M);
         w.MINR = (int*)take(4 * B * M);
         w.parentE = (int*)take(4 * B * M);
         w.childA = (int*)take(4 * B * M);
         w.childB = (int*)take(4 * B * M);
-        w.stamp = (int*)take(4 * B * NL);
         w.P = (int*)take(4 * B * NL);
         w.CS = (int*)take(4 * B * NL);
         w.MX = (int*)take(4 * B * NL);
@@ -134,10 +134,13 @@ struct Pipeline {
         w.anc1 = (int*)take(4 * B * NL);
         w.acc1 = (int*)take(4 * B * NL);
         w.ord = (int*)take(4 * B * NL);
-        w.linfo = (int*)take(4 * B * NL);
         w.isleaf = (int*)take(4 * B * NL);
         w.lscan = (int*)take(4 * B * NL);
-        w.V = (NodeVal*)take(sizeof(NodeVal) * B * NL);
+        w.In = (StepIn*)take(sizeof(StepIn) * B * NL);
+        w.Rmx = (float*)take(4 * B * NL);
+        w.Rmy = (float*)take(4 * B * NL);
+        w.Rrank = (int*)take(4 * B * NL);
+        w.Rroot = (int*)take(4 * B * NL);
         w.ready = (int*)take(4 * B * NL);
         w.LP = (int*)take(4 * B * N);
         w.leaf_order = (int*)take(4 * B * N);
@@ -219,13 +222,12 @@ struct Pipeline {
         be.launch(B, M, KEdgeInit{w});
         be.launch(B, NL, KLabelInit{w});
         be.launch(B, M, KLeafParent{w});
-        int depth = 0;
-        for (int64_t S = (int64_t)1 << ceil_log2(M); S >= 2; S >>= 1, ++depth) {
-            be.launch(B, M, KDncTouch{w, S, depth});
+        for (int64_t S = (int64_t)1 << ceil_log2(M); S >= 2; S >>= 1) {
             be.launch(B, M, KDncUnion{w, S});
             be.launch(B, M, KDncCompress{w, S});
             be.launch(B, M, KDncLRoot{w, S});
-            be.launch(B, M, KDncRelabelR{w, S, depth});
+            be.launch(B, M, KDncRelabelR{w, S});
+            be.launch(B, M, KDncCleanup{w, S});
         }
         be.launch(B, M, KDncParent{w});
         be.launch(B, N, KLeafChild{w});
@@ -254,15 +256,15 @@ struct Pipeline {
         const int RR = ceil_log2(N) + 2;
         for (int r = 0; r < RR; ++r) {
             be.launch(B, N, KReplay{w, r, w.list_short, C_SHORT});
-            be.replay_long(w, r);
+            be.replay_long(w, r);  // HIP: two-wave kernel; emulator: KReplay on the long list
         }
 
         be.mark(6);
         // K6 new_merge filters, lifting, per-slot arg-max, snapshots
-        be.launch(B, M, KFilter{w});
+        be.launch(B, M, KFilter{w, pre});
         be.launch(B, N, KSlotInit{w});
-        be.launch(B, M, KLift{w});
-        be.launch(B, M, KSlotEvent{w});
+        be.launch(B, M, KLift{w, pre});
+        be.launch(B, M, KSlotEvent{w, pre});
         be.launch(B, N, KSlotFlag{w});
         be.scan_excl(w.sflag, w.soff, N, B);
         be.launch(B, 1, KSnapCount{w});
