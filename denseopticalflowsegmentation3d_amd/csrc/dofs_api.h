@@ -257,7 +257,7 @@ int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity
     std::vector<int> eu((size_t)d.M), evv((size_t)d.M), pre((size_t)d.M), rrank((size_t)d.NL), rroot((size_t)d.NL),
         sz((size_t)d.M);
     std::vector<float> rmx((size_t)d.NL), rmy((size_t)d.NL);
-    std::vector<I4> bb((size_t)d.M);
+    std::vector<B4> bb((size_t)d.NL);
     std::vector<unsigned long long> key((size_t)d.M);
     const int64_t fo = (int64_t)frame * d.NL;
     be.d2h(eu.data(), w.EU + (int64_t)frame * d.M, 4 * (size_t)d.M);
@@ -269,7 +269,7 @@ int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity
     be.d2h(rrank.data(), w.Rrank + fo, 4 * (size_t)d.NL);
     be.d2h(rroot.data(), w.Rroot + fo, 4 * (size_t)d.NL);
     be.d2h(sz.data(), w.SZ + fo + d.N, 4 * (size_t)d.M);
-    be.d2h(bb.data(), w.BB + fo + d.N, sizeof(I4) * (size_t)d.M);
+    be.d2h(bb.data(), w.Rbb + fo, sizeof(B4) * (size_t)d.NL);
     be.sync();
     for (int64_t i = 0; i < d.M; ++i) {
         dofs_event& e = ev[i];
@@ -280,10 +280,10 @@ int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity
         e.root = rroot[q];
         e.size = sz[i];
         e.rank = rrank[q];
-        e.bbox[0] = bb[i].x0;
-        e.bbox[1] = bb[i].y0;
-        e.bbox[2] = bb[i].x1;
-        e.bbox[3] = bb[i].y1;
+        e.bbox[0] = bb[q].x0;
+        e.bbox[1] = bb[q].y0;
+        e.bbox[2] = bb[q].x1;
+        e.bbox[3] = bb[q].y1;
         e.mean[0] = rmx[q];
         e.mean[1] = rmy[q];
     }

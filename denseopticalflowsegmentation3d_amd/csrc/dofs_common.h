@@ -24,6 +24,10 @@ struct F2 {
     float x, y;
 };
 
+struct B4 {  // inclusive bbox with 16-bit coordinates (H, W < 32768)
+    int16_t x0, y0, x1, y1;
+};
+
 struct I4 {
     int x0, y0, x1, y1;
 };

@@ -48,8 +48,7 @@ __device__ inline T wave_reduce(T v, Op op) {
 __device__ inline void dofs_amin(int* p, int v);
 __device__ inline void dofs_amax(int* p, int v);
 __device__ inline int dofs_aadd(int* p, int v);
-template <class B4>
-__device__ inline void dofs_agg_size_bbox(int* cs, B4* bb, int key, int val, const B4& b, bool act) {
+__device__ inline void dofs_agg_add(int* base, int key, int val, bool act) {
     const unsigned long long present = __ballot(1);
     const unsigned long long on = __ballot(act);
     if (!on) return;
@@ -58,29 +57,11 @@ __device__ inline void dofs_agg_size_bbox(int* cs, B4* bb, int key, int val, con
         const int leader = __ffsll((long long)on) - 1;
         const int k0 = __shfl(key, leader, 64);
         const bool same = act && key == k0;
-        const int s = wave_reduce(same ? val : 0, [](int a, int c) { return a + c; });
-        const int x0 = wave_reduce(same ? b.x0 : 0x7fffffff, [](int a, int c) { return a < c ? a : c; });
-        const int y0 = wave_reduce(same ? b.y0 : 0x7fffffff, [](int a, int c) { return a < c ? a : c; });
-        const int x1 = wave_reduce(same ? b.x1 : -1, [](int a, int c) { return a > c ? a : c; });
-        const int y1 = wave_reduce(same ? b.y1 : -1, [](int a, int c) { return a > c ? a : c; });
-        if (wave_lane() == leader) {
-            atomicAdd(cs + k0, s);
-            B4* a = bb + k0;
-            if (__hip_atomic_load(&a->x0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > x0) atomicMin(&a->x0, x0);
-            if (__hip_atomic_load(&a->y0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > y0) atomicMin(&a->y0, y0);
-            if (__hip_atomic_load(&a->x1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < x1) atomicMax(&a->x1, x1);
-            if (__hip_atomic_load(&a->y1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < y1) atomicMax(&a->y1, y1);
-        }
+        const int sum = wave_reduce(same ? val : 0, [](int x, int y) { return x + y; });
+        if (wave_lane() == leader) atomicAdd(base + k0, sum);
         done = same;
     }
-    if (act && !done) {
-        atomicAdd(cs + key, val);
-        B4* a = bb + key;
-        atomicMin(&a->x0, b.x0);
-        atomicMin(&a->y0, b.y0);
-        atomicMax(&a->x1, b.x1);
-        atomicMax(&a->y1, b.y1);
-    }
+    if (act && !done) atomicAdd(base + key, val);
 }
 template <bool kMax>
 __device__ inline void agg_minmax(int* base, int key, int val, bool act) {
@@ -133,16 +114,18 @@ __global__ __launch_bounds__(kBlock) void k_generic(F f, int64_t n) {
 // reads step k with uniform LDS loads and writes step k's output to LDS; one coalesced store per
 // chunk writes the outputs back by preorder position.
 // ---------------------------------------------------------------------------------------------
-struct LongStep {  // resolved inputs of one step, one channel (32 B)
+struct LongStep {  // resolved inputs of one step for one wave (32 B)
     float fs;
-    float wb;
-    int meta;  // StepIn meta | kLongOk (inputs ready)
+    float wb;   // light child's weighted flow for this wave's channel
+    int meta;   // StepIn meta | kLongOk (inputs ready)
     int pad;
     double r;
-    int lrank;
-    int lroot;
+    int la;     // wave 0: light rank; wave 1: light bbox (x0 | y0 << 16)
+    int lb;     // wave 0: light root; wave 1: light bbox (x1 | y1 << 16)
 };
 constexpr int kLongOk = 8;
+
+__device__ inline int pack_xy(int x, int y) { return (x & 0xffff) | (y << 16); }
 
 __device__ inline LongStep long_resolve(const Ws& w, int64_t lb, int p, int top, int round, int ch) {
     LongStep s;
@@ -150,8 +133,8 @@ __device__ inline LongStep long_resolve(const Ws& w, int64_t lb, int p, int top,
     s.fs = 0.f;
     s.wb = 0.f;
     s.r = 0.0;
-    s.lrank = 0;
-    s.lroot = 0;
+    s.la = 0;
+    s.lb = 0;
     s.pad = 0;
     if (p < top) return s;
     const StepIn in = w.In[lb + p];
@@ -159,26 +142,32 @@ __device__ inline LongStep long_resolve(const Ws& w, int64_t lb, int p, int top,
     s.r = in.r;
     s.meta = in.meta;
     if (in.meta & kStepDyn) {
-        const int lq = in.lroot;
+        const int lq = in.lb;
         if (w.ready[lb + lq] >= round) return s;  // not ok: light child completes in a later round
-        s.wb = (ch ? w.Rmy[lb + lq] : w.Rmx[lb + lq]) * (float)in.lrank;
-        s.lrank = w.Rrank[lb + lq];
-        s.lroot = w.Rroot[lb + lq];
+        s.wb = (ch ? w.Rmy[lb + lq] : w.Rmx[lb + lq]) * (float)in.la;
+        if (ch) {
+            const B4 b = w.Rbb[lb + lq];
+            s.la = pack_xy(b.x0, b.y0);
+            s.lb = pack_xy(b.x1, b.y1);
+        } else {
+            s.la = w.Rrank[lb + lq];
+            s.lb = w.Rroot[lb + lq];
+        }
     } else {
         s.wb = ch ? in.wby : in.wbx;
-        s.lrank = in.lrank;
-        s.lroot = in.lroot;
+        s.la = ch ? in.la : 0;     // pixel light child: rank 0 / bbox = its coordinates
+        s.lb = ch ? in.la : in.lb;
     }
     s.meta |= kLongOk;
     return s;
 }
 
 __device__ void replay_long_path(const Ws& w, int f, int jj, int round, LongStep (*buf)[2][64], float (*res)[64],
-                                 int (*resi)[2][64]) {
+                                 int (*resi)[64]) {
     const Dims& d = w.d;
     const int j = w.list_long[f * d.N + jj];
     int* curp = w.cur + f * d.N + j;
-    const int wv = threadIdx.x >> 6;  // channel
+    const int wv = threadIdx.x >> 6;  // 0: mean x + rank + root, 1: mean y + bbox
     const int lane = threadIdx.x & 63;
     int q = *curp;
     const int top = w.ptop[f * d.N + j];
@@ -186,60 +175,89 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, LongStep
     if (q < 0) return;
     const int64_t lb = f * d.NL;
     float m = wv ? w.Rmy[lb + q + 1] : w.Rmx[lb + q + 1];
-    int rank = w.Rrank[lb + q + 1], root = w.Rroot[lb + q + 1];
+    int a0, a1, a2, a3;  // wave 0: rank, root; wave 1: bbox x0, y0, x1, y1
+    if (wv == 0) {
+        a0 = w.Rrank[lb + q + 1];
+        a1 = w.Rroot[lb + q + 1];
+        a2 = a3 = 0;
+    } else {
+        const B4 b = w.Rbb[lb + q + 1];
+        a0 = b.x0;
+        a1 = b.y0;
+        a2 = b.x1;
+        a3 = b.y1;
+    }
     int cb = 0;
-    buf[wv][cb][lane] = long_resolve(w, lb, q - lane, top, round, wv);
+    LongStep mine = long_resolve(w, lb, q - lane, top, round, wv);
+    buf[wv][cb][lane] = mine;
     for (;;) {
         const LongStep nx = long_resolve(w, lb, q - 64 - lane, top, round, wv);  // next chunk in flight
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS staging is visible
+        // steps to run in this chunk: up to the first blocked position or through the path top
+        const unsigned long long blocked = __ballot(!(mine.meta & kLongOk));
+        const unsigned long long tops = __ballot((mine.meta & kLongOk) && (mine.meta & kStepTop));
+        const int fb = blocked ? __ffsll((long long)blocked) - 1 : 64;
+        const int ft = tops ? __ffsll((long long)tops) - 1 : 64;
+        const int finished = ft < fb;
+        const int n = finished ? ft + 1 : fb;
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS staging has landed
         __builtin_amdgcn_wave_barrier();
         const LongStep* b = buf[wv][cb];
-        int done = 64, finished = 0;
+        if (wv == 0) {
 #pragma unroll 8
-        for (int k = 0; k < 64; ++k) {
-            const LongStep st = b[k];
-            if (!(st.meta & kLongOk)) {
-                done = k;
-                break;
+            for (int k = 0; k < n; ++k) {
+                const LongStep st = b[k];
+                m = (float)((double)(m * st.fs + st.wb) * st.r);
+                const int nroot = (st.meta & kStepB) ? (a0 > st.la ? a1 : st.lb) : (st.la > a0 ? st.lb : a1);
+                a0 = (a0 == st.la) ? a0 + 1 : (a0 > st.la ? a0 : st.la);
+                a1 = nroot;
+                res[0][k] = m;
+                resi[0][k] = a0;
+                resi[1][k] = a1;
             }
-            const float t = m * st.fs;
-            m = (float)((double)(t + st.wb) * st.r);
-            res[wv][k] = m;
-            if (wv == 0) {
-                const int nroot = (st.meta & kStepB) ? (rank > st.lrank ? root : st.lroot)
-                                                     : (st.lrank > rank ? st.lroot : root);
-                rank = (rank == st.lrank) ? rank + 1 : (rank > st.lrank ? rank : st.lrank);
-                root = nroot;
-                resi[0][0][k] = rank;
-                resi[0][1][k] = root;
-            }
-            if (st.meta & kStepTop) {
-                done = k + 1;
-                finished = 1;
-                break;
+        } else {
+#pragma unroll 8
+            for (int k = 0; k < n; ++k) {
+                const LongStep st = b[k];
+                m = (float)((double)(m * st.fs + st.wb) * st.r);
+                const int lx0 = (int16_t)(st.la & 0xffff), ly0 = st.la >> 16;
+                const int lx1 = (int16_t)(st.lb & 0xffff), ly1 = st.lb >> 16;
+                a0 = lx0 < a0 ? lx0 : a0;
+                a1 = ly0 < a1 ? ly0 : a1;
+                a2 = lx1 > a2 ? lx1 : a2;
+                a3 = ly1 > a3 ? ly1 : a3;
+                res[1][k] = m;
+                resi[2][k] = pack_xy(a0, a1);
+                resi[3][k] = pack_xy(a2, a3);
             }
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
-        if (lane < done) {
+        if (lane < n) {
             const int p = q - lane;
             if (wv) {
                 w.Rmy[lb + p] = res[1][lane];
+                const int lo = resi[2][lane], hi = resi[3][lane];
+                B4 bb;
+                bb.x0 = (int16_t)(lo & 0xffff);
+                bb.y0 = (int16_t)(lo >> 16);
+                bb.x1 = (int16_t)(hi & 0xffff);
+                bb.y1 = (int16_t)(hi >> 16);
+                w.Rbb[lb + p] = bb;
             } else {
                 w.Rmx[lb + p] = res[0][lane];
-                w.Rrank[lb + p] = resi[0][0][lane];
-                w.Rroot[lb + p] = resi[0][1][lane];
+                w.Rrank[lb + p] = resi[0][lane];
+                w.Rroot[lb + p] = resi[1][lane];
             }
         }
-        if (finished || done < 64) {
-            // both waves stop at the same step (same inputs); the top's readiness is read only in
+        if (n < 64 || finished) {
+            // both waves stop at the same step (same flags); the top's readiness is read only in
             // later rounds (kernel boundary), so either wave may publish it
             if (wv == 0 && lane == 0) {
                 if (finished) {
-                    w.ready[lb + q - done + 1] = round;
+                    w.ready[lb + q - n + 1] = round;
                     *curp = -1;
                 } else {
-                    *curp = q - done;
+                    *curp = q - n;
                 }
             }
             __syncthreads();
@@ -247,14 +265,15 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, LongStep
         }
         q -= 64;
         cb ^= 1;
-        buf[wv][cb][lane] = nx;
+        mine = nx;
+        buf[wv][cb][lane] = mine;
     }
 }
 
 __global__ __launch_bounds__(128) void k_replay_long(Ws w, int round) {
     __shared__ LongStep buf[2][2][64];
     __shared__ float res[2][64];
-    __shared__ int resi[1][2][64];
+    __shared__ int resi[4][64];
     const int f = blockIdx.y;
     const int n = w.C(f)[C_LONG];
     for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path(w, f, jj, round, buf, res, resi);

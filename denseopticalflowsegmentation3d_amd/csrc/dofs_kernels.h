@@ -27,16 +27,17 @@ namespace dofs {
 // Inputs of the merge at preorder position q (node x, heavy child h, light child l), precomputed in
 // parallel; the replay then only carries the order-dependent state (mean, rank, root).
 //   fs = (float)size(h)      r = 1 / (double)size(x)
-//   wb = float(mean(l) * (float)size(l))  — static when l is a pixel; when l is a merge node
-//        (kStepDyn) its mean is produced by the replay itself: lrank holds size(l) and lroot its
-//        preorder position, and wb / rank / root are read once l's path has completed.
+//   wb = float(mean(l) * (float)size(l))  — static when l is a pixel (la = its x | y << 16,
+//        lb = its id: rank 0, root = itself); when l is a merge node (kStepDyn) its mean, rank,
+//        root and bbox are produced by the replay itself: la holds size(l) and lb its preorder
+//        position, and they are read once l's path has completed.
 struct StepIn {
     float fs;
     float wbx, wby;
     int meta;
     double r;
-    int lrank;
-    int lroot;
+    int la;
+    int lb;
 };
 static_assert(sizeof(StepIn) == 32, "StepIn is one 32-byte record");
 constexpr int kStepB = 1;    // light child is the end side (B) of the merge
@@ -81,9 +82,7 @@ struct Ws {
     int* P;
     int* CS;
     int* MX;
-    I4* BBacc;
     int* SZ;
-    I4* BB;
     int* anc0;
     int* acc0;
     int* anc1;
@@ -96,6 +95,7 @@ struct Ws {
     float* Rmy;
     int* Rrank;
     int* Rroot;
+    B4* Rbb;
     int* ready;
     // per pixel (stride N)
     int* LP;
@@ -452,7 +452,7 @@ struct KEdgeInit {
     }
 };
 
-struct KLabelInit {
+struct KLabelInit {  // clean label state (P[x] = x, MX = -1, CS = 0), pixel sizes, root size
     Ws w;
     DOFS_HD void operator()(int f, int64_t x) const {
         const Dims& d = w.d;
@@ -460,30 +460,11 @@ struct KLabelInit {
         w.P[o] = (int)x;
         w.MX[o] = -1;
         w.CS[o] = 0;
-        I4 e;
-        e.x0 = kIntMax;
-        e.y0 = kIntMax;
-        e.x1 = -1;
-        e.y1 = -1;
-        w.BBacc[o] = e;
         if (x < d.N) {
-            const int px = (int)(x % d.W), py = (int)(x / d.W);
             w.SZ[o] = 1;
-            I4 b;
-            b.x0 = px;
-            b.y0 = py;
-            b.x1 = px;
-            b.y1 = py;
-            w.BB[o] = b;
             w.LP[f * d.N + x] = kIntMax;
         } else if (x == d.NL - 1) {  // KRT root = last merge: the whole frame
             w.SZ[o] = (int)d.N;
-            I4 b;
-            b.x0 = 0;
-            b.y0 = 0;
-            b.x1 = d.W - 1;
-            b.y1 = d.H - 1;
-            w.BB[o] = b;
         }
     }
 };
@@ -569,10 +550,10 @@ struct KDncCompress {
         const int64_t lb = f * d.NL;
         const int h = w.own[o];
         const int r = walk_compress(w.P + lb, h);
-        // component size / bbox over the labels hooked in it (the root label is added by the
-        // L-root edge) and the max L-edge rank; wave-aggregated: a big component's root is the
-        // key of most lanes at the top levels
-        dofs_agg_size_bbox(w.CS + lb, w.BBacc + lb, r, w.SZ[lb + h], w.BB[lb + h], true);
+        // component size over the labels hooked in it (the root label is added by the L-root
+        // edge) and the max L-edge rank; wave-aggregated: a big component's root is the key of
+        // most lanes at the top levels
+        dofs_agg_add(w.CS + lb, r, w.SZ[lb + h], true);
         dofs_agg_max(w.MX + lb, r, (int)i, true);
     }
 };
@@ -592,13 +573,6 @@ struct KDncLRoot {
         }
         w.lrr[o] = r;
         w.SZ[lb + d.N + i] = w.CS[lb + r] + w.SZ[lb + r];
-        const I4 a = w.BBacc[lb + r], b = w.BB[lb + r];
-        I4 m;
-        m.x0 = a.x0 < b.x0 ? a.x0 : b.x0;
-        m.y0 = a.y0 < b.y0 ? a.y0 : b.y0;
-        m.x1 = a.x1 > b.x1 ? a.x1 : b.x1;
-        m.y1 = a.y1 > b.y1 ? a.y1 : b.y1;
-        w.BB[lb + d.N + i] = m;
     }
 };
 
@@ -624,7 +598,7 @@ struct KDncRelabelR {
     }
 };
 
-struct KDncCleanup {  // restore the clean label state (P[x] = x, MX = -1, CS = 0, BBacc = empty)
+struct KDncCleanup {  // restore the clean label state (P[x] = x, MX = -1, CS = 0)
     Ws w;
     int64_t S;
     DOFS_HD void operator()(int f, int64_t i) const {
@@ -638,12 +612,6 @@ struct KDncCleanup {  // restore the clean label state (P[x] = x, MX = -1, CS = 
         if (r >= 0) {
             w.MX[lb + r] = -1;
             w.CS[lb + r] = 0;
-            I4 e;
-            e.x0 = kIntMax;
-            e.y0 = kIntMax;
-            e.x1 = -1;
-            e.y1 = -1;
-            w.BBacc[lb + r] = e;
         }
     }
 };
@@ -791,13 +759,13 @@ struct KPathInit {
                 const F2 v = w.blur[f * d.N + lt];
                 in.wbx = v.x * (float)1;
                 in.wby = v.y * (float)1;
-                in.lrank = 0;
-                in.lroot = lt;
+                in.la = (lt % d.W) | ((lt / d.W) << 16);
+                in.lb = lt;
             } else {
                 in.meta |= kStepDyn;
                 in.wbx = in.wby = 0.f;
-                in.lrank = w.SZ[lb + lt];
-                in.lroot = pre[lb + lt];
+                in.la = w.SZ[lb + lt];
+                in.lb = pre[lb + lt];
             }
             w.In[lb + q] = in;
             w.ready[lb + q] = kIntMax;
@@ -818,6 +786,10 @@ struct KPathInit {
             w.Rmy[lb + q] = v.y;
             w.Rrank[lb + q] = 0;
             w.Rroot[lb + q] = (int)x;
+            B4 b;
+            b.x0 = b.x1 = (int16_t)(x % d.W);
+            b.y0 = b.y1 = (int16_t)(x / d.W);
+            w.Rbb[lb + q] = b;
             w.ready[lb + q] = -1;
         }
     }
@@ -829,15 +801,20 @@ struct KPathInit {
 struct RunState {
     float mx, my;
     int rank, root;
+    B4 bb;
 };
 DOFS_HD inline void step_merge(RunState& s, float fs, float wbx, float wby, double r, int meta, int lrank,
-                               int lroot) {
+                               int lroot, B4 lbb) {
     const float tx = s.mx * fs, ty = s.my * fs;
     s.mx = (float)((double)(tx + wbx) * r);
     s.my = (float)((double)(ty + wby) * r);
     const int nroot = (meta & kStepB) ? (s.rank > lrank ? s.root : lroot) : (lrank > s.rank ? lroot : s.root);
     s.rank = (s.rank == lrank) ? s.rank + 1 : (s.rank > lrank ? s.rank : lrank);
     s.root = nroot;
+    s.bb.x0 = lbb.x0 < s.bb.x0 ? lbb.x0 : s.bb.x0;  // graph.cpp:197-207
+    s.bb.y0 = lbb.y0 < s.bb.y0 ? lbb.y0 : s.bb.y0;
+    s.bb.x1 = lbb.x1 > s.bb.x1 ? lbb.x1 : s.bb.x1;
+    s.bb.y1 = lbb.y1 > s.bb.y1 ? lbb.y1 : s.bb.y1;
 }
 
 // K5 — sequential replay along one heavy path (bottom-up), round `round`: advances until a light
@@ -862,26 +839,33 @@ struct KReplay {
         s.my = w.Rmy[lb + q + 1];
         s.rank = w.Rrank[lb + q + 1];
         s.root = w.Rroot[lb + q + 1];
+        s.bb = w.Rbb[lb + q + 1];
         for (;;) {
             const StepIn in = w.In[lb + q];
             float wbx = in.wbx, wby = in.wby;
-            int lrank = in.lrank, lroot = in.lroot;
+            int lrank = 0, lroot = in.lb;
+            B4 lbb;
             if (in.meta & kStepDyn) {
-                const int lq = in.lroot;
+                const int lq = in.lb;
                 if (w.ready[lb + lq] >= round) {
                     *curp = q;
                     return;
                 }
-                wbx = w.Rmx[lb + lq] * (float)in.lrank;
-                wby = w.Rmy[lb + lq] * (float)in.lrank;
+                wbx = w.Rmx[lb + lq] * (float)in.la;
+                wby = w.Rmy[lb + lq] * (float)in.la;
                 lrank = w.Rrank[lb + lq];
                 lroot = w.Rroot[lb + lq];
+                lbb = w.Rbb[lb + lq];
+            } else {
+                lbb.x0 = lbb.x1 = (int16_t)(in.la & 0xffff);
+                lbb.y0 = lbb.y1 = (int16_t)(in.la >> 16);
             }
-            step_merge(s, in.fs, wbx, wby, in.r, in.meta, lrank, lroot);
+            step_merge(s, in.fs, wbx, wby, in.r, in.meta, lrank, lroot, lbb);
             w.Rmx[lb + q] = s.mx;
             w.Rmy[lb + q] = s.my;
             w.Rrank[lb + q] = s.rank;
             w.Rroot[lb + q] = s.root;
+            w.Rbb[lb + q] = s.bb;
             if (in.meta & kStepTop) {
                 w.ready[lb + q] = round;
                 *curp = -1;
@@ -903,11 +887,11 @@ DOFS_HD inline NodeVal node_val(const Ws& w, const int* pre, int f, int64_t x) {
     v.rank = w.Rrank[lb + q];
     v.root = w.Rroot[lb + q];
     v.size = w.SZ[lb + x];
-    const I4 b = w.BB[lb + x];
-    v.x0 = (int16_t)b.x0;
-    v.y0 = (int16_t)b.y0;
-    v.x1 = (int16_t)b.x1;
-    v.y1 = (int16_t)b.y1;
+    const B4 b = w.Rbb[lb + q];
+    v.x0 = b.x0;
+    v.y0 = b.y0;
+    v.x1 = b.x1;
+    v.y1 = b.y1;
     v.pad = 0;
     return v;
 }

@@ -126,9 +126,7 @@ struct Pipeline {
         w.P = (int*)take(4 * B * NL);
         w.CS = (int*)take(4 * B * NL);
         w.MX = (int*)take(4 * B * NL);
-        w.BBacc = (I4*)take(sizeof(I4) * B * NL);
         w.SZ = (int*)take(4 * B * NL);
-        w.BB = (I4*)take(sizeof(I4) * B * NL);
         w.anc0 = (int*)take(4 * B * NL);
         w.acc0 = (int*)take(4 * B * NL);
         w.anc1 = (int*)take(4 * B * NL);
@@ -141,6 +139,7 @@ struct Pipeline {
         w.Rmy = (float*)take(4 * B * NL);
         w.Rrank = (int*)take(4 * B * NL);
         w.Rroot = (int*)take(4 * B * NL);
+        w.Rbb = (B4*)take(sizeof(B4) * B * NL);
         w.ready = (int*)take(4 * B * NL);
         w.LP = (int*)take(4 * B * N);
         w.leaf_order = (int*)take(4 * B * N);

@@ -37,18 +37,8 @@ inline int dofs_aadd(int* p, int v) {
     return o;
 }
 inline void dofs_aor(int* p, int v) { *p |= v; }
-namespace dofs {
-struct I4;
-}
-template <class B>
-inline void dofs_agg_size_bbox(int* cs, B* bb, int key, int val, const B& b, bool act) {
-    if (!act) return;
-    cs[key] += val;
-    B& a = bb[key];
-    a.x0 = std::min(a.x0, b.x0);
-    a.y0 = std::min(a.y0, b.y0);
-    a.x1 = std::max(a.x1, b.x1);
-    a.y1 = std::max(a.y1, b.y1);
+inline void dofs_agg_add(int* base, int key, int val, bool act) {
+    if (act) base[key] += val;
 }
 inline void dofs_agg_max(int* base, int key, int val, bool act) {
     if (act) base[key] = std::max(base[key], val);
