@@ -104,155 +104,199 @@ __global__ __launch_bounds__(kBlock) void k_generic(F f, int64_t n) {
 
 
 // ---------------------------------------------------------------------------------------------
-// K5 (long heavy paths): two wave64s per path, one per mean channel (wave 0 also carries rank and
-// root on the side). The float running mean of Forest::merge (graph.cpp:184-190) is a strictly
-// sequential recurrence — mul, add (f32), cvt, mul (f64), cvt per merge — whose roundings must be
-// replayed in Kruskal order; splitting the two channels over two SIMDs halves the issue load of the
-// latency-bound chain (tools/replay_micro.hip: 41 vs 54 ns per step for one wave doing both).
-// Per 64-step chunk every lane resolves one position's inputs (StepIn, plus the light child's
-// replay output when it is a merge node) into LDS while the previous chunk is consumed; the chain
-// reads step k with uniform LDS loads and writes step k's output to LDS; one coalesced store per
-// chunk writes the outputs back by preorder position.
+// K5 (long heavy paths): three wave64s per path. The float running mean of Forest::merge
+// (graph.cpp:184-190) is a strictly sequential recurrence — f32 mul, f32 add, cvt, f64 mul, cvt per
+// merge — whose roundings must be replayed in Kruskal order. Waves 0 and 1 carry only that chain
+// (mean x, mean y; one per SIMD: tools/replay_micro.hip measured 41 ns/step against 54 for one wave
+// doing both); wave 2 carries the union-by-rank rank/root recurrence and the bbox. Per 64-step
+// chunk every lane resolves one position's inputs (StepIn, plus the light child's replay output
+// when it is a merge node) into its wave's LDS records while the previous chunk is consumed; the
+// chains read step k with uniform LDS loads and write step k's output to LDS; one coalesced store
+// per chunk writes the outputs back by preorder position.
 // ---------------------------------------------------------------------------------------------
-struct LongStep {  // resolved inputs of one step for one wave (32 B)
+struct ChainRec {  // wave 0/1 step record (16 B)
     float fs;
-    float wb;   // light child's weighted flow for this wave's channel
-    int meta;   // StepIn meta | kLongOk (inputs ready)
-    int pad;
+    float wb;
     double r;
-    int la;     // wave 0: light rank; wave 1: light bbox (x0 | y0 << 16)
-    int lb;     // wave 0: light root; wave 1: light bbox (x1 | y1 << 16)
+};
+struct SideRec {  // wave 2 step record (16 B)
+    int meta;     // StepIn meta | kLongOk
+    int lrank;
+    int lroot;
+    int pad;
 };
 constexpr int kLongOk = 8;
 
-__device__ inline int pack_xy(int x, int y) { return (x & 0xffff) | (y << 16); }
+struct LongShared {
+    ChainRec chain[2][2][64];  // [wave][buffer][step]
+    SideRec side[2][64];       // [buffer][step]
+    float mean[2][64];         // [wave][step] chain outputs
+    int rank[64], root[64];    // wave 2 outputs
+};
 
-__device__ inline LongStep long_resolve(const Ws& w, int64_t lb, int p, int top, int round, int ch) {
-    LongStep s;
-    s.meta = 0;
-    s.fs = 0.f;
-    s.wb = 0.f;
-    s.r = 0.0;
-    s.la = 0;
-    s.lb = 0;
-    s.pad = 0;
-    if (p < top) return s;
+// Resolve position p for wave `wv`. Returns the meta flags (kLongOk when the inputs are ready).
+__device__ inline int long_resolve(const Ws& w, int64_t lb, int p, int top, int round, int wv, ChainRec* cr,
+                                   SideRec* sr, B4* lbb) {
+    lbb->x0 = lbb->y0 = 0x7fff;  // neutral for the bbox scan (positions past the stop)
+    lbb->x1 = lbb->y1 = -1;
+    if (p < top) return 0;
     const StepIn in = w.In[lb + p];
-    s.fs = in.fs;
-    s.r = in.r;
-    s.meta = in.meta;
+    int meta = in.meta;
+    float wb;
+    int lrank = 0, lroot = in.lb;
     if (in.meta & kStepDyn) {
         const int lq = in.lb;
-        if (w.ready[lb + lq] >= round) return s;  // not ok: light child completes in a later round
-        s.wb = (ch ? w.Rmy[lb + lq] : w.Rmx[lb + lq]) * (float)in.la;
-        if (ch) {
-            const B4 b = w.Rbb[lb + lq];
-            s.la = pack_xy(b.x0, b.y0);
-            s.lb = pack_xy(b.x1, b.y1);
+        if (w.ready[lb + lq] >= round) return meta;  // light child completes in a later round
+        if (wv < 2) {
+            wb = (wv ? w.Rmy[lb + lq] : w.Rmx[lb + lq]) * (float)in.la;
         } else {
-            s.la = w.Rrank[lb + lq];
-            s.lb = w.Rroot[lb + lq];
+            wb = 0.f;
+            lrank = w.Rrank[lb + lq];
+            lroot = w.Rroot[lb + lq];
+            *lbb = w.Rbb[lb + lq];
         }
     } else {
-        s.wb = ch ? in.wby : in.wbx;
-        s.la = ch ? in.la : 0;     // pixel light child: rank 0 / bbox = its coordinates
-        s.lb = ch ? in.la : in.lb;
+        wb = wv ? in.wby : in.wbx;
+        if (wv == 2) {
+            lbb->x0 = lbb->x1 = (int16_t)(in.la & 0xffff);
+            lbb->y0 = lbb->y1 = (int16_t)(in.la >> 16);
+        }
     }
-    s.meta |= kLongOk;
-    return s;
+    meta |= kLongOk;
+    if (wv < 2) {
+        cr->fs = in.fs;
+        cr->wb = wb;
+        cr->r = in.r;
+    } else {
+        sr->meta = meta;
+        sr->lrank = lrank;
+        sr->lroot = lroot;
+        sr->pad = 0;
+    }
+    return meta;
 }
 
-__device__ void replay_long_path(const Ws& w, int f, int jj, int round, LongStep (*buf)[2][64], float (*res)[64],
-                                 int (*resi)[64]) {
+__device__ inline B4 bb_join(B4 a, B4 b) {
+    B4 r;
+    r.x0 = a.x0 < b.x0 ? a.x0 : b.x0;
+    r.y0 = a.y0 < b.y0 ? a.y0 : b.y0;
+    r.x1 = a.x1 > b.x1 ? a.x1 : b.x1;
+    r.y1 = a.y1 > b.y1 ? a.y1 : b.y1;
+    return r;
+}
+__device__ inline B4 bb_shfl_up(B4 b, int delta) {
+    const int lo = __shfl_up((int)((unsigned short)b.x0 | ((unsigned)(unsigned short)b.y0 << 16)), delta, 64);
+    const int hi = __shfl_up((int)((unsigned short)b.x1 | ((unsigned)(unsigned short)b.y1 << 16)), delta, 64);
+    B4 r;
+    r.x0 = (int16_t)(lo & 0xffff);
+    r.y0 = (int16_t)(lo >> 16);
+    r.x1 = (int16_t)(hi & 0xffff);
+    r.y1 = (int16_t)(hi >> 16);
+    return r;
+}
+
+__device__ void replay_long_path(const Ws& w, int f, int jj, int round, LongShared& sh) {
     const Dims& d = w.d;
     const int j = w.list_long[f * d.N + jj];
     int* curp = w.cur + f * d.N + j;
-    const int wv = threadIdx.x >> 6;  // 0: mean x + rank + root, 1: mean y + bbox
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform role
     const int lane = threadIdx.x & 63;
     int q = *curp;
     const int top = w.ptop[f * d.N + j];
-    __syncthreads();  // both waves have read the cursor before wave 0 may rewrite it
+    __syncthreads();  // every wave has read the cursor before it may be rewritten
     if (q < 0) return;
     const int64_t lb = f * d.NL;
-    float m = wv ? w.Rmy[lb + q + 1] : w.Rmx[lb + q + 1];
-    int a0, a1, a2, a3;  // wave 0: rank, root; wave 1: bbox x0, y0, x1, y1
-    if (wv == 0) {
-        a0 = w.Rrank[lb + q + 1];
-        a1 = w.Rroot[lb + q + 1];
-        a2 = a3 = 0;
-    } else {
-        const B4 b = w.Rbb[lb + q + 1];
-        a0 = b.x0;
-        a1 = b.y0;
-        a2 = b.x1;
-        a3 = b.y1;
+    float m = 0.f;
+    int rank = 0, root = 0;
+    B4 bb;
+    bb.x0 = bb.y0 = bb.x1 = bb.y1 = 0;
+    if (wv == 0) m = w.Rmx[lb + q + 1];
+    if (wv == 1) m = w.Rmy[lb + q + 1];
+    if (wv == 2) {
+        rank = w.Rrank[lb + q + 1];
+        root = w.Rroot[lb + q + 1];
+        bb = w.Rbb[lb + q + 1];
     }
     int cb = 0;
-    LongStep mine = long_resolve(w, lb, q - lane, top, round, wv);
-    buf[wv][cb][lane] = mine;
+    ChainRec cr;
+    SideRec sr;
+    B4 lbb;
+    int meta = long_resolve(w, lb, q - lane, top, round, wv, &cr, &sr, &lbb);
+    if (wv < 2)
+        sh.chain[wv][cb][lane] = cr;
+    else
+        sh.side[cb][lane] = sr;
     for (;;) {
-        const LongStep nx = long_resolve(w, lb, q - 64 - lane, top, round, wv);  // next chunk in flight
+        ChainRec ncr;
+        SideRec nsr;
+        B4 nlbb;
+        const int nmeta = long_resolve(w, lb, q - 64 - lane, top, round, wv, &ncr, &nsr, &nlbb);
         // steps to run in this chunk: up to the first blocked position or through the path top
-        const unsigned long long blocked = __ballot(!(mine.meta & kLongOk));
-        const unsigned long long tops = __ballot((mine.meta & kLongOk) && (mine.meta & kStepTop));
+        const unsigned long long blocked = __ballot(!(meta & kLongOk));
+        const unsigned long long tops = __ballot((meta & kLongOk) && (meta & kStepTop));
         const int fb = blocked ? __ffsll((long long)blocked) - 1 : 64;
         const int ft = tops ? __ffsll((long long)tops) - 1 : 64;
         const int finished = ft < fb;
         const int n = finished ? ft + 1 : fb;
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS staging has landed
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS records have landed
         __builtin_amdgcn_wave_barrier();
-        const LongStep* b = buf[wv][cb];
-        if (wv == 0) {
+        if (wv < 2) {
+            const ChainRec* c = sh.chain[wv][cb];
+            float* out = sh.mean[wv];
 #pragma unroll 8
             for (int k = 0; k < n; ++k) {
-                const LongStep st = b[k];
+                const ChainRec st = c[k];
                 m = (float)((double)(m * st.fs + st.wb) * st.r);
-                const int nroot = (st.meta & kStepB) ? (a0 > st.la ? a1 : st.lb) : (st.la > a0 ? st.lb : a1);
-                a0 = (a0 == st.la) ? a0 + 1 : (a0 > st.la ? a0 : st.la);
-                a1 = nroot;
-                res[0][k] = m;
-                resi[0][k] = a0;
-                resi[1][k] = a1;
+                out[k] = m;
             }
         } else {
+            const SideRec* c = sh.side[cb];
 #pragma unroll 8
             for (int k = 0; k < n; ++k) {
-                const LongStep st = b[k];
-                m = (float)((double)(m * st.fs + st.wb) * st.r);
-                const int lx0 = (int16_t)(st.la & 0xffff), ly0 = st.la >> 16;
-                const int lx1 = (int16_t)(st.lb & 0xffff), ly1 = st.lb >> 16;
-                a0 = lx0 < a0 ? lx0 : a0;
-                a1 = ly0 < a1 ? ly0 : a1;
-                a2 = lx1 > a2 ? lx1 : a2;
-                a3 = ly1 > a3 ? ly1 : a3;
-                res[1][k] = m;
-                resi[2][k] = pack_xy(a0, a1);
-                resi[3][k] = pack_xy(a2, a3);
+                const SideRec st = c[k];
+                const int nroot = (st.meta & kStepB) ? (rank > st.lrank ? root : st.lroot)
+                                                     : (st.lrank > rank ? st.lroot : root);
+                rank = (rank == st.lrank) ? rank + 1 : (rank > st.lrank ? rank : st.lrank);
+                root = nroot;
+                sh.rank[k] = rank;
+                sh.root[k] = root;
+            }
+            // bbox: inclusive prefix join over the chunk (lane = step), then the carried box
+            B4 x = lbb;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const B4 y = bb_shfl_up(x, o);
+                if (lane >= o) x = bb_join(x, y);
+            }
+            x = bb_join(x, bb);
+            if (lane < n) w.Rbb[lb + q - lane] = x;
+            {
+                const int src = n > 0 ? n - 1 : 0;
+                const int lo = __shfl((int)((unsigned short)x.x0 | ((unsigned)(unsigned short)x.y0 << 16)), src, 64);
+                const int hi = __shfl((int)((unsigned short)x.x1 | ((unsigned)(unsigned short)x.y1 << 16)), src, 64);
+                if (n > 0) {
+                    bb.x0 = (int16_t)(lo & 0xffff);
+                    bb.y0 = (int16_t)(lo >> 16);
+                    bb.x1 = (int16_t)(hi & 0xffff);
+                    bb.y1 = (int16_t)(hi >> 16);
+                }
             }
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
         if (lane < n) {
             const int p = q - lane;
-            if (wv) {
-                w.Rmy[lb + p] = res[1][lane];
-                const int lo = resi[2][lane], hi = resi[3][lane];
-                B4 bb;
-                bb.x0 = (int16_t)(lo & 0xffff);
-                bb.y0 = (int16_t)(lo >> 16);
-                bb.x1 = (int16_t)(hi & 0xffff);
-                bb.y1 = (int16_t)(hi >> 16);
-                w.Rbb[lb + p] = bb;
-            } else {
-                w.Rmx[lb + p] = res[0][lane];
-                w.Rrank[lb + p] = resi[0][lane];
-                w.Rroot[lb + p] = resi[1][lane];
+            if (wv == 0) w.Rmx[lb + p] = sh.mean[0][lane];
+            if (wv == 1) w.Rmy[lb + p] = sh.mean[1][lane];
+            if (wv == 2) {
+                w.Rrank[lb + p] = sh.rank[lane];
+                w.Rroot[lb + p] = sh.root[lane];
             }
         }
         if (n < 64 || finished) {
-            // both waves stop at the same step (same flags); the top's readiness is read only in
-            // later rounds (kernel boundary), so either wave may publish it
-            if (wv == 0 && lane == 0) {
+            // all waves stop at the same step (same flags); the top's readiness is read only in
+            // later rounds (kernel boundary), so one wave publishes it
+            if (wv == 2 && lane == 0) {
                 if (finished) {
                     w.ready[lb + q - n + 1] = round;
                     *curp = -1;
@@ -265,18 +309,20 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, LongStep
         }
         q -= 64;
         cb ^= 1;
-        mine = nx;
-        buf[wv][cb][lane] = mine;
+        meta = nmeta;
+        lbb = nlbb;
+        if (wv < 2)
+            sh.chain[wv][cb][lane] = ncr;
+        else
+            sh.side[cb][lane] = nsr;
     }
 }
 
-__global__ __launch_bounds__(128) void k_replay_long(Ws w, int round) {
-    __shared__ LongStep buf[2][2][64];
-    __shared__ float res[2][64];
-    __shared__ int resi[4][64];
+__global__ __launch_bounds__(192) void k_replay_long(Ws w, int round) {
+    __shared__ LongShared sh;
     const int f = blockIdx.y;
     const int n = w.C(f)[C_LONG];
-    for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path(w, f, jj, round, buf, res, resi);
+    for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path(w, f, jj, round, sh);
 }
 
 struct HipBackend {
@@ -416,7 +462,7 @@ struct HipBackend {
     }
 
     void replay_long(const Ws& w, int round) {
-        hipLaunchKernelGGL(k_replay_long, dim3(256u, (unsigned)w.d.B), dim3(128), 0, stream, w, round);
+        hipLaunchKernelGGL(k_replay_long, dim3(256u, (unsigned)w.d.B), dim3(192), 0, stream, w, round);
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_replay_long launch");
     }
 
