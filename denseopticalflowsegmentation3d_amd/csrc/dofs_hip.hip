@@ -130,8 +130,6 @@ constexpr int kLongOk = 8;
 struct LongShared {
     ChainRec chain[2][2][64];  // [wave][buffer][step]
     SideRec side[2][64];       // [buffer][step]
-    float mean[2][64];         // [wave][step] chain outputs
-    int rank[64], root[64];    // wave 2 outputs
 };
 
 // Resolve position p for wave `wv`. Returns the meta flags (kLongOk when the inputs are ready).
@@ -240,14 +238,17 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, LongShar
         const int n = finished ? ft + 1 : fb;
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS records have landed
         __builtin_amdgcn_wave_barrier();
+        // the loops read their step records from LDS and keep step k's output in lane k (no LDS
+        // stores inside the loop, so the compiler can issue the record loads ahead of the chain)
+        float om = 0.f;
+        int orank = 0, oroot = 0;
         if (wv < 2) {
             const ChainRec* c = sh.chain[wv][cb];
-            float* out = sh.mean[wv];
 #pragma unroll 8
             for (int k = 0; k < n; ++k) {
                 const ChainRec st = c[k];
                 m = (float)((double)(m * st.fs + st.wb) * st.r);
-                out[k] = m;
+                om = lane == k ? m : om;
             }
         } else {
             const SideRec* c = sh.side[cb];
@@ -258,8 +259,8 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, LongShar
                                                      : (st.lrank > rank ? st.lroot : root);
                 rank = (rank == st.lrank) ? rank + 1 : (rank > st.lrank ? rank : st.lrank);
                 root = nroot;
-                sh.rank[k] = rank;
-                sh.root[k] = root;
+                orank = lane == k ? rank : orank;
+                oroot = lane == k ? root : oroot;
             }
             // bbox: inclusive prefix join over the chunk (lane = step), then the carried box
             B4 x = lbb;
@@ -282,15 +283,13 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, LongShar
                 }
             }
         }
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_wave_barrier();
         if (lane < n) {
             const int p = q - lane;
-            if (wv == 0) w.Rmx[lb + p] = sh.mean[0][lane];
-            if (wv == 1) w.Rmy[lb + p] = sh.mean[1][lane];
+            if (wv == 0) w.Rmx[lb + p] = om;
+            if (wv == 1) w.Rmy[lb + p] = om;
             if (wv == 2) {
-                w.Rrank[lb + p] = sh.rank[lane];
-                w.Rroot[lb + p] = sh.root[lane];
+                w.Rrank[lb + p] = orank;
+                w.Rroot[lb + p] = oroot;
             }
         }
         if (n < 64 || finished) {
@@ -323,6 +322,159 @@ __global__ __launch_bounds__(192) void k_replay_long(Ws w, int round) {
     const int f = blockIdx.y;
     const int n = w.C(f)[C_LONG];
     for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path(w, f, jj, round, sh);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// K3 deep levels: once the divide-and-conquer block size is kDeepS (512 merges), every remaining
+// level of a block only involves that block's merges and the labels they touch, so one workgroup
+// runs all of them in LDS: the block's labels get local ids (slots of an LDS hash table), a
+// component created at merge t of the block gets local id kDeepHT + t, and the per-level union /
+// compress / L-root / relabel / cleanup phases of dofs_kernels.h (KDnc*) run between workgroup
+// barriers. Output: the KRT parents found inside the block (MINR) and the sizes of its new
+// components — identical to the global kernels (the union-find shapes differ, results do not).
+// ---------------------------------------------------------------------------------------------
+constexpr int kDeepS = 512;
+constexpr int kDeepHT = 2 * kDeepS * 2;  // hash slots (load factor <= 1/2)
+constexpr int kDeepL = kDeepHT + kDeepS;  // local label space
+constexpr int kDeepT = 256;               // threads per block
+
+__device__ inline int lds_ld(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ inline void lds_st(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ inline int lds_find(int* P, int x) {
+    for (;;) {
+        const int p = lds_ld(P + x);
+        if (p == x) return x;
+        const int gp = lds_ld(P + p);
+        if (gp == p) return p;
+        lds_st(P + x, gp);
+        x = gp;
+    }
+}
+__device__ inline int lds_union(int* P, const int* SZ, int a, int b) {
+    for (;;) {
+        a = lds_find(P, a);
+        b = lds_find(P, b);
+        if (a == b) return -1;
+        if (!dnc_above(SZ, a, b)) {
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        int old = a;
+        __hip_atomic_compare_exchange_strong(P + a, &old, b, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (old == a) return a;
+    }
+}
+
+__global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
+    __shared__ int keys[kDeepHT];
+    __shared__ int P[kDeepL], SZ[kDeepL], CS[kDeepL], MX[kDeepL];
+    __shared__ int lu[kDeepS], lv[kDeepS], own[kDeepS], lrr[kDeepS], minr[kDeepS];
+    const Dims& d = w.d;
+    const int f = blockIdx.y;
+    const int64_t s0 = (int64_t)blockIdx.x * kDeepS;
+    if (s0 >= d.M) return;
+    const int64_t lb = f * d.NL, eb = f * d.M;
+    const int cnt = (int)((d.M - s0) < kDeepS ? (d.M - s0) : kDeepS);
+    for (int x = threadIdx.x; x < kDeepL; x += kDeepT) {
+        P[x] = x;
+        CS[x] = 0;
+        MX[x] = -1;
+        SZ[x] = 0;
+        if (x < kDeepHT) keys[x] = -1;
+    }
+    for (int t = threadIdx.x; t < kDeepS; t += kDeepT) minr[t] = kIntMax;
+    __syncthreads();
+    for (int t = threadIdx.x; t < cnt; t += kDeepT) {  // local ids: hash slots of the global labels
+        for (int side = 0; side < 2; ++side) {
+            const int g = side ? w.lv[eb + s0 + t] : w.lu[eb + s0 + t];
+            unsigned h = uf_prio(g) & (kDeepHT - 1);
+            for (;;) {
+                int old = -1;
+                __hip_atomic_compare_exchange_strong(keys + h, &old, g, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (old == -1 || old == g) break;
+                h = (h + 1) & (kDeepHT - 1);
+            }
+            if (side)
+                lv[t] = (int)h;
+            else
+                lu[t] = (int)h;
+            SZ[h] = w.SZ[lb + g];
+        }
+    }
+    __syncthreads();
+    for (int S = kDeepS; S >= 2; S >>= 1) {
+        const int half = S >> 1;
+        // union (L edges of sub-blocks whose R half exists)
+        for (int t = threadIdx.x; t < cnt; t += kDeepT) {
+            const bool isL = (t & (S - 1)) < half && s0 + (t & ~(S - 1)) + half < d.M;
+            if (isL) own[t] = lds_union(P, SZ, lu[t], lv[t]);
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < cnt; t += kDeepT) {  // compress + aggregate
+            const bool isL = (t & (S - 1)) < half && s0 + (t & ~(S - 1)) + half < d.M;
+            if (!isL) continue;
+            const int h = own[t];
+            int r = h;
+            for (int p = lds_ld(P + r); p != r; p = lds_ld(P + r)) r = p;
+            for (int y = h; y != r;) {
+                const int p = lds_ld(P + y);
+                if (p != r) lds_st(P + y, r);
+                y = p;
+            }
+            atomicAdd(CS + r, SZ[h]);
+            atomicMax(MX + r, t);
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < cnt; t += kDeepT) {  // L-roots: sizes of the new components
+            const bool isL = (t & (S - 1)) < half && s0 + (t & ~(S - 1)) + half < d.M;
+            if (!isL) continue;
+            const int r = P[own[t]];
+            if (MX[r] != t) {
+                lrr[t] = -1;
+                continue;
+            }
+            lrr[t] = r;
+            const int sz = CS[r] + SZ[r];
+            SZ[kDeepHT + t] = sz;
+            w.SZ[lb + d.N + s0 + t] = sz;
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < cnt; t += kDeepT) {  // relabel R edges, first touching R edge
+            if ((t & (S - 1)) < half) continue;
+            for (int side = 0; side < 2; ++side) {
+                const int x = side ? lv[t] : lu[t];
+                const int r = P[x];
+                const int li = MX[r];
+                if (r != x || li >= 0) {
+                    if (side)
+                        lv[t] = kDeepHT + li;
+                    else
+                        lu[t] = kDeepHT + li;
+                    atomicMin(minr + li, 2 * t + side);
+                }
+            }
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < cnt; t += kDeepT) {  // cleanup
+            const bool isL = (t & (S - 1)) < half && s0 + (t & ~(S - 1)) + half < d.M;
+            if (!isL) continue;
+            P[own[t]] = own[t];
+            const int r = lrr[t];
+            if (r >= 0) {
+                MX[r] = -1;
+                CS[r] = 0;
+            }
+        }
+        __syncthreads();
+    }
+    for (int t = threadIdx.x; t < cnt; t += kDeepT) {
+        const int c = minr[t];
+        if (c != kIntMax) w.MINR[eb + s0 + t] = (int)(2 * (s0 + (c >> 1)) + (c & 1));
+    }
 }
 
 struct HipBackend {
@@ -461,6 +613,12 @@ struct HipBackend {
         if (launch_on(stream, nf, n, f) != DOFS_OK) note(hipErrorLaunchFailure, "kernel launch");
     }
 
+    static constexpr int64_t deep_block() { return kDeepS; }
+    void dnc_deep(const Ws& w) {
+        const unsigned nb = (unsigned)((w.d.M + kDeepS - 1) / kDeepS);
+        hipLaunchKernelGGL(k_dnc_deep, dim3(nb, (unsigned)w.d.B), dim3(kDeepT), 0, stream, w);
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_dnc_deep launch");
+    }
     void replay_long(const Ws& w, int round) {
         hipLaunchKernelGGL(k_replay_long, dim3(256u, (unsigned)w.d.B), dim3(192), 0, stream, w, round);
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_replay_long launch");

@@ -221,13 +221,15 @@ struct Pipeline {
         be.launch(B, M, KEdgeInit{w});
         be.launch(B, NL, KLabelInit{w});
         be.launch(B, M, KLeafParent{w});
-        for (int64_t S = (int64_t)1 << ceil_log2(M); S >= 2; S >>= 1) {
+        const int64_t deep = Backend::deep_block();  // levels with block size <= deep run per block
+        for (int64_t S = (int64_t)1 << ceil_log2(M); S > deep; S >>= 1) {
             be.launch(B, M, KDncUnion{w, S});
             be.launch(B, M, KDncCompress{w, S});
             be.launch(B, M, KDncLRoot{w, S});
             be.launch(B, M, KDncRelabelR{w, S});
             be.launch(B, M, KDncCleanup{w, S});
         }
+        be.dnc_deep(w);
         be.launch(B, M, KDncParent{w});
         be.launch(B, N, KLeafChild{w});
 

@@ -66,6 +66,21 @@ struct HostBackend {
     void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height) {
         for (size_t r = 0; r < height; ++r) memcpy((char*)dst + r * dpitch, (const char*)src + r * spitch, width);
     }
+    // the HIP build runs the levels with block size <= 512 per block in LDS (k_dnc_deep); the
+    // emulator runs them with the global kernels (same parents and sizes)
+    static constexpr int64_t deep_block() { return 512; }
+    void dnc_deep(const Ws& w) {
+        const int64_t M = w.d.M;
+        int64_t top = 1;
+        while (top < M) top <<= 1;
+        for (int64_t S = std::min<int64_t>(512, top); S >= 2; S >>= 1) {
+            launch(w.d.B, M, KDncUnion{w, S});
+            launch(w.d.B, M, KDncCompress{w, S});
+            launch(w.d.B, M, KDncLRoot{w, S});
+            launch(w.d.B, M, KDncRelabelR{w, S});
+            launch(w.d.B, M, KDncCleanup{w, S});
+        }
+    }
     void replay_long(const Ws& w, int r) { launch(w.d.B, w.d.N, KReplay{w, r, w.list_long, C_LONG}); }
     void profile(bool) {}
     void mark(int) {}
