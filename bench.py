@@ -25,7 +25,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from denseopticalflowsegmentation3d_amd import runtime  # noqa: E402
-from denseopticalflowsegmentation3d_amd.abi import DofsBoxRecord, default_params  # noqa: E402
+from denseopticalflowsegmentation3d_amd.abi import default_params  # noqa: E402
+from denseopticalflowsegmentation3d_amd.frames import FrameParallel  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 GATHER_PER_FRAME = 64  # box records per frame in the gathered block
@@ -36,7 +37,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=8, help="frames per GPU per step")
+    ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--cpu-frames", type=int, default=1, help="frames of the CPU baseline sample (0 = skip)")
@@ -81,18 +82,23 @@ def main():
 
     flows = torch.empty((B, H, W, 2), dtype=torch.float32, device=dev)
     runtime.synth_flow_device(flows.data_ptr(), B, H, W, seed0=rank * B, stream=sh)
-    rec_bytes = 4 * B + B * GATHER_PER_FRAME * DofsBoxRecord.np_dtype().itemsize
-    rec = torch.empty(rec_bytes, dtype=torch.uint8, device=dev)
-    gathered = torch.empty(world * rec_bytes, dtype=torch.uint8, device=dev) if world > 1 else None
+    fp = FrameParallel(ctx, world, GATHER_PER_FRAME)
+    pending = []
 
+    # one step = submit a batch, then gather the records of the previous one (the context overlaps
+    # the previous batch's replay stage with this batch's graph stage); flush() gathers the last.
     def step():
-        ctx.segment_batch_device(flows.data_ptr(), B, H, W, persp, inv, up, params=prm, stream=sh)
-        ctx.records_copy(rec.data_ptr(), GATHER_PER_FRAME, stream=sh)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, rec)
+        pending.append(fp.submit(flows, persp, inv, up, params=prm, stream=sh))
+        if len(pending) > 1:
+            fp.collect(pending.pop(0), stream=sh)
+
+    def flush():
+        while pending:
+            fp.collect(pending.pop(0), stream=sh)
 
     for _ in range(a.warmup):
         step()
+    flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -102,6 +108,7 @@ def main():
     e0.record(stream)
     for _ in range(a.steps):
         step()
+    flush()
     e1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -122,6 +129,7 @@ def main():
         ctx.profile(True)
         for _ in range(max(2, a.steps // 2)):
             step()
+        flush()
         torch.cuda.synchronize()
         ms, nb = ctx.profile_read()
         ctx.profile(False)

@@ -157,21 +157,54 @@ struct KSynth {
 
 template <class Backend>
 struct Context {
+    // Two workspaces used alternately by consecutive batches. A batch runs phase A (graph) on
+    // stream sA and phase B (replay + scoring) on stream sB, so batch k's phase B overlaps batch
+    // k+1's phase A. A workspace is reused only after its previous batch's phase B (evDone) ended.
+    struct Meta {
+        int B = 0, H = 0, W = 0;
+        dofs_params prm;
+    };
     Backend be;
-    Pipeline<Backend> pipe;
+    Pipeline<Backend> p0, p1;
     std::string err;
     void* d_in = nullptr;
     size_t d_in_bytes = 0;
     void* d_scratch = nullptr;
     size_t d_scratch_bytes = 0;
-    bool have_batch = false;
-    int last_B = 0, last_H = 0, last_W = 0;
-    dofs_params last_prm;
+    int64_t nbatch = 0;  // batches issued; batch id b used workspace b & 1
+    int64_t snap_cap = 4096;
+    bool used[2] = {false, false};
+    Meta meta[2];
+    void* sA = nullptr;
+    void* sB = nullptr;
+    void* evIn = nullptr;
+    void* evA[2] = {nullptr, nullptr};
+    void* evDone[2] = {nullptr, nullptr};
 
-    explicit Context(int device) : be(device), pipe(be) { default_params(&last_prm); }
+    explicit Context(int device) : be(device), p0(be), p1(be) {
+        sA = be.new_stream();
+        sB = be.new_stream();
+        evIn = be.new_event();
+        for (int s = 0; s < 2; ++s) {
+            evA[s] = be.new_event();
+            evDone[s] = be.new_event();
+        }
+    }
     ~Context() {
+        drain();
         if (d_in) be.free(d_in);
         if (d_scratch) be.free(d_scratch);
+    }
+    Pipeline<Backend>& pipe(int slot) { return slot ? p1 : p0; }
+    bool have_batch() const { return nbatch > 0; }
+    int last_slot() const { return (int)((nbatch - 1) & 1); }
+    // valid batch ids for result access: the last two issued
+    bool live(int64_t id) const { return id >= 0 && id < nbatch && id >= nbatch - 2; }
+    // make the current stream wait for batch id's results
+    void join(int64_t id) { be.wait(be.cur_stream(), evDone[id & 1]); }
+    void drain() {
+        for (int s = 0; s < 2; ++s)
+            if (used[s]) be.event_sync(evDone[s]);
     }
     void* scratch(size_t bytes) {
         if (bytes > d_scratch_bytes) {
@@ -191,6 +224,9 @@ struct Context {
     }
 };
 
+// Enqueue one batch on the context's streams, ordered after the work already on the caller's
+// (current) stream. On return the caller's stream is ordered after phase A, so it may overwrite
+// the input; results are joined by api_fetch / api_events / api_records_copy.
 template <class Backend>
 int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int H, int W, const float persp[9],
             const float inv[9], const float inv_upper[27], const dofs_params* params) {
@@ -205,29 +241,60 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     // segment.cpp:38-43: anything but 8 segments with the 4-neighbourhood (logged, not an error)
     const int nbr8 = prm.neighbor == 8 ? 1 : 0;
     Dims d = Pipeline<Backend>::dims_for(B, H, W, nbr8);
-    if (!cx->pipe.reserve(d)) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
-    cx->pipe.set_params(prm, persp, inv, inv_upper);
-    cx->pipe.run(d_flow, fstride);
-    cx->have_batch = true;
-    cx->last_B = B;
-    cx->last_H = H;
-    cx->last_W = W;
-    cx->last_prm = prm;
+    Backend& be = cx->be;
+    const int64_t id = cx->nbatch;
+    const int s = (int)(id & 1);
+    Pipeline<Backend>& P = cx->pipe(s);
+    if (P.snap_cap != cx->snap_cap) {
+        P.snap_cap = cx->snap_cap;
+        P.cap.B = 0;  // force a new layout
+    }
+    if (!P.fits(d) && cx->used[s]) be.event_sync(cx->evDone[s]);  // reallocation: batch id-2 must be done
+    if (!P.reserve(d)) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    P.set_params(prm, persp, inv, inv_upper);
+
+    void* caller = be.cur_stream();
+    void* sa = cx->sA;
+    void* sb = be.profiling() ? cx->sA : cx->sB;  // stage timing runs the phases back to back
+    be.record(cx->evIn, caller);
+    be.wait(sa, cx->evIn);
+    if (cx->used[s]) be.wait(sa, cx->evDone[s]);
+    be.use(sa);
+    P.run_a(d_flow, fstride);
+    be.record(cx->evA[s], sa);
+    if (sb != sa) be.wait(sb, cx->evA[s]);
+    be.use(sb);
+    P.run_b();
+    be.record(cx->evDone[s], sb);
+    be.wait(caller, cx->evA[s]);
+    be.use(caller);
+
+    cx->used[s] = true;
+    cx->nbatch = id + 1;
+    auto& m = cx->meta[s];
+    m.B = B;
+    m.H = H;
+    m.W = W;
+    m.prm = prm;
     return cx->check();
 }
 
 template <class Backend>
 int api_fetch(Context<Backend>* cx, int frame, dofs_result* out) {
-    if (!cx->have_batch || frame < 0 || frame >= cx->last_B || !out) return cx->fail(DOFS_ERR_INVALID_ARG, "no frame");
+    if (!cx->have_batch() || !out) return cx->fail(DOFS_ERR_INVALID_ARG, "no batch");
+    const int slot = cx->last_slot();
+    const typename Context<Backend>::Meta& m = cx->meta[slot];
+    if (frame < 0 || frame >= m.B) return cx->fail(DOFS_ERR_INVALID_ARG, "no frame");
     Backend& be = cx->be;
-    const Ws& w = cx->pipe.w;
+    cx->join(cx->nbatch - 1);
+    const Ws& w = cx->pipe(slot).w;
     const Dims& d = w.d;
     int ctr[kCounters];
     be.d2h(ctr, w.ctr + (int64_t)frame * kCounters, sizeof(ctr));
     be.sync();
     const int ns = ctr[C_SNAP];
     out->n_snapshots = ns;
-    out->stats.n_edges = graph_edges(cx->last_H, cx->last_W, cx->last_prm.neighbor == 8);
+    out->stats.n_edges = graph_edges(m.H, m.W, m.prm.neighbor == 8);
     out->stats.n_merges = d.M;
     out->stats.n_candidates = ctr[C_CAND];
     out->stats.n_scored = ctr[C_SCORED];
@@ -248,8 +315,11 @@ int api_fetch(Context<Backend>* cx, int frame, dofs_result* out) {
 
 template <class Backend>
 int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity) {
-    if (!cx->have_batch || frame < 0 || frame >= cx->last_B || !ev) return cx->fail(DOFS_ERR_INVALID_ARG, "no frame");
-    const Ws& w = cx->pipe.w;
+    if (!cx->have_batch() || !ev) return cx->fail(DOFS_ERR_INVALID_ARG, "no batch");
+    const int slot = cx->last_slot();
+    if (frame < 0 || frame >= cx->meta[slot].B) return cx->fail(DOFS_ERR_INVALID_ARG, "no frame");
+    cx->join(cx->nbatch - 1);
+    const Ws& w = cx->pipe(slot).w;
     const Dims& d = w.d;
     if (capacity < d.M) return cx->fail(DOFS_ERR_CAPACITY, "event capacity");
     if (d.M <= 0) return DOFS_OK;
@@ -263,7 +333,7 @@ int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity
     be.d2h(eu.data(), w.EU + (int64_t)frame * d.M, 4 * (size_t)d.M);
     be.d2h(evv.data(), w.EV + (int64_t)frame * d.M, 4 * (size_t)d.M);
     be.d2h(key.data(), w.key_out + (int64_t)frame * d.M, 8 * (size_t)d.M);
-    be.d2h(pre.data(), cx->pipe.pre + fo + d.N, 4 * (size_t)d.M);
+    be.d2h(pre.data(), cx->pipe(slot).pre + fo + d.N, 4 * (size_t)d.M);
     be.d2h(rmx.data(), w.Rmx + fo, 4 * (size_t)d.NL);
     be.d2h(rmy.data(), w.Rmy + fo, 4 * (size_t)d.NL);
     be.d2h(rrank.data(), w.Rrank + fo, 4 * (size_t)d.NL);
@@ -313,11 +383,11 @@ int api_segment(Context<Backend>* cx, const float* flow, int H, int W, size_t st
     int rc = api_run(cx, (const F2*)cx->d_in, (int64_t)H * W, 1, H, W, persp, inv, inv_upper, params);
     if (rc) return rc;
     int n = 0;  // more history slots than the device snapshot capacity: grow it and run again
-    cx->be.d2h(&n, cx->pipe.w.ctr + C_SNAP, sizeof(int));
+    cx->join(cx->nbatch - 1);
+    cx->be.d2h(&n, cx->pipe(cx->last_slot()).w.ctr + C_SNAP, sizeof(int));
     cx->be.sync();
-    if (n > cx->pipe.snap_cap) {
-        while (cx->pipe.snap_cap < n) cx->pipe.snap_cap *= 2;
-        cx->pipe.cap.B = 0;  // force a new layout
+    if (n > cx->snap_cap) {
+        while (cx->snap_cap < n) cx->snap_cap *= 2;
         rc = api_run(cx, (const F2*)cx->d_in, (int64_t)H * W, 1, H, W, persp, inv, inv_upper, params);
         if (rc) return rc;
     }
@@ -325,12 +395,14 @@ int api_segment(Context<Backend>* cx, const float* flow, int H, int W, size_t st
 }
 
 template <class Backend>
-int api_records_copy(Context<Backend>* cx, void* dst, int per_frame, void* stream) {
-    if (!cx->have_batch || !dst || per_frame < 0) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
-    const Ws& w = cx->pipe.w;
-    const int B = cx->last_B;
+int api_records_copy(Context<Backend>* cx, int64_t batch, void* dst, int per_frame, void* stream) {
+    if (!cx->live(batch) || !dst || per_frame < 0) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
+    const int slot = (int)(batch & 1);
+    const Ws& w = cx->pipe(slot).w;
+    const int B = cx->meta[slot].B;
     const int k = per_frame < w.snap_cap ? per_frame : w.snap_cap;
     cx->be.set_stream(stream);
+    cx->join(batch);
     cx->be.copy2d(dst, sizeof(int), w.ctr + C_SNAP, sizeof(int) * kCounters, sizeof(int), B);
     if (k > 0)
         cx->be.copy2d((char*)dst + sizeof(int) * B, sizeof(dofs_box_record) * per_frame, w.recs,

@@ -70,17 +70,26 @@ int32_t dofs_batch_fetch(dofs_ctx* ctx, int32_t frame, dofs_result* out) {
 }
 
 int32_t dofs_batch_records_device(dofs_ctx* ctx, void** d_records, void** d_counts, int32_t* capacity) {
-    if (!ctx || !ctx->have_batch) return DOFS_ERR_INVALID_ARG;
-    if (d_records) *d_records = ctx->pipe.w.recs;
-    if (d_counts) *d_counts = ctx->pipe.w.ctr;  // int32 counters, stride kCounters, count at C_SNAP
-    if (capacity) *capacity = ctx->pipe.w.snap_cap;
-    return DOFS_OK;
+    if (!ctx || !ctx->have_batch()) return DOFS_ERR_INVALID_ARG;
+    ctx->be.event_sync(ctx->evDone[ctx->last_slot()]);  // the pointers are read after the batch ended
+    const dofs::Ws& w = ctx->pipe(ctx->last_slot()).w;
+    if (d_records) *d_records = w.recs;
+    if (d_counts) *d_counts = w.ctr;  // int32 counters, stride kCounters, count at C_SNAP
+    if (capacity) *capacity = w.snap_cap;
+    return ctx->check();
 }
 
 int32_t dofs_batch_records_copy(dofs_ctx* ctx, void* d_dst, int32_t per_frame, void* stream) {
     if (!ctx) return DOFS_ERR_INVALID_ARG;
-    return dofs::api_records_copy(ctx, d_dst, per_frame, stream);
+    return dofs::api_records_copy(ctx, ctx->nbatch - 1, d_dst, per_frame, stream);
 }
+
+int32_t dofs_batch_records_copy_id(dofs_ctx* ctx, int64_t batch, void* d_dst, int32_t per_frame, void* stream) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    return dofs::api_records_copy(ctx, batch, d_dst, per_frame, stream);
+}
+
+int64_t dofs_batch_count(dofs_ctx* ctx) { return ctx ? ctx->nbatch : -1; }
 
 int32_t dofs_profile(dofs_ctx* ctx, int32_t enable) {
     if (!ctx) return DOFS_ERR_INVALID_ARG;
@@ -90,6 +99,7 @@ int32_t dofs_profile(dofs_ctx* ctx, int32_t enable) {
 
 int32_t dofs_profile_read(dofs_ctx* ctx, double ms[8], int32_t* batches) {
     if (!ctx || !ms) return DOFS_ERR_INVALID_ARG;
+    ctx->drain();
     int n = ctx->be.profile_read(ms);
     if (batches) *batches = n;
     return ctx->check();

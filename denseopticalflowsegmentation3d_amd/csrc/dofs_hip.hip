@@ -483,8 +483,14 @@ struct HipBackend {
     hipStream_t stream = nullptr;
     hipError_t last = hipSuccess;
     std::string msg;
-    void* tmp = nullptr;
-    size_t tmp_bytes = 0;
+    struct Temp {
+        hipStream_t s;
+        void* p;
+        size_t n;
+    };
+    std::vector<Temp> tmps;  // hipcub scratch, one per stream (the pipeline's phases run concurrently)
+    std::vector<hipStream_t> streams;
+    std::vector<hipEvent_t> events;
 
     static bool device_ok(int dev) {
         int n = 0;
@@ -501,7 +507,10 @@ struct HipBackend {
     }
     ~HipBackend() {
         for (auto e : pool) (void)hipEventDestroy(e);
-        if (tmp) (void)hipFree(tmp);
+        for (auto e : events) (void)hipEventDestroy(e);
+        for (auto& t : tmps)
+            if (t.p) (void)hipFree(t.p);
+        for (auto st : streams) (void)hipStreamDestroy(st);
         if (own) (void)hipStreamDestroy(own);
     }
     void note(hipError_t e, const char* what) {
@@ -516,6 +525,25 @@ struct HipBackend {
         (void)hipSetDevice(device);
         stream = s ? (hipStream_t)s : own;
     }
+
+    void* cur_stream() const { return stream; }
+    void use(void* s) { stream = (hipStream_t)s; }
+    void* new_stream() {
+        hipStream_t st = nullptr;
+        note(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+        if (st) streams.push_back(st);
+        return st;
+    }
+    void* new_event() {
+        hipEvent_t e = nullptr;
+        note(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        if (e) events.push_back(e);
+        return e;
+    }
+    void record(void* ev, void* s) { note(hipEventRecord((hipEvent_t)ev, (hipStream_t)s), "hipEventRecord"); }
+    void wait(void* s, void* ev) { note(hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)ev, 0), "hipStreamWaitEvent"); }
+    void event_sync(void* ev) { note(hipEventSynchronize((hipEvent_t)ev), "hipEventSynchronize"); }
+    bool profiling() const { return prof; }
 
     void* alloc(size_t bytes) {
         void* p = nullptr;
@@ -625,13 +653,20 @@ struct HipBackend {
     }
 
     void* temp(size_t bytes) {
-        if (bytes > tmp_bytes) {
-            sync();
-            if (tmp) (void)hipFree(tmp);
-            tmp = alloc(bytes);
-            tmp_bytes = tmp ? bytes : 0;
+        Temp* t = nullptr;
+        for (auto& x : tmps)
+            if (x.s == stream) t = &x;
+        if (!t) {
+            tmps.push_back(Temp{stream, nullptr, 0});
+            t = &tmps.back();
         }
-        return tmp;
+        if (bytes > t->n) {
+            sync();
+            if (t->p) (void)hipFree(t->p);
+            t->p = alloc(bytes);
+            t->n = t->p ? bytes : 0;
+        }
+        return t->p;
     }
     // exclusive prefix sum of each frame's segment [f*n, (f+1)*n)
     void scan_excl(const int* in, int* out, int64_t n, int nf) {

@@ -294,6 +294,36 @@ struct KBoruvkaInit {
     }
 };
 
+// Round 0: every pixel is its own component, so its minimum edge is the min over its <= 8 incident
+// edges (4 it emits, 4 its right/lower neighbours emit towards it) — no atomics.
+struct KBoruvkaFirst {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t p) const {
+        const Dims& d = w.d;
+        const int x = (int)(p % d.W), y = (int)(p / d.W);
+        const F2* b = w.blur + f * d.N;
+        unsigned long long best = ~0ull;
+        unsigned bidx = kNoEdge;
+        auto take = [&](int64_t s, int k, int64_t e) {
+            const unsigned long long wb = dbits(edge_weight(b, s, e));
+            const unsigned idx = (unsigned)(4 * s + k);
+            if (wb < best || (wb == best && idx < bidx)) {
+                best = wb;
+                bidx = idx;
+            }
+        };
+        for (int k = 0; k < 4; ++k)
+            if (edge_exists(d, x, y, k)) take(p, k, edge_end(d, p, k));
+        if (x + 1 < d.W) take(p + 1, 0, p);                                       // right: its left edge
+        if (y + 1 < d.H) take(p + d.W, 1, p);                                     // below: its up edge
+        if (d.nbr8 && x + 1 < d.W && y + 1 < d.H) take(p + d.W + 1, 2, p);       // down-right: up-left
+        if (d.nbr8 && x + 1 < d.W && y >= 1) take(p - d.W + 1, 3, p);            // up-right: down-left
+        w.bw[f * d.N + p] = best;
+        w.bi[f * d.N + p] = bidx;
+        if (bidx != kNoEdge && p == 0) w.C(f)[C_ACT + 0] = 1;
+    }
+};
+
 struct KBoruvkaReset {  // round r: clear per-component minima
     Ws w;
     int r;
@@ -323,8 +353,8 @@ struct KBoruvkaMinW {
             const int cq = comp[q];
             if (cp == cq) continue;
             const unsigned long long wb = dbits(edge_weight(b, p, q));
-            dofs_amin_u64(bw + cp, wb);
-            dofs_amin_u64(bw + cq, wb);
+            if (wb < bw[cp]) dofs_amin_u64(bw + cp, wb);  // plain read first: bw only decreases
+            if (wb < bw[cq]) dofs_amin_u64(bw + cq, wb);
             any = true;
         }
         if (any) w.C(f)[C_ACT + r] = 1;
@@ -350,8 +380,8 @@ struct KBoruvkaMinI {
             if (cp == cq) continue;
             const unsigned long long wb = dbits(edge_weight(b, p, q));
             const unsigned idx = (unsigned)(4 * p + k);
-            if (wb == bw[cp]) dofs_amin_u32(bi + cp, idx);
-            if (wb == bw[cq]) dofs_amin_u32(bi + cq, idx);
+            if (wb == bw[cp] && idx < bi[cp]) dofs_amin_u32(bi + cp, idx);
+            if (wb == bw[cq] && idx < bi[cq]) dofs_amin_u32(bi + cq, idx);
         }
     }
 };
@@ -558,32 +588,27 @@ struct KDncCompress {
     }
 };
 
-struct KDncLRoot {
+// After KDncCompress (roots final, hooked labels point at them): an L edge whose rank is its
+// component's max (an L-root) gets the component size; an R edge relabels its endpoints to the
+// components' new labels and offers itself as their first touching merge (KRT parent candidate).
+struct KDncLRootRelabel {
     Ws w;
     int64_t S;
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
-        if (!dnc_is_L(d, i, S)) return;
         const int64_t o = f * d.M + i;
         const int64_t lb = f * d.NL;
-        const int r = w.P[lb + w.own[o]];  // hooked labels point at their root after KDncCompress
-        if (w.MX[lb + r] != (int)i) {
-            w.lrr[o] = -1;
+        if (dnc_is_L(d, i, S)) {
+            const int r = w.P[lb + w.own[o]];
+            if (w.MX[lb + r] != (int)i) {
+                w.lrr[o] = -1;
+                return;
+            }
+            w.lrr[o] = r;
+            w.SZ[lb + d.N + i] = w.CS[lb + r] + w.SZ[lb + r];
             return;
         }
-        w.lrr[o] = r;
-        w.SZ[lb + d.N + i] = w.CS[lb + r] + w.SZ[lb + r];
-    }
-};
-
-struct KDncRelabelR {
-    Ws w;
-    int64_t S;
-    DOFS_HD void operator()(int f, int64_t j) const {
-        const Dims& d = w.d;
-        if (!dnc_is_R(j, S)) return;
-        const int64_t o = f * d.M + j;
-        const int64_t lb = f * d.NL;
+        if (!dnc_is_R(i, S)) return;
         for (int side = 0; side < 2; ++side) {  // uniform per wave while S/2 >= 64 (aggregation)
             int* lp = side ? (w.lv + o) : (w.lu + o);
             const int x = *lp;
@@ -593,7 +618,7 @@ struct KDncRelabelR {
             const bool act = (r != x) || li >= 0;
             if (act) *lp = (int)(d.N + li);
             // smallest-rank R edge touching the L component li (many R edges touch a big one)
-            dofs_agg_min(w.MINR + f * d.M, act ? li : 0, (int)(2 * j + side), act);
+            dofs_agg_min(w.MINR + f * d.M, act ? li : 0, (int)(2 * i + side), act);
         }
     }
 };

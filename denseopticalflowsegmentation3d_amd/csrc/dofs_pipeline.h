@@ -74,10 +74,11 @@ struct Pipeline {
         return d;
     }
 
+    bool fits(const Dims& d) const { return base && cap.B >= d.B && cap.N == d.N && cap.W == d.W; }
+
     // Carve every buffer from one allocation (grow-only). Returns false on allocation failure.
     bool reserve(const Dims& d) {
-        const bool fits = base && cap.B >= d.B && cap.N == d.N && cap.W == d.W;
-        if (!fits) {
+        if (!fits(d)) {
             if (base) be.free(base);
             base = nullptr;
             size_t bytes = layout(d, nullptr);
@@ -177,8 +178,9 @@ struct Pipeline {
         w.overlay_min_score = prm.overlay_min_score;
     }
 
-    // Run the whole path on B frames of device-resident flow (frame stride fstride F2 elements).
-    void run(const F2* flow, int64_t fstride) {
+    // Phase A (graph): blur, MST, Kruskal order, KRT, preorder, replay inputs — on B frames of
+    // device-resident flow (frame stride fstride F2 elements). Throughput-bound.
+    void run_a(const F2* flow, int64_t fstride) {
         const Dims& d = w.d;
         const int B = d.B;
         const int64_t N = d.N, M = d.M, NL = d.NL;
@@ -203,9 +205,13 @@ struct Pipeline {
         be.launch(B, N, KBoruvkaInit{w});
         const int R = std::min(ceil_log2(N) + 2, kRoundsMax - 1);
         for (int r = 0; r < R; ++r) {
-            be.launch(B, N, KBoruvkaReset{w, r});
-            be.launch(B, N, KBoruvkaMinW{w, r});
-            be.launch(B, N, KBoruvkaMinI{w, r});
+            if (r == 0) {
+                be.launch(B, N, KBoruvkaFirst{w});
+            } else {
+                be.launch(B, N, KBoruvkaReset{w, r});
+                be.launch(B, N, KBoruvkaMinW{w, r});
+                be.launch(B, N, KBoruvkaMinI{w, r});
+            }
             be.launch(B, N, KBoruvkaHook{w, r});
             be.launch(B, N, KBoruvkaCompress{w, r});
             be.launch(B, N, KBoruvkaRelabel{w, r});
@@ -225,8 +231,7 @@ struct Pipeline {
         for (int64_t S = (int64_t)1 << ceil_log2(M); S > deep; S >>= 1) {
             be.launch(B, M, KDncUnion{w, S});
             be.launch(B, M, KDncCompress{w, S});
-            be.launch(B, M, KDncLRoot{w, S});
-            be.launch(B, M, KDncRelabelR{w, S});
+            be.launch(B, M, KDncLRootRelabel{w, S});
             be.launch(B, M, KDncCleanup{w, S});
         }
         be.dnc_deep(w);
@@ -251,7 +256,15 @@ struct Pipeline {
         be.scan_excl(w.isleaf, w.lscan, NL, B);
         be.launch(B, N, KLeafOrder{w, pre});
         be.launch(B, NL, KPathInit{w, pre});
+    }
 
+    // Phase B (replay + scoring): the order-dependent replay is latency-bound (a few waves per
+    // frame), so the HIP backend overlaps it with the next batch's phase A on a second stream.
+    void run_b() {
+        const Dims& d = w.d;
+        const int B = d.B;
+        const int64_t N = d.N, M = d.M;
+        if (M <= 0) return;
         be.mark(5);
         // K5 bottom-up replay of Forest::merge along heavy paths
         const int RR = ceil_log2(N) + 2;

@@ -59,18 +59,32 @@ def decode_gathered(gathered: np.ndarray, world: int, frames_per_rank: int, per_
 
 
 class FrameParallel:
-    """One rank's share of a frame-parallel job: segment a device-resident batch, then gather the
-    fixed-size box records of every frame to every rank."""
+    """One rank's share of a frame-parallel job: segment device-resident batches, then gather the
+    fixed-size box records of every frame to every rank.
+
+    `submit` only enqueues; `collect(batch)` gathers a batch's records. Collecting batch k after
+    submitting batch k+1 lets the context overlap k's replay stage with k+1's graph stage."""
 
     def __init__(self, ctx, world: int = 1, per_frame: int = 64):
         self.ctx, self.world, self.per_frame = ctx, world, per_frame
         self.block = None
+        self.frames = {}
 
-    def step(self, flows: torch.Tensor, persp, inv, inv_upper, params=None, stream: int | None = None):
+    def submit(self, flows: torch.Tensor, persp, inv, inv_upper, params=None, stream: int | None = None) -> int:
         B, H, W = flows.shape[:3]
-        self.ctx.segment_batch_device(flows.data_ptr(), B, H, W, persp, inv, inv_upper, params=params, stream=stream)
+        bid = self.ctx.segment_batch_device(flows.data_ptr(), B, H, W, persp, inv, inv_upper, params=params,
+                                            stream=stream)
+        self.frames = {k: v for k, v in self.frames.items() if k >= bid - 1}
+        self.frames[bid] = (B, flows.device)
+        return bid
+
+    def collect(self, bid: int, stream: int | None = None) -> torch.Tensor:
+        B, device = self.frames[bid]
         nb = records_nbytes(B, self.per_frame)
         if self.block is None or self.block.numel() != nb:
-            self.block = torch.empty(nb, dtype=torch.uint8, device=flows.device)
-        self.ctx.records_copy(self.block.data_ptr(), self.per_frame, stream=stream)
+            self.block = torch.empty(nb, dtype=torch.uint8, device=device)
+        self.ctx.records_copy(self.block.data_ptr(), self.per_frame, stream=stream, batch=bid)
         return gather_records(self.block, self.world)
+
+    def step(self, flows: torch.Tensor, persp, inv, inv_upper, params=None, stream: int | None = None):
+        return self.collect(self.submit(flows, persp, inv, inv_upper, params, stream), stream)

@@ -55,6 +55,10 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_batch_records_device.restype = C.c_int32
     L.dofs_batch_records_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
     L.dofs_batch_records_copy.restype = C.c_int32
+    L.dofs_batch_records_copy_id.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p]
+    L.dofs_batch_records_copy_id.restype = C.c_int32
+    L.dofs_batch_count.argtypes = [C.c_void_p]
+    L.dofs_batch_count.restype = C.c_int64
     L.dofs_profile.argtypes = [C.c_void_p, C.c_int32]
     L.dofs_profile.restype = C.c_int32
     L.dofs_profile_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), _ip]
@@ -178,13 +182,15 @@ class Dofs:
         return ev[:n]
 
     def segment_batch_device(self, d_flow: int, B: int, H: int, W: int, persp, inv, inv_upper,
-                             params: DofsParams | None = None, stream: int | None = None) -> None:
-        """Device-resident batch (d_flow = device pointer to B×H×W×2 float32). Asynchronous."""
+                             params: DofsParams | None = None, stream: int | None = None) -> int:
+        """Device-resident batch (d_flow = device pointer to B×H×W×2 float32). Asynchronous; returns
+        the batch id (consecutive batches overlap in the context's two-stage pipeline)."""
         p, i, u = self._mats(persp, inv, inv_upper)
         rc = self.lib.dofs_segment_batch_device(self.ctx, C.c_void_p(d_flow), B, H, W, _p(p), _p(i), _p(u),
                                                 C.byref(params or default_params()), C.c_void_p(stream or 0))
         self._err(rc, "dofs_segment_batch_device")
         self._last_hw = (H, W)
+        return int(self.lib.dofs_batch_count(self.ctx)) - 1
 
     def fetch(self, frame: int, capacity: int = 65536, want_blur: bool = True) -> FrameResult:
         H, W = self._last_hw
@@ -199,10 +205,18 @@ class Dofs:
                   "dofs_batch_records_device")
         return rec.value, cnt.value, cap.value
 
-    def records_copy(self, d_dst: int, per_frame: int, stream: int | None = None) -> None:
-        """int32 counts[B] then B × per_frame DofsBoxRecord into a device buffer (stream-ordered)."""
-        self._err(self.lib.dofs_batch_records_copy(self.ctx, C.c_void_p(d_dst), per_frame, C.c_void_p(stream or 0)),
-                  "dofs_batch_records_copy")
+    def records_copy(self, d_dst: int, per_frame: int, stream: int | None = None, batch: int | None = None) -> None:
+        """int32 counts[B] then B × per_frame DofsBoxRecord into a device buffer (stream-ordered), of the
+        last batch or of batch id `batch` (one of the last two)."""
+        if batch is None:
+            rc = self.lib.dofs_batch_records_copy(self.ctx, C.c_void_p(d_dst), per_frame, C.c_void_p(stream or 0))
+        else:
+            rc = self.lib.dofs_batch_records_copy_id(self.ctx, batch, C.c_void_p(d_dst), per_frame,
+                                                     C.c_void_p(stream or 0))
+        self._err(rc, "dofs_batch_records_copy")
+
+    def batch_count(self) -> int:
+        return int(self.lib.dofs_batch_count(self.ctx))
 
     STAGES = ("blur", "mst", "mst_sort", "krt", "preorder", "replay", "lift", "labels")
 

@@ -158,19 +158,29 @@ int32_t dofs_segment(dofs_ctx* ctx, const float* flow_uv, int32_t H, int32_t W, 
 int32_t dofs_events(dofs_ctx* ctx, int32_t frame, dofs_event* events, int64_t capacity);
 
 /* Frame-parallel batch on device-resident input: d_flow = B×H×W×2 float32 (device pointer),
- * stream = hipStream_t or NULL (the context's stream). Results stay on the device until
- * dofs_batch_fetch / dofs_batch_records. */
+ * stream = hipStream_t or NULL (the context's stream). Asynchronous: the batch is ordered after the
+ * work already queued on `stream`, and `stream` is ordered after the batch has consumed d_flow.
+ * Batches alternate between two device workspaces and run as a two-stage pipeline (graph stage,
+ * then replay + scoring stage), so consecutive calls overlap. Batch ids count calls from 0; the
+ * results of the last two batches stay readable (dofs_batch_records_copy_id); dofs_batch_fetch,
+ * dofs_events and dofs_batch_records_* read the last one. */
 int32_t dofs_segment_batch_device(dofs_ctx* ctx, const float* d_flow, int32_t B, int32_t H, int32_t W,
                                   const float persp[9], const float inv[9], const float inv_upper[27],
                                   const dofs_params* params, void* stream);
 int32_t dofs_batch_fetch(dofs_ctx* ctx, int32_t frame, dofs_result* out);
-/* Device pointer to the batch's fixed-capacity box records (B × capacity records, frame-major;
- * unused records have slot == -1) and per-frame counts (device int32[B]). */
+/* Device pointers to the last batch's fixed-capacity box records (B × capacity records, frame-major;
+ * unused records have slot == -1) and per-frame counters (device int32, 64 per frame, the snapshot
+ * count at index 4). Waits for the batch; valid until the next-but-one batch is issued. */
 int32_t dofs_batch_records_device(dofs_ctx* ctx, void** d_records, void** d_counts, int32_t* capacity);
 
 /* Copy the batch's box records to a caller device buffer on `stream`: int32 counts[B] (snapshots per
  * frame), then B × per_frame dofs_box_record (the first per_frame records of each frame). */
 int32_t dofs_batch_records_copy(dofs_ctx* ctx, void* d_dst, int32_t per_frame, void* stream);
+/* Same for batch id `batch` (one of the last two issued); ordered after that batch on `stream`. */
+int32_t dofs_batch_records_copy_id(dofs_ctx* ctx, int64_t batch, void* d_dst, int32_t per_frame,
+                                   void* stream);
+/* Number of batches issued on ctx (the last batch id + 1). */
+int64_t dofs_batch_count(dofs_ctx* ctx);
 
 /* Stage timing with device events (0 = off). Stages: 0 blur, 1 MST (Borůvka), 2 MST sort, 3 KRT,
  * 4 preorder, 5 replay, 6 lift + slots, 7 labels. dofs_profile_read returns the accumulated

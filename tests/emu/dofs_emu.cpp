@@ -57,6 +57,14 @@ struct HostBackend {
     bool ok() const { return true; }
     std::string error() const { return std::string(); }
     void set_stream(void*) {}
+    void* cur_stream() const { return nullptr; }
+    void use(void*) {}
+    void* new_stream() { return nullptr; }
+    void* new_event() { return nullptr; }
+    void record(void*, void*) {}
+    void wait(void*, void*) {}
+    void event_sync(void*) {}
+    bool profiling() const { return false; }
     void* alloc(size_t bytes) { return malloc(bytes); }
     void free(void* p) { ::free(p); }
     void memset(void* p, int v, size_t bytes) { ::memset(p, v, bytes); }
@@ -76,8 +84,7 @@ struct HostBackend {
         for (int64_t S = std::min<int64_t>(512, top); S >= 2; S >>= 1) {
             launch(w.d.B, M, KDncUnion{w, S});
             launch(w.d.B, M, KDncCompress{w, S});
-            launch(w.d.B, M, KDncLRoot{w, S});
-            launch(w.d.B, M, KDncRelabelR{w, S});
+            launch(w.d.B, M, KDncLRootRelabel{w, S});
             launch(w.d.B, M, KDncCleanup{w, S});
         }
     }
