@@ -331,7 +331,7 @@ __global__ __launch_bounds__(192) void k_replay_long(Ws w, int round) {
 // runs all of them in LDS: the block's labels get local ids (slots of an LDS hash table), a
 // component created at merge t of the block gets local id kDeepHT + t, and the per-level union /
 // compress / L-root / relabel / cleanup phases of dofs_kernels.h (KDnc*) run between workgroup
-// barriers. Output: the KRT parents found inside the block (MINR) and the sizes of its new
+// barriers. Output: the final endpoint labels of the block's merges (their KRT children) and the sizes of its new
 // components — identical to the global kernels (the union-find shapes differ, results do not).
 // ---------------------------------------------------------------------------------------------
 constexpr int kDeepS = 512;
@@ -371,7 +371,7 @@ __device__ inline int lds_union(int* P, const int* SZ, int a, int b) {
 __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
     __shared__ int keys[kDeepHT];
     __shared__ int P[kDeepL], SZ[kDeepL], CS[kDeepL], MX[kDeepL];
-    __shared__ int lu[kDeepS], lv[kDeepS], own[kDeepS], lrr[kDeepS], minr[kDeepS];
+    __shared__ int lu[kDeepS], lv[kDeepS], own[kDeepS], lrr[kDeepS];
     const Dims& d = w.d;
     const int f = blockIdx.y;
     const int64_t s0 = (int64_t)blockIdx.x * kDeepS;
@@ -385,7 +385,6 @@ __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
         SZ[x] = 0;
         if (x < kDeepHT) keys[x] = -1;
     }
-    for (int t = threadIdx.x; t < kDeepS; t += kDeepT) minr[t] = kIntMax;
     __syncthreads();
     for (int t = threadIdx.x; t < cnt; t += kDeepT) {  // local ids: hash slots of the global labels
         for (int side = 0; side < 2; ++side) {
@@ -443,7 +442,7 @@ __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
             w.SZ[lb + d.N + s0 + t] = sz;
         }
         __syncthreads();
-        for (int t = threadIdx.x; t < cnt; t += kDeepT) {  // relabel R edges, first touching R edge
+        for (int t = threadIdx.x; t < cnt; t += kDeepT) {  // relabel R edges
             if ((t & (S - 1)) < half) continue;
             for (int side = 0; side < 2; ++side) {
                 const int x = side ? lv[t] : lu[t];
@@ -454,7 +453,6 @@ __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
                         lv[t] = kDeepHT + li;
                     else
                         lu[t] = kDeepHT + li;
-                    atomicMin(minr + li, 2 * t + side);
                 }
             }
         }
@@ -471,9 +469,10 @@ __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
         }
         __syncthreads();
     }
-    for (int t = threadIdx.x; t < cnt; t += kDeepT) {
-        const int c = minr[t];
-        if (c != kIntMax) w.MINR[eb + s0 + t] = (int)(2 * (s0 + (c >> 1)) + (c & 1));
+    for (int t = threadIdx.x; t < cnt; t += kDeepT) {  // final labels (the edge's KRT children), global ids
+        const int a = lu[t], b = lv[t];
+        w.lu[eb + s0 + t] = a < kDeepHT ? keys[a] : (int)(d.N + s0 + (a - kDeepHT));
+        w.lv[eb + s0 + t] = b < kDeepHT ? keys[b] : (int)(d.N + s0 + (b - kDeepHT));
     }
 }
 

@@ -74,10 +74,7 @@ struct Ws {
     int* lv;
     int* own;
     int* lrr;
-    int* MINR;
     int* parentE;
-    int* childA;
-    int* childB;
     // label / node space (stride NL)
     int* P;
     int* CS;
@@ -474,10 +471,7 @@ struct KEdgeInit {
         w.EV[o] = (int)q;
         w.lu[o] = (int)p;
         w.lv[o] = (int)q;
-        w.MINR[o] = kIntMax;
         w.parentE[o] = -1;
-        w.childA[o] = -1;
-        w.childB[o] = -1;
         w.own[o] = 0;
     }
 };
@@ -499,23 +493,13 @@ struct KLabelInit {  // clean label state (P[x] = x, MX = -1, CS = 0), pixel siz
     }
 };
 
-// Leaf parent of pixel v = its smallest-rank incident MST edge; side bit = v is Edge::end.
-struct KLeafParent {
-    Ws w;
-    DOFS_HD void operator()(int f, int64_t i) const {
-        const int64_t o = f * w.d.M + i;
-        int* LP = w.LP + f * w.d.N;
-        dofs_amin(LP + w.EU[o], (int)(2 * i));
-        dofs_amin(LP + w.EV[o], (int)(2 * i + 1));
-    }
-};
-
 // ---------------------------------------------------------------------------------------------
 // K3 — KRT by top-down divide and conquer over rank blocks. At depth d with
 // block size S: L = first S/2 ranks of a block, R = the rest. Labels of every edge endpoint are the
 // components at the start of its block (pixel id, or N + max edge rank of the component). The
 // L-edges of all blocks form a forest over a collision-free label space; its components get the
-// label N + (max L rank) and every L-root's KRT parent is the smallest-rank R edge touching it.
+// label N + (max L rank). After the last depth (S = 2) every edge's endpoint labels are the
+// components it merges at its own rank — its two KRT children (KDncParent).
 // ---------------------------------------------------------------------------------------------
 DOFS_HD inline bool dnc_is_L(const Dims& d, int64_t i, int64_t S) {
     const int64_t h = S >> 1;
@@ -590,7 +574,7 @@ struct KDncCompress {
 
 // After KDncCompress (roots final, hooked labels point at them): an L edge whose rank is its
 // component's max (an L-root) gets the component size; an R edge relabels its endpoints to the
-// components' new labels and offers itself as their first touching merge (KRT parent candidate).
+// components' new labels.
 struct KDncLRootRelabel {
     Ws w;
     int64_t S;
@@ -609,16 +593,13 @@ struct KDncLRootRelabel {
             return;
         }
         if (!dnc_is_R(i, S)) return;
-        for (int side = 0; side < 2; ++side) {  // uniform per wave while S/2 >= 64 (aggregation)
+        for (int side = 0; side < 2; ++side) {
             int* lp = side ? (w.lv + o) : (w.lu + o);
             const int x = *lp;
             const int r = w.P[lb + x];
             // x is a label of this block's L forest <=> hooked (P[x] != x) or a touched root (MX set)
             const int li = w.MX[lb + r];
-            const bool act = (r != x) || li >= 0;
-            if (act) *lp = (int)(d.N + li);
-            // smallest-rank R edge touching the L component li (many R edges touch a big one)
-            dofs_agg_min(w.MINR + f * d.M, act ? li : 0, (int)(2 * i + side), act);
+            if (r != x || li >= 0) *lp = (int)(d.N + li);
         }
     }
 };
@@ -641,33 +622,21 @@ struct KDncCleanup {  // restore the clean label state (P[x] = x, MX = -1, CS = 
     }
 };
 
+// Final labels (lu, lv) of edge i = its KRT children (start side A, end side B): every node gets
+// its parent from the one edge whose final label it is. A pixel's parent is its smallest-rank
+// incident MST edge (LP = 2 * rank + side, side 1 = the pixel is Edge::end).
 struct KDncParent {
     Ws w;
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
         const int64_t o = f * d.M + i;
-        const int c = w.MINR[o];
-        if (c == kIntMax) return;
-        const int p = c >> 1;
-        w.parentE[o] = p;
-        if (c & 1)
-            w.childB[f * d.M + p] = (int)(d.N + i);
-        else
-            w.childA[f * d.M + p] = (int)(d.N + i);
-    }
-};
-
-struct KLeafChild {
-    Ws w;
-    DOFS_HD void operator()(int f, int64_t v) const {
-        const Dims& d = w.d;
-        const int c = w.LP[f * d.N + v];
-        if (c == kIntMax) return;
-        const int p = c >> 1;
-        if (c & 1)
-            w.childB[f * d.M + p] = (int)v;
-        else
-            w.childA[f * d.M + p] = (int)v;
+        for (int side = 0; side < 2; ++side) {
+            const int c = side ? w.lv[o] : w.lu[o];
+            if (c >= d.N)
+                w.parentE[f * d.M + (c - d.N)] = (int)i;
+            else
+                w.LP[f * d.N + c] = (int)(2 * i + side);
+        }
     }
 };
 
@@ -688,7 +657,7 @@ DOFS_HD inline int node_parent(const Ws& w, int f, int64_t x) {
 DOFS_HD inline int heavy_child(const Ws& w, int f, int y, int* light, int* light_is_B) {
     const Dims& d = w.d;
     const int64_t e = f * d.M + (y - d.N);
-    const int a = w.childA[e], b = w.childB[e];
+    const int a = w.lu[e], b = w.lv[e];  // final labels = children
     const int sa = w.SZ[f * d.NL + a], sb = w.SZ[f * d.NL + b];
     if (sa >= sb) {
         *light = b;

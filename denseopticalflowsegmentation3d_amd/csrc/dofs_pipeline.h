@@ -120,10 +120,7 @@ struct Pipeline {
         w.lv = (int*)take(4 * B * M);
         w.own = (int*)take(4 * B * M);
         w.lrr = (int*)take(4 * B * M);
-        w.MINR = (int*)take(4 * B * M);
         w.parentE = (int*)take(4 * B * M);
-        w.childA = (int*)take(4 * B * M);
-        w.childB = (int*)take(4 * B * M);
         w.P = (int*)take(4 * B * NL);
         w.CS = (int*)take(4 * B * NL);
         w.MX = (int*)take(4 * B * NL);
@@ -226,7 +223,6 @@ struct Pipeline {
         // K3 Kruskal reconstruction tree
         be.launch(B, M, KEdgeInit{w});
         be.launch(B, NL, KLabelInit{w});
-        be.launch(B, M, KLeafParent{w});
         const int64_t deep = Backend::deep_block();  // levels with block size <= deep run per block
         for (int64_t S = (int64_t)1 << ceil_log2(M); S > deep; S >>= 1) {
             be.launch(B, M, KDncUnion{w, S});
@@ -236,7 +232,6 @@ struct Pipeline {
         }
         be.dnc_deep(w);
         be.launch(B, M, KDncParent{w});
-        be.launch(B, N, KLeafChild{w});
 
         be.mark(4);
         // K4 heavy-first preorder (pointer jumping)
