@@ -44,16 +44,6 @@ constexpr int kStepB = 1;    // light child is the end side (B) of the merge
 constexpr int kStepTop = 2;  // x is the top of its heavy path
 constexpr int kStepDyn = 4;  // light child is a merge node (value produced by the replay)
 
-// Union-find record of one KRT label (pixel or merge node) at one divide-and-conquer depth: every
-// field a depth touches for a label shares one 16-byte record (one memory transaction per label).
-struct Lab {
-    int P;   // union-find parent
-    int SZ;  // component size (pixels)
-    int CS;  // sum of the sizes of the labels hooked below this root
-    int MX;  // max L-edge rank of the component rooted here (-1: untouched)
-};
-static_assert(sizeof(Lab) == 16, "Lab is one 16-byte record");
-
 // Workspace: device pointers (frame-major; per-frame strides by size class) + constants.
 struct Ws {
     Dims d;
@@ -86,8 +76,9 @@ struct Ws {
     int* lrr;
     int* parentE;
     // label / node space (stride NL)
-    Lab* LA0;  // KRT label records of the even / odd divide-and-conquer depths
-    Lab* LA1;
+    int* P;
+    int* CS;
+    int* MX;
     int* SZ;
     int* anc0;
     int* acc0;
@@ -134,7 +125,6 @@ struct Ws {
     double min_convexity[3];
 
     DOFS_HD int* C(int f) const { return ctr + (int64_t)f * kCounters; }
-    DOFS_HD Lab* lab(int q, int f) const { return (q ? LA1 : LA0) + (int64_t)f * d.NL; }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -482,31 +472,24 @@ struct KEdgeInit {
         w.lu[o] = (int)p;
         w.lv[o] = (int)q;
         w.parentE[o] = -1;
-        w.own[o] = -1;
-        w.lrr[o] = -1;
+        w.own[o] = 0;
     }
 };
 
-struct KLabelInit {  // clean label records (P = x, CS = 0, MX = -1), pixel sizes, root size
+struct KLabelInit {  // clean label state (P[x] = x, MX = -1, CS = 0), pixel sizes, root size
     Ws w;
     DOFS_HD void operator()(int f, int64_t x) const {
         const Dims& d = w.d;
         const int64_t o = f * d.NL + x;
-        Lab r;
-        r.P = (int)x;
-        r.SZ = 0;
-        r.CS = 0;
-        r.MX = -1;
+        w.P[o] = (int)x;
+        w.MX[o] = -1;
+        w.CS[o] = 0;
         if (x < d.N) {
-            r.SZ = 1;
             w.SZ[o] = 1;
             w.LP[f * d.N + x] = kIntMax;
         } else if (x == d.NL - 1) {  // KRT root = last merge: the whole frame
-            r.SZ = (int)d.N;
             w.SZ[o] = (int)d.N;
         }
-        w.lab(0, f)[x] = r;
-        w.lab(1, f)[x] = r;
     }
 };
 
@@ -525,78 +508,49 @@ DOFS_HD inline bool dnc_is_L(const Dims& d, int64_t i, int64_t S) {
 }
 DOFS_HD inline bool dnc_is_R(int64_t i, int64_t S) { return (i & (S - 1)) >= (S >> 1); }
 
-// Depths alternate between two label-record arrays (parity of log2 S): depth S dirties its own
-// array, and the next depth's union kernel restores the records depth S dirtied (hooked labels,
-// L-root records) while it works on the other array — no separate cleanup pass.
-DOFS_HD inline int dnc_par(int64_t S) {
-    int k = 0;
-    while (S > 1) {
-        S >>= 1;
-        ++k;
-    }
-    return k & 1;
-}
-
 // Union-find over the label space of one depth, linking by component size (big components stay
 // roots, so the many small components touching one big component hook onto it without CAS
 // contention on its root), ties by hash. Returns the label whose parent pointer this union set:
 // in a forest every edge hooks exactly one label and every non-root label is hooked by exactly one
 // edge, which gives each label a unique owner without atomics.
-DOFS_HD inline int lab_find(Lab* A, int x) {
-    for (;;) {
-        const int p = dofs_ld(&A[x].P);
-        if (p == x) return x;
-        const int gp = dofs_ld(&A[p].P);
-        if (gp == p) return p;
-        dofs_st(&A[x].P, gp);  // path halving
-        x = gp;
-    }
-}
-DOFS_HD inline bool dnc_above(const Lab* A, int a, int b) {  // a is hooked below b
-    const int sa = A[a].SZ, sb = A[b].SZ;
+DOFS_HD inline bool dnc_above(const int* SZ, int a, int b) {  // a is hooked below b
+    const int sa = SZ[a], sb = SZ[b];
     if (sa != sb) return sa < sb;
     return uf_above(a, b);
 }
-DOFS_HD inline int dnc_union(Lab* A, int a, int b) {
+DOFS_HD inline int dnc_union(int* P, const int* SZ, int a, int b) {
     for (;;) {
-        a = lab_find(A, a);
-        b = lab_find(A, b);
+        a = uf_find(P, a);
+        b = uf_find(P, b);
         if (a == b) return -1;  // unreachable: L-edges form a forest over the labels
-        if (!dnc_above(A, a, b)) {
+        if (!dnc_above(SZ, a, b)) {
             int t = a;
             a = b;
             b = t;
         }
-        if (dofs_cas(&A[a].P, a, b) == a) return a;
+        if (dofs_cas(P + a, a, b) == a) return a;
     }
 }
-DOFS_HD inline int walk_compress(Lab* A, int x) {  // no union runs concurrently: plain loads
+DOFS_HD inline int walk_compress(int* P, int x) {  // no union runs concurrently: plain loads
     int r = x;
-    for (int p = A[r].P; p != r; p = A[r].P) r = p;
+    for (int p = P[r]; p != r; p = P[r]) r = p;
     for (int y = x; y != r;) {
-        const int p = A[y].P;
-        if (p != r) A[y].P = r;
+        const int p = P[y];
+        if (p != r) P[y] = r;
         y = p;
     }
     return r;
 }
 
-// Depth S: restore the records depth 2S dirtied (other parity), then union the L edges.
 struct KDncUnion {
     Ws w;
     int64_t S;
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
+        if (!dnc_is_L(d, i, S)) return;
         const int64_t o = f * d.M + i;
-        const int q = dnc_par(S);
-        Lab* prev = w.lab(q ^ 1, f);
-        const int h0 = w.own[o], r0 = w.lrr[o];
-        if (h0 >= 0) prev[h0].P = h0;
-        if (r0 >= 0) {
-            prev[r0].CS = 0;
-            prev[r0].MX = -1;
-        }
-        w.own[o] = dnc_is_L(d, i, S) ? dnc_union(w.lab(q, f), w.lu[o], w.lv[o]) : -1;
+        const int64_t lb = f * d.NL;
+        w.own[o] = dnc_union(w.P + lb, w.SZ + lb, w.lu[o], w.lv[o]);
     }
 };
 
@@ -607,14 +561,14 @@ struct KDncCompress {
         const Dims& d = w.d;
         if (!dnc_is_L(d, i, S)) return;  // uniform per wave while S/2 >= 64 (aggregation below)
         const int64_t o = f * d.M + i;
-        Lab* A = w.lab(dnc_par(S), f);
+        const int64_t lb = f * d.NL;
         const int h = w.own[o];
-        const int r = walk_compress(A, h);
+        const int r = walk_compress(w.P + lb, h);
         // component size over the labels hooked in it (the root label is added by the L-root
         // edge) and the max L-edge rank; wave-aggregated: a big component's root is the key of
-        // most lanes at the top levels (key 4r = record r's word offset)
-        dofs_agg_add(&A[0].CS, 4 * r, A[h].SZ, true);
-        dofs_agg_max(&A[0].MX, 4 * r, (int)i, true);
+        // most lanes at the top levels
+        dofs_agg_add(w.CS + lb, r, w.SZ[lb + h], true);
+        dofs_agg_max(w.MX + lb, r, (int)i, true);
     }
 };
 
@@ -627,32 +581,43 @@ struct KDncLRootRelabel {
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
         const int64_t o = f * d.M + i;
-        const int q = dnc_par(S);
-        Lab* A = w.lab(q, f);
+        const int64_t lb = f * d.NL;
         if (dnc_is_L(d, i, S)) {
-            const int r = A[w.own[o]].P;
-            const Lab R = A[r];
-            if (R.MX != (int)i) {
+            const int r = w.P[lb + w.own[o]];
+            if (w.MX[lb + r] != (int)i) {
                 w.lrr[o] = -1;
                 return;
             }
             w.lrr[o] = r;
-            const int sz = R.CS + R.SZ;
-            const int64_t x = d.N + i;
-            w.lab(0, f)[x].SZ = sz;  // the new label's size, for every later depth of both parities
-            w.lab(1, f)[x].SZ = sz;
-            w.SZ[f * d.NL + x] = sz;
+            w.SZ[lb + d.N + i] = w.CS[lb + r] + w.SZ[lb + r];
             return;
         }
-        w.lrr[o] = -1;
         if (!dnc_is_R(i, S)) return;
         for (int side = 0; side < 2; ++side) {
             int* lp = side ? (w.lv + o) : (w.lu + o);
             const int x = *lp;
-            const int r = A[x].P;
+            const int r = w.P[lb + x];
             // x is a label of this block's L forest <=> hooked (P[x] != x) or a touched root (MX set)
-            const int li = A[r].MX;
+            const int li = w.MX[lb + r];
             if (r != x || li >= 0) *lp = (int)(d.N + li);
+        }
+    }
+};
+
+struct KDncCleanup {  // restore the clean label state (P[x] = x, MX = -1, CS = 0)
+    Ws w;
+    int64_t S;
+    DOFS_HD void operator()(int f, int64_t i) const {
+        const Dims& d = w.d;
+        if (!dnc_is_L(d, i, S)) return;
+        const int64_t o = f * d.M + i;
+        const int64_t lb = f * d.NL;
+        const int h = w.own[o];
+        w.P[lb + h] = h;
+        const int r = w.lrr[o];
+        if (r >= 0) {
+            w.MX[lb + r] = -1;
+            w.CS[lb + r] = 0;
         }
     }
 };

@@ -121,8 +121,9 @@ struct Pipeline {
         w.own = (int*)take(4 * B * M);
         w.lrr = (int*)take(4 * B * M);
         w.parentE = (int*)take(4 * B * M);
-        w.LA0 = (Lab*)take(sizeof(Lab) * B * NL);
-        w.LA1 = (Lab*)take(sizeof(Lab) * B * NL);
+        w.P = (int*)take(4 * B * NL);
+        w.CS = (int*)take(4 * B * NL);
+        w.MX = (int*)take(4 * B * NL);
         w.SZ = (int*)take(4 * B * NL);
         w.anc0 = (int*)take(4 * B * NL);
         w.acc0 = (int*)take(4 * B * NL);
@@ -227,6 +228,7 @@ struct Pipeline {
             be.launch(B, M, KDncUnion{w, S});
             be.launch(B, M, KDncCompress{w, S});
             be.launch(B, M, KDncLRootRelabel{w, S});
+            be.launch(B, M, KDncCleanup{w, S});
         }
         be.dnc_deep(w);
         be.launch(B, M, KDncParent{w});

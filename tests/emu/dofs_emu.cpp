@@ -85,6 +85,7 @@ struct HostBackend {
             launch(w.d.B, M, KDncUnion{w, S});
             launch(w.d.B, M, KDncCompress{w, S});
             launch(w.d.B, M, KDncLRootRelabel{w, S});
+            launch(w.d.B, M, KDncCleanup{w, S});
         }
     }
     void replay_long(const Ws& w, int r) { launch(w.d.B, w.d.N, KReplay{w, r, w.list_long, C_LONG}); }
