@@ -44,6 +44,16 @@ constexpr int kStepB = 1;    // light child is the end side (B) of the merge
 constexpr int kStepTop = 2;  // x is the top of its heavy path
 constexpr int kStepDyn = 4;  // light child is a merge node (value produced by the replay)
 
+// Union-find record of one KRT label (pixel or merge node) at one divide-and-conquer depth: every
+// field a depth touches for a label shares one 16-byte record (one memory transaction per label).
+struct Lab {
+    int P;   // union-find parent
+    int SZ;  // component size (pixels)
+    int CS;  // sum of the sizes of the labels hooked below this root
+    int MX;  // max L-edge rank of the component rooted here (-1: untouched)
+};
+static_assert(sizeof(Lab) == 16, "Lab is one 16-byte record");
+
 // Workspace: device pointers (frame-major; per-frame strides by size class) + constants.
 struct Ws {
     Dims d;
@@ -76,9 +86,7 @@ struct Ws {
     int* lrr;
     int* parentE;
     // label / node space (stride NL)
-    int* P;
-    int* CS;
-    int* MX;
+    Lab* LA;  // KRT label records (union-find state of the current divide-and-conquer depth)
     int* SZ;
     int* anc0;
     int* acc0;
@@ -125,6 +133,7 @@ struct Ws {
     double min_convexity[3];
 
     DOFS_HD int* C(int f) const { return ctr + (int64_t)f * kCounters; }
+    DOFS_HD Lab* lab(int f) const { return LA + (int64_t)f * d.NL; }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -472,24 +481,30 @@ struct KEdgeInit {
         w.lu[o] = (int)p;
         w.lv[o] = (int)q;
         w.parentE[o] = -1;
-        w.own[o] = 0;
+        w.own[o] = -1;
+        w.lrr[o] = -1;
     }
 };
 
-struct KLabelInit {  // clean label state (P[x] = x, MX = -1, CS = 0), pixel sizes, root size
+struct KLabelInit {  // clean label records (P = x, CS = 0, MX = -1), pixel sizes, root size
     Ws w;
     DOFS_HD void operator()(int f, int64_t x) const {
         const Dims& d = w.d;
         const int64_t o = f * d.NL + x;
-        w.P[o] = (int)x;
-        w.MX[o] = -1;
-        w.CS[o] = 0;
+        Lab r;
+        r.P = (int)x;
+        r.SZ = 0;
+        r.CS = 0;
+        r.MX = -1;
         if (x < d.N) {
+            r.SZ = 1;
             w.SZ[o] = 1;
             w.LP[f * d.N + x] = kIntMax;
         } else if (x == d.NL - 1) {  // KRT root = last merge: the whole frame
+            r.SZ = (int)d.N;
             w.SZ[o] = (int)d.N;
         }
+        w.lab(f)[x] = r;
     }
 };
 
@@ -513,30 +528,40 @@ DOFS_HD inline bool dnc_is_R(int64_t i, int64_t S) { return (i & (S - 1)) >= (S 
 // contention on its root), ties by hash. Returns the label whose parent pointer this union set:
 // in a forest every edge hooks exactly one label and every non-root label is hooked by exactly one
 // edge, which gives each label a unique owner without atomics.
-DOFS_HD inline bool dnc_above(const int* SZ, int a, int b) {  // a is hooked below b
-    const int sa = SZ[a], sb = SZ[b];
+DOFS_HD inline int lab_find(Lab* A, int x) {
+    for (;;) {
+        const int p = dofs_ld(&A[x].P);
+        if (p == x) return x;
+        const int gp = dofs_ld(&A[p].P);
+        if (gp == p) return p;
+        dofs_st(&A[x].P, gp);  // path halving
+        x = gp;
+    }
+}
+DOFS_HD inline bool dnc_above(const Lab* A, int a, int b) {  // a is hooked below b
+    const int sa = A[a].SZ, sb = A[b].SZ;
     if (sa != sb) return sa < sb;
     return uf_above(a, b);
 }
-DOFS_HD inline int dnc_union(int* P, const int* SZ, int a, int b) {
+DOFS_HD inline int dnc_union(Lab* A, int a, int b) {
     for (;;) {
-        a = uf_find(P, a);
-        b = uf_find(P, b);
+        a = lab_find(A, a);
+        b = lab_find(A, b);
         if (a == b) return -1;  // unreachable: L-edges form a forest over the labels
-        if (!dnc_above(SZ, a, b)) {
+        if (!dnc_above(A, a, b)) {
             int t = a;
             a = b;
             b = t;
         }
-        if (dofs_cas(P + a, a, b) == a) return a;
+        if (dofs_cas(&A[a].P, a, b) == a) return a;
     }
 }
-DOFS_HD inline int walk_compress(int* P, int x) {  // no union runs concurrently: plain loads
+DOFS_HD inline int walk_compress(Lab* A, int x) {  // no union runs concurrently: plain loads
     int r = x;
-    for (int p = P[r]; p != r; p = P[r]) r = p;
+    for (int p = A[r].P; p != r; p = A[r].P) r = p;
     for (int y = x; y != r;) {
-        const int p = P[y];
-        if (p != r) P[y] = r;
+        const int p = A[y].P;
+        if (p != r) A[y].P = r;
         y = p;
     }
     return r;
@@ -549,8 +574,7 @@ struct KDncUnion {
         const Dims& d = w.d;
         if (!dnc_is_L(d, i, S)) return;
         const int64_t o = f * d.M + i;
-        const int64_t lb = f * d.NL;
-        w.own[o] = dnc_union(w.P + lb, w.SZ + lb, w.lu[o], w.lv[o]);
+        w.own[o] = dnc_union(w.lab(f), w.lu[o], w.lv[o]);
     }
 };
 
@@ -561,14 +585,14 @@ struct KDncCompress {
         const Dims& d = w.d;
         if (!dnc_is_L(d, i, S)) return;  // uniform per wave while S/2 >= 64 (aggregation below)
         const int64_t o = f * d.M + i;
-        const int64_t lb = f * d.NL;
+        Lab* A = w.lab(f);
         const int h = w.own[o];
-        const int r = walk_compress(w.P + lb, h);
+        const int r = walk_compress(A, h);
         // component size over the labels hooked in it (the root label is added by the L-root
         // edge) and the max L-edge rank; wave-aggregated: a big component's root is the key of
-        // most lanes at the top levels
-        dofs_agg_add(w.CS + lb, r, w.SZ[lb + h], true);
-        dofs_agg_max(w.MX + lb, r, (int)i, true);
+        // most lanes at the top levels (key 4r = record r's word offset)
+        dofs_agg_add(&A[0].CS, 4 * r, A[h].SZ, true);
+        dofs_agg_max(&A[0].MX, 4 * r, (int)i, true);
     }
 };
 
@@ -581,43 +605,47 @@ struct KDncLRootRelabel {
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
         const int64_t o = f * d.M + i;
-        const int64_t lb = f * d.NL;
+        Lab* A = w.lab(f);
         if (dnc_is_L(d, i, S)) {
-            const int r = w.P[lb + w.own[o]];
-            if (w.MX[lb + r] != (int)i) {
+            const int r = A[w.own[o]].P;
+            const Lab R = A[r];
+            if (R.MX != (int)i) {
                 w.lrr[o] = -1;
                 return;
             }
             w.lrr[o] = r;
-            w.SZ[lb + d.N + i] = w.CS[lb + r] + w.SZ[lb + r];
+            const int sz = R.CS + R.SZ;
+            const int64_t x = d.N + i;
+            A[x].SZ = sz;
+            w.SZ[f * d.NL + x] = sz;
             return;
         }
         if (!dnc_is_R(i, S)) return;
         for (int side = 0; side < 2; ++side) {
             int* lp = side ? (w.lv + o) : (w.lu + o);
             const int x = *lp;
-            const int r = w.P[lb + x];
+            const int r = A[x].P;
             // x is a label of this block's L forest <=> hooked (P[x] != x) or a touched root (MX set)
-            const int li = w.MX[lb + r];
+            const int li = A[r].MX;
             if (r != x || li >= 0) *lp = (int)(d.N + li);
         }
     }
 };
 
-struct KDncCleanup {  // restore the clean label state (P[x] = x, MX = -1, CS = 0)
+struct KDncCleanup {  // restore the clean records (P = x, CS = 0, MX = -1) this depth dirtied
     Ws w;
     int64_t S;
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
         if (!dnc_is_L(d, i, S)) return;
         const int64_t o = f * d.M + i;
-        const int64_t lb = f * d.NL;
+        Lab* A = w.lab(f);
         const int h = w.own[o];
-        w.P[lb + h] = h;
+        A[h].P = h;
         const int r = w.lrr[o];
         if (r >= 0) {
-            w.MX[lb + r] = -1;
-            w.CS[lb + r] = 0;
+            A[r].CS = 0;
+            A[r].MX = -1;
         }
     }
 };
