@@ -356,8 +356,7 @@ __device__ inline int lds_union(int* P, const int* SZ, int a, int b) {
         a = lds_find(P, a);
         b = lds_find(P, b);
         if (a == b) return -1;
-        const int sa = SZ[a], sb = SZ[b];
-        if (!(sa != sb ? sa < sb : uf_above(a, b))) {  // dnc_above on the LDS arrays
+        if (!dnc_above(SZ, a, b)) {
             const int t = a;
             a = b;
             b = t;

@@ -44,16 +44,6 @@ constexpr int kStepB = 1;    // light child is the end side (B) of the merge
 constexpr int kStepTop = 2;  // x is the top of its heavy path
 constexpr int kStepDyn = 4;  // light child is a merge node (value produced by the replay)
 
-// Union-find record of one KRT label (pixel or merge node) at one divide-and-conquer depth: every
-// field a depth touches for a label shares one 16-byte record (one memory transaction per label).
-struct Lab {
-    int P;   // union-find parent
-    int SZ;  // component size (pixels)
-    int CS;  // sum of the sizes of the labels hooked below this root
-    int MX;  // max L-edge rank of the component rooted here (-1: untouched)
-};
-static_assert(sizeof(Lab) == 16, "Lab is one 16-byte record");
-
 // Workspace: device pointers (frame-major; per-frame strides by size class) + constants.
 struct Ws {
     Dims d;
@@ -86,7 +76,9 @@ struct Ws {
     int* lrr;
     int* parentE;
     // label / node space (stride NL)
-    Lab* LA;  // KRT label records (union-find state of the current divide-and-conquer depth)
+    int* P;
+    int* CS;
+    int* MX;
     int* SZ;
     int* anc0;
     int* acc0;
@@ -133,7 +125,6 @@ struct Ws {
     double min_convexity[3];
 
     DOFS_HD int* C(int f) const { return ctr + (int64_t)f * kCounters; }
-    DOFS_HD Lab* lab(int f) const { return LA + (int64_t)f * d.NL; }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -481,30 +472,24 @@ struct KEdgeInit {
         w.lu[o] = (int)p;
         w.lv[o] = (int)q;
         w.parentE[o] = -1;
-        w.own[o] = -1;
-        w.lrr[o] = -1;
+        w.own[o] = 0;
     }
 };
 
-struct KLabelInit {  // clean label records (P = x, CS = 0, MX = -1), pixel sizes, root size
+struct KLabelInit {  // clean label state (P[x] = x, MX = -1, CS = 0), pixel sizes, root size
     Ws w;
     DOFS_HD void operator()(int f, int64_t x) const {
         const Dims& d = w.d;
         const int64_t o = f * d.NL + x;
-        Lab r;
-        r.P = (int)x;
-        r.SZ = 0;
-        r.CS = 0;
-        r.MX = -1;
+        w.P[o] = (int)x;
+        w.MX[o] = -1;
+        w.CS[o] = 0;
         if (x < d.N) {
-            r.SZ = 1;
             w.SZ[o] = 1;
             w.LP[f * d.N + x] = kIntMax;
         } else if (x == d.NL - 1) {  // KRT root = last merge: the whole frame
-            r.SZ = (int)d.N;
             w.SZ[o] = (int)d.N;
         }
-        w.lab(f)[x] = r;
     }
 };
 
@@ -528,40 +513,30 @@ DOFS_HD inline bool dnc_is_R(int64_t i, int64_t S) { return (i & (S - 1)) >= (S 
 // contention on its root), ties by hash. Returns the label whose parent pointer this union set:
 // in a forest every edge hooks exactly one label and every non-root label is hooked by exactly one
 // edge, which gives each label a unique owner without atomics.
-DOFS_HD inline int lab_find(Lab* A, int x) {
-    for (;;) {
-        const int p = dofs_ld(&A[x].P);
-        if (p == x) return x;
-        const int gp = dofs_ld(&A[p].P);
-        if (gp == p) return p;
-        dofs_st(&A[x].P, gp);  // path halving
-        x = gp;
-    }
-}
-DOFS_HD inline bool dnc_above(const Lab* A, int a, int b) {  // a is hooked below b
-    const int sa = A[a].SZ, sb = A[b].SZ;
+DOFS_HD inline bool dnc_above(const int* SZ, int a, int b) {  // a is hooked below b
+    const int sa = SZ[a], sb = SZ[b];
     if (sa != sb) return sa < sb;
     return uf_above(a, b);
 }
-DOFS_HD inline int dnc_union(Lab* A, int a, int b) {
+DOFS_HD inline int dnc_union(int* P, const int* SZ, int a, int b) {
     for (;;) {
-        a = lab_find(A, a);
-        b = lab_find(A, b);
+        a = uf_find(P, a);
+        b = uf_find(P, b);
         if (a == b) return -1;  // unreachable: L-edges form a forest over the labels
-        if (!dnc_above(A, a, b)) {
+        if (!dnc_above(SZ, a, b)) {
             int t = a;
             a = b;
             b = t;
         }
-        if (dofs_cas(&A[a].P, a, b) == a) return a;
+        if (dofs_cas(P + a, a, b) == a) return a;
     }
 }
-DOFS_HD inline int walk_compress(Lab* A, int x) {  // no union runs concurrently: plain loads
+DOFS_HD inline int walk_compress(int* P, int x) {  // no union runs concurrently: plain loads
     int r = x;
-    for (int p = A[r].P; p != r; p = A[r].P) r = p;
+    for (int p = P[r]; p != r; p = P[r]) r = p;
     for (int y = x; y != r;) {
-        const int p = A[y].P;
-        if (p != r) A[y].P = r;
+        const int p = P[y];
+        if (p != r) P[y] = r;
         y = p;
     }
     return r;
@@ -574,7 +549,8 @@ struct KDncUnion {
         const Dims& d = w.d;
         if (!dnc_is_L(d, i, S)) return;
         const int64_t o = f * d.M + i;
-        w.own[o] = dnc_union(w.lab(f), w.lu[o], w.lv[o]);
+        const int64_t lb = f * d.NL;
+        w.own[o] = dnc_union(w.P + lb, w.SZ + lb, w.lu[o], w.lv[o]);
     }
 };
 
@@ -585,14 +561,14 @@ struct KDncCompress {
         const Dims& d = w.d;
         if (!dnc_is_L(d, i, S)) return;  // uniform per wave while S/2 >= 64 (aggregation below)
         const int64_t o = f * d.M + i;
-        Lab* A = w.lab(f);
+        const int64_t lb = f * d.NL;
         const int h = w.own[o];
-        const int r = walk_compress(A, h);
+        const int r = walk_compress(w.P + lb, h);
         // component size over the labels hooked in it (the root label is added by the L-root
         // edge) and the max L-edge rank; wave-aggregated: a big component's root is the key of
-        // most lanes at the top levels (key 4r = record r's word offset)
-        dofs_agg_add(&A[0].CS, 4 * r, A[h].SZ, true);
-        dofs_agg_max(&A[0].MX, 4 * r, (int)i, true);
+        // most lanes at the top levels
+        dofs_agg_add(w.CS + lb, r, w.SZ[lb + h], true);
+        dofs_agg_max(w.MX + lb, r, (int)i, true);
     }
 };
 
@@ -605,47 +581,43 @@ struct KDncLRootRelabel {
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
         const int64_t o = f * d.M + i;
-        Lab* A = w.lab(f);
+        const int64_t lb = f * d.NL;
         if (dnc_is_L(d, i, S)) {
-            const int r = A[w.own[o]].P;
-            const Lab R = A[r];
-            if (R.MX != (int)i) {
+            const int r = w.P[lb + w.own[o]];
+            if (w.MX[lb + r] != (int)i) {
                 w.lrr[o] = -1;
                 return;
             }
             w.lrr[o] = r;
-            const int sz = R.CS + R.SZ;
-            const int64_t x = d.N + i;
-            A[x].SZ = sz;
-            w.SZ[f * d.NL + x] = sz;
+            w.SZ[lb + d.N + i] = w.CS[lb + r] + w.SZ[lb + r];
             return;
         }
         if (!dnc_is_R(i, S)) return;
         for (int side = 0; side < 2; ++side) {
             int* lp = side ? (w.lv + o) : (w.lu + o);
             const int x = *lp;
-            const int r = A[x].P;
+            const int r = w.P[lb + x];
             // x is a label of this block's L forest <=> hooked (P[x] != x) or a touched root (MX set)
-            const int li = A[r].MX;
+            const int li = w.MX[lb + r];
             if (r != x || li >= 0) *lp = (int)(d.N + li);
         }
     }
 };
 
-struct KDncCleanup {  // restore the clean records (P = x, CS = 0, MX = -1) this depth dirtied
+struct KDncCleanup {  // restore the clean label state (P[x] = x, MX = -1, CS = 0)
     Ws w;
     int64_t S;
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
         if (!dnc_is_L(d, i, S)) return;
         const int64_t o = f * d.M + i;
-        Lab* A = w.lab(f);
+        const int64_t lb = f * d.NL;
         const int h = w.own[o];
-        A[h].P = h;
+        w.P[lb + h] = h;
         const int r = w.lrr[o];
         if (r >= 0) {
-            A[r].CS = 0;
-            A[r].MX = -1;
+            w.MX[lb + r] = -1;
+            w.CS[lb + r] = 0;
         }
     }
 };

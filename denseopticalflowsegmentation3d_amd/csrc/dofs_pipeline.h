@@ -121,7 +121,9 @@ struct Pipeline {
         w.own = (int*)take(4 * B * M);
         w.lrr = (int*)take(4 * B * M);
         w.parentE = (int*)take(4 * B * M);
-        w.LA = (Lab*)take(sizeof(Lab) * B * NL);
+        w.P = (int*)take(4 * B * NL);
+        w.CS = (int*)take(4 * B * NL);
+        w.MX = (int*)take(4 * B * NL);
         w.SZ = (int*)take(4 * B * NL);
         w.anc0 = (int*)take(4 * B * NL);
         w.acc0 = (int*)take(4 * B * NL);
