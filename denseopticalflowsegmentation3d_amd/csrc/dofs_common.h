@@ -4,6 +4,7 @@
 //   DOFS_HD                          function qualifier of per-element kernel bodies
 //   DOFS_HDM                         host+device qualifier of pure math helpers (dofs_lift.h)
 //   dofs_ld / dofs_st                relaxed agent-scope load / store of an int
+//   dofs_ld64 / dofs_st64            relaxed agent-scope load / store of a 64-bit word
 //   dofs_cas / dofs_exch             agent-scope compare-and-swap / exchange of an int
 //   dofs_amin_u64 / dofs_amax_u64    agent-scope atomic min / max of a uint64
 //   dofs_amin / dofs_amax / dofs_aadd / dofs_aor   agent-scope atomics on int

@@ -8,6 +8,9 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <stdlib.h>
+
+#include <algorithm>
 #include <array>
 #include <string>
 #include <vector>
@@ -23,6 +26,12 @@ __device__ inline int dofs_cas(int* p, int expected, int v) {
     return old;
 }
 __device__ inline int dofs_exch(int* p, int v) { return atomicExch(p, v); }
+__device__ inline unsigned long long dofs_ld64(unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void dofs_st64(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ inline void dofs_amin_u64(unsigned long long* p, unsigned long long v) { atomicMin(p, v); }
 __device__ inline void dofs_amax_u64(unsigned long long* p, unsigned long long v) { atomicMax(p, v); }
 __device__ inline void dofs_amin_u32(unsigned* p, unsigned v) { atomicMin(p, v); }
@@ -623,11 +632,21 @@ struct HipBackend {
         return n;
     }
 
+    // total workgroups of one grid-stride launch (all frames): enough to fill 256 CUs several
+    // times over, few enough that near-empty passes (converged rounds) cost little to dispatch
+    static int64_t grid_cap() {
+        static const int64_t cap = [] {
+            const char* e = getenv("DOFS_GRID_CAP");
+            return e ? (int64_t)atoll(e) : (int64_t)16384;
+        }();
+        return cap;
+    }
     template <class F>
     static int launch_on(hipStream_t s, int nf, int64_t n, const F& f) {
         if (n <= 0 || nf <= 0) return DOFS_OK;
         int64_t gx = (n + kBlock - 1) / kBlock;
-        if (gx > 8192) gx = 8192;
+        const int64_t cap = grid_cap() > 0 ? std::max<int64_t>(1, grid_cap() / nf) : 8192;
+        if (gx > cap) gx = cap;
         hipLaunchKernelGGL(k_generic<F>, dim3((unsigned)gx, (unsigned)nf), dim3(kBlock), 0, s, f, n);
         return hipGetLastError() == hipSuccess ? DOFS_OK : DOFS_ERR_DEVICE;
     }

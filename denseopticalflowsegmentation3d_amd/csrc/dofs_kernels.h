@@ -80,10 +80,8 @@ struct Ws {
     int* CS;
     int* MX;
     int* SZ;
-    int* anc0;
-    int* acc0;
-    int* anc1;
-    int* acc1;
+    unsigned long long* J;  // pointer jumping: (ancestor, offset sum) packed (jump_pack)
+    int* pre;               // heavy-first preorder position
     int* ord;
     int* isleaf;
     int* lscan;
@@ -669,6 +667,12 @@ DOFS_HD inline int heavy_child(const Ws& w, int f, int y, int* light, int* light
     return b;
 }
 
+DOFS_HD inline unsigned long long jump_pack(int anc, int sum) {
+    return (unsigned long long)(unsigned)anc | ((unsigned long long)(unsigned)sum << 32);
+}
+DOFS_HD inline int jump_anc(unsigned long long v) { return (int)(unsigned)(v & 0xffffffffu); }
+DOFS_HD inline int jump_sum(unsigned long long v) { return (int)(unsigned)(v >> 32); }
+
 struct KTreeInit {
     Ws w;
     DOFS_HD void operator()(int f, int64_t x) const {
@@ -681,36 +685,34 @@ struct KTreeInit {
             const int h = heavy_child(w, f, p, &lt, &lb);
             off = (h == (int)x) ? 1 : 1 + (2 * w.SZ[f * d.NL + h] - 1);
         }
-        w.anc0[o] = p;
-        w.acc0[o] = off;
+        w.J[o] = jump_pack(p, off);
     }
 };
 
+// In-place asynchronous pointer jumping. Invariant: J[x] = (a, s) with s = the sum of the offsets
+// from x (inclusive) up to its ancestor a (exclusive); a = -1 once s reaches the root. Every
+// 64-bit snapshot of J[a] satisfies it too, so x may jump over a with whatever value of J[a] it
+// reads, in any order: each round at least halves every remaining distance, as the synchronous
+// double-buffered form does, at half the traffic (one array, converged nodes idle).
 struct KJump {
-    const int* anc_in;
-    const int* acc_in;
-    int* anc_out;
-    int* acc_out;
+    unsigned long long* J;
     int64_t NL;
     DOFS_HD void operator()(int f, int64_t x) const {
         const int64_t o = f * NL + x;
-        const int a = anc_in[o];
-        if (a < 0) {
-            anc_out[o] = -1;
-            acc_out[o] = acc_in[o];
-            return;
-        }
-        anc_out[o] = anc_in[f * NL + a];
-        acc_out[o] = acc_in[o] + acc_in[f * NL + a];
+        const unsigned long long v = dofs_ld64(J + o);
+        const int a = jump_anc(v);
+        if (a < 0) return;
+        const unsigned long long u = dofs_ld64(J + f * NL + a);
+        dofs_st64(J + o, jump_pack(jump_anc(u), jump_sum(v) + jump_sum(u)));
     }
 };
 
 struct KOrd {
     Ws w;
-    const int* pre;
     DOFS_HD void operator()(int f, int64_t x) const {
         const Dims& d = w.d;
-        const int q = pre[f * d.NL + x];
+        const int q = jump_sum(w.J[f * d.NL + x]);
+        w.pre[f * d.NL + x] = q;
         w.ord[f * d.NL + q] = (int)x;
         w.isleaf[f * d.NL + q] = x < d.N ? 1 : 0;
     }

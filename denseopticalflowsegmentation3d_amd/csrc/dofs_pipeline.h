@@ -125,10 +125,8 @@ struct Pipeline {
         w.CS = (int*)take(4 * B * NL);
         w.MX = (int*)take(4 * B * NL);
         w.SZ = (int*)take(4 * B * NL);
-        w.anc0 = (int*)take(4 * B * NL);
-        w.acc0 = (int*)take(4 * B * NL);
-        w.anc1 = (int*)take(4 * B * NL);
-        w.acc1 = (int*)take(4 * B * NL);
+        w.J = (unsigned long long*)take(8 * B * NL);
+        w.pre = (int*)take(4 * B * NL);
         w.ord = (int*)take(4 * B * NL);
         w.isleaf = (int*)take(4 * B * NL);
         w.lscan = (int*)take(4 * B * NL);
@@ -236,18 +234,10 @@ struct Pipeline {
         be.mark(4);
         // K4 heavy-first preorder (pointer jumping)
         be.launch(B, NL, KTreeInit{w});
-        int* anc_a = w.anc0;
-        int* acc_a = w.acc0;
-        int* anc_b = w.anc1;
-        int* acc_b = w.acc1;
         const int J = ceil_log2(NL) + 1;
-        for (int t = 0; t < J; ++t) {
-            be.launch(B, NL, KJump{anc_a, acc_a, anc_b, acc_b, NL});
-            std::swap(anc_a, anc_b);
-            std::swap(acc_a, acc_b);
-        }
-        pre = acc_a;
-        be.launch(B, NL, KOrd{w, pre});
+        for (int t = 0; t < J; ++t) be.launch(B, NL, KJump{w.J, NL});
+        pre = w.pre;
+        be.launch(B, NL, KOrd{w});
         be.scan_excl(w.isleaf, w.lscan, NL, B);
         be.launch(B, N, KLeafOrder{w, pre});
         be.launch(B, NL, KPathInit{w, pre});

@@ -26,6 +26,8 @@ inline int dofs_exch(int* p, int v) {
     *p = v;
     return o;
 }
+inline unsigned long long dofs_ld64(unsigned long long* p) { return *p; }
+inline void dofs_st64(unsigned long long* p, unsigned long long v) { *p = v; }
 inline void dofs_amin_u64(unsigned long long* p, unsigned long long v) { *p = std::min(*p, v); }
 inline void dofs_amax_u64(unsigned long long* p, unsigned long long v) { *p = std::max(*p, v); }
 inline void dofs_amin_u32(unsigned* p, unsigned v) { *p = std::min(*p, v); }
