@@ -485,42 +485,6 @@ __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// K2 round 0: tile-local Borůvka (mst_tile in dofs_kernels.h), one 256-lane workgroup per 32x32 tile.
-// ---------------------------------------------------------------------------------------------
-struct LdsOps {
-    __device__ void sync() { __syncthreads(); }
-    __device__ int ld(int* p) { return lds_ld(p); }
-    __device__ void st(int* p, int v) { lds_st(p, v); }
-    __device__ unsigned long long ld64(unsigned long long* p) {
-        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    __device__ void amin64(unsigned long long* p, unsigned long long v) { atomicMin(p, v); }
-    __device__ void amin32(unsigned* p, unsigned v) { atomicMin(p, v); }
-    __device__ void aor(int* p, int v) { atomicOr(p, v); }
-    __device__ bool unite(int* P, int a, int b) {  // hash-priority linking; true if this call linked
-        for (;;) {
-            a = lds_find(P, a);
-            b = lds_find(P, b);
-            if (a == b) return false;
-            if (!uf_above(a, b)) {
-                const int t = a;
-                a = b;
-                b = t;
-            }
-            int old = a;
-            __hip_atomic_compare_exchange_strong(P + a, &old, b, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (old == a) return true;
-        }
-    }
-};
-__global__ __launch_bounds__(256) void k_mst_tiles(Ws w) {
-    __shared__ TileLds S;
-    LdsOps ops;
-    mst_tile(w, blockIdx.y, blockIdx.x, S, threadIdx.x, blockDim.x, ops);
-}
-
 struct HipBackend {
     int device = 0;
     hipStream_t own = nullptr;
@@ -695,11 +659,6 @@ struct HipBackend {
         if (launch_on(stream, nf, n, f) != DOFS_OK) note(hipErrorLaunchFailure, "kernel launch");
     }
 
-    void mst_tiles(const Ws& w) {
-        const unsigned tiles = (unsigned)(((w.d.W + kTileW - 1) / kTileW) * ((w.d.H + kTileH - 1) / kTileH));
-        hipLaunchKernelGGL(k_mst_tiles, dim3(tiles, (unsigned)w.d.B), dim3(256), 0, stream, w);
-        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_mst_tiles launch");
-    }
     static constexpr int64_t deep_block() { return kDeepS; }
     void dnc_deep(const Ws& w) {
         const unsigned nb = (unsigned)((w.d.M + kDeepS - 1) / kDeepS);

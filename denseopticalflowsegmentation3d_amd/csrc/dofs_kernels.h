@@ -279,134 +279,45 @@ DOFS_HD inline int uf_root_ro(const int* P, int x) {  // read-only walk (no writ
 // ---------------------------------------------------------------------------------------------
 // K2 — Borůvka MST on the implicit grid graph, strict order (weight bits, idx).
 // ---------------------------------------------------------------------------------------------
-// Tile-local Borůvka (rounds before the global ones): one workgroup contracts a 32x32 tile in LDS. A component
-// hooks along its minimum incident edge (over ALL its incident edges, tile-crossing ones included)
-// when that edge lies inside the tile — an MST edge by the cut property, exactly as in a global
-// round — and is frozen for the round when it leaves the tile. Rounds repeat until no hook, so every
-// remaining component touches the tile border; the global rounds finish from that contraction.
-// `Ops` supplies the workgroup barrier and the LDS atomics (tid / nt: lane and lane count).
-constexpr int kTileW = 32, kTileH = 32, kTileN = kTileW * kTileH, kTileRounds = 16;
-struct TileLds {
-    unsigned long long wk[4 * kTileN];  // weight bits of the 4 edges each tile pixel emits
-    unsigned long long bw[kTileN];      // per local root: min weight, then min index among ties
-    unsigned bi[kTileN];
-    int par[kTileN];  // local union-find
-    int mst[kTileN];  // MST bits of the edges each tile pixel emits
-    int hooks;
+struct KBoruvkaInit {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t p) const {
+        const int64_t o = f * w.d.N + p;
+        w.comp[o] = (int)p;
+        w.uf[o] = (int)p;
+        w.mstbits[o] = 0;
+    }
 };
 
-template <class Ops>
-DOFS_HD inline void mst_tile(const Ws& w, int f, int tile, TileLds& S, int tid, int nt, Ops& ops) {
-    const Dims& d = w.d;
-    const int tiles_x = (d.W + kTileW - 1) / kTileW;
-    const int x0 = (tile % tiles_x) * kTileW, y0 = (tile / tiles_x) * kTileH;
-    const F2* b = w.blur + f * d.N;
-    auto inside = [&](int x, int y) {
-        return x >= x0 && x < x0 + kTileW && y >= y0 && y < y0 + kTileH && x < d.W && y < d.H;
-    };
-    // incident edge `dir` of pixel (x, y): 0-3 emitted by it (k = dir), 4-7 emitted by its right,
-    // lower, lower-right and upper-right neighbour (k = dir - 4); returns false if absent
-    auto incident = [&](int x, int y, int dir, int& sx, int& sy, int& k, int& qx, int& qy) {
-        k = dir & 3;
-        const int ox = k == 1 ? 0 : -1, oy = k == 0 ? 0 : (k == 3 ? 1 : -1);  // emitter → end offset
-        if (dir < 4) {
-            sx = x;
-            sy = y;
-            if (!edge_exists(d, sx, sy, k)) return false;
-            qx = x + ox;
-            qy = y + oy;
-        } else {
-            sx = x - ox;
-            sy = y - oy;
-            if (sx >= d.W || sy < 0 || sy >= d.H) return false;
-            if (!edge_exists(d, sx, sy, k)) return false;
-            qx = sx;
-            qy = sy;
-        }
-        return true;
-    };
-    auto weight = [&](int sx, int sy, int k) {
-        if (inside(sx, sy)) return S.wk[4 * ((sy - y0) * kTileW + (sx - x0)) + k];
-        const int64_t s = (int64_t)sy * d.W + sx;
-        return dbits(edge_weight(b, s, edge_end(d, s, k)));
-    };
-    for (int l = tid; l < kTileN; l += nt) {
-        S.par[l] = l;
-        S.mst[l] = 0;
-        const int x = x0 + l % kTileW, y = y0 + l / kTileW;
-        for (int k = 0; k < 4; ++k) {
-            unsigned long long v = ~0ull;
-            if (x < d.W && y < d.H && edge_exists(d, x, y, k)) {
-                const int64_t p = (int64_t)y * d.W + x;
-                v = dbits(edge_weight(b, p, edge_end(d, p, k)));
+// Round 0: every pixel is its own component, so its minimum edge is the min over its <= 8 incident
+// edges (4 it emits, 4 its right/lower neighbours emit towards it) — no atomics.
+struct KBoruvkaFirst {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t p) const {
+        const Dims& d = w.d;
+        const int x = (int)(p % d.W), y = (int)(p / d.W);
+        const F2* b = w.blur + f * d.N;
+        unsigned long long best = ~0ull;
+        unsigned bidx = kNoEdge;
+        auto take = [&](int64_t s, int k, int64_t e) {
+            const unsigned long long wb = dbits(edge_weight(b, s, e));
+            const unsigned idx = (unsigned)(4 * s + k);
+            if (wb < best || (wb == best && idx < bidx)) {
+                best = wb;
+                bidx = idx;
             }
-            S.wk[4 * l + k] = v;
-        }
+        };
+        for (int k = 0; k < 4; ++k)
+            if (edge_exists(d, x, y, k)) take(p, k, edge_end(d, p, k));
+        if (x + 1 < d.W) take(p + 1, 0, p);                                       // right: its left edge
+        if (y + 1 < d.H) take(p + d.W, 1, p);                                     // below: its up edge
+        if (d.nbr8 && x + 1 < d.W && y + 1 < d.H) take(p + d.W + 1, 2, p);       // down-right: up-left
+        if (d.nbr8 && x + 1 < d.W && y >= 1) take(p - d.W + 1, 3, p);            // up-right: down-left
+        w.bw[f * d.N + p] = best;
+        w.bi[f * d.N + p] = bidx;
+        if (bidx != kNoEdge && p == 0) w.C(f)[C_ACT + 0] = 1;
     }
-    ops.sync();
-    for (int round = 0; round < kTileRounds; ++round) {
-        for (int l = tid; l < kTileN; l += nt) {
-            S.bw[l] = ~0ull;
-            S.bi[l] = kNoEdge;
-        }
-        if (tid == 0) S.hooks = 0;
-        ops.sync();
-        for (int pass = 0; pass < 2; ++pass) {  // min weight, then min emission index among ties
-            for (int l = tid; l < kTileN; l += nt) {
-                const int x = x0 + l % kTileW, y = y0 + l / kTileW;
-                if (x >= d.W || y >= d.H) continue;
-                const int cp = S.par[l];
-                for (int dir = 0; dir < 8; ++dir) {
-                    int sx, sy, k, qx, qy;
-                    if (!incident(x, y, dir, sx, sy, k, qx, qy)) continue;
-                    if (inside(qx, qy) && S.par[(qy - y0) * kTileW + (qx - x0)] == cp) continue;
-                    const unsigned long long wb = weight(sx, sy, k);
-                    if (pass == 0) {
-                        if (wb < ops.ld64(&S.bw[cp])) ops.amin64(&S.bw[cp], wb);
-                    } else if (wb == S.bw[cp]) {
-                        ops.amin32(&S.bi[cp], (unsigned)(4 * ((int64_t)sy * d.W + sx) + k));
-                    }
-                }
-            }
-            ops.sync();
-        }
-        for (int c = tid; c < kTileN; c += nt) {  // roots at the round start are those with an edge
-            const unsigned e = S.bi[c];
-            if (e == kNoEdge) continue;
-            const int64_t s = e >> 2;
-            const int k = e & 3;
-            const int64_t t = edge_end(d, s, k);
-            const int sx = (int)(s % d.W), sy = (int)(s / d.W), tx = (int)(t % d.W), ty = (int)(t / d.W);
-            if (!inside(sx, sy) || !inside(tx, ty)) continue;  // frozen: its minimum edge leaves the tile
-            const int a = (sy - y0) * kTileW + (sx - x0), z = (ty - y0) * kTileW + (tx - x0);
-            if (ops.unite(S.par, a, z)) {
-                ops.aor(&S.mst[a], 1 << k);
-                S.hooks = 1;
-            }
-        }
-        ops.sync();
-        for (int l = tid; l < kTileN; l += nt) {  // compress: par = root
-            int r = l;
-            for (int p = ops.ld(&S.par[r]); p != r; p = ops.ld(&S.par[r])) r = p;
-            ops.st(&S.par[l], r);
-        }
-        ops.sync();
-        const int any = S.hooks;
-        ops.sync();
-        if (!any) break;
-    }
-    for (int l = tid; l < kTileN; l += nt) {
-        const int x = x0 + l % kTileW, y = y0 + l / kTileW;
-        if (x >= d.W || y >= d.H) continue;
-        const int r = S.par[l];
-        const int64_t p = (int64_t)y * d.W + x, o = f * d.N + p;
-        const int root = (int)((int64_t)(y0 + r / kTileW) * d.W + (x0 + r % kTileW));
-        w.comp[o] = root;
-        w.uf[o] = root;
-        w.mstbits[o] = S.mst[l];
-    }
-    if (tile == 0 && tid == 0 && d.N > 1) w.C(f)[C_ACT + 0] = 1;
-}
+};
 
 struct KBoruvkaReset {  // round r: clear per-component minima
     Ws w;

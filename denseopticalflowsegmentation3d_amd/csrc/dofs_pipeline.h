@@ -197,12 +197,16 @@ struct Pipeline {
 
         be.mark(1);
         // K2 Borůvka MST under (weight, emission index)
-        be.mst_tiles(w);  // round 0: tile-local contraction (mst_tile)
+        be.launch(B, N, KBoruvkaInit{w});
         const int R = std::min(ceil_log2(N) + 2, kRoundsMax - 1);
-        for (int r = 1; r < R; ++r) {
-            be.launch(B, N, KBoruvkaReset{w, r});
-            be.launch(B, N, KBoruvkaMinW{w, r});
-            be.launch(B, N, KBoruvkaMinI{w, r});
+        for (int r = 0; r < R; ++r) {
+            if (r == 0) {
+                be.launch(B, N, KBoruvkaFirst{w});
+            } else {
+                be.launch(B, N, KBoruvkaReset{w, r});
+                be.launch(B, N, KBoruvkaMinW{w, r});
+                be.launch(B, N, KBoruvkaMinI{w, r});
+            }
             be.launch(B, N, KBoruvkaHook{w, r});
             be.launch(B, N, KBoruvkaCompress{w, r});
             be.launch(B, N, KBoruvkaRelabel{w, r});

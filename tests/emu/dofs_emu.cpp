@@ -53,23 +53,6 @@ inline void dofs_agg_min(int* base, int key, int val, bool act) {
 #include "../../denseopticalflowsegmentation3d_amd/csrc/dofs_kernels.h"
 
 namespace dofs {
-struct SeqOps {  // one "lane" running every loop of mst_tile in order
-    void sync() {}
-    int ld(int* p) { return *p; }
-    void st(int* p, int v) { *p = v; }
-    unsigned long long ld64(unsigned long long* p) { return *p; }
-    void amin64(unsigned long long* p, unsigned long long v) { *p = std::min(*p, v); }
-    void amin32(unsigned* p, unsigned v) { *p = std::min(*p, v); }
-    void aor(int* p, int v) { *p |= v; }
-    bool unite(int* P, int a, int b) {
-        while (P[a] != a) a = P[a];
-        while (P[b] != b) b = P[b];
-        if (a == b) return false;
-        if (!uf_above(a, b)) std::swap(a, b);
-        P[a] = b;
-        return true;
-    }
-};
 struct HostBackend {
     explicit HostBackend(int) {}
     static bool device_ok(int) { return true; }
@@ -92,13 +75,6 @@ struct HostBackend {
     void sync() {}
     void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height) {
         for (size_t r = 0; r < height; ++r) memcpy((char*)dst + r * dpitch, (const char*)src + r * spitch, width);
-    }
-    void mst_tiles(const Ws& w) {
-        const int tiles = ((w.d.W + kTileW - 1) / kTileW) * ((w.d.H + kTileH - 1) / kTileH);
-        std::vector<TileLds> S(1);
-        SeqOps ops;
-        for (int f = 0; f < w.d.B; ++f)
-            for (int t = 0; t < tiles; ++t) mst_tile(w, f, t, S[0], 0, 1, ops);
     }
     // the HIP build runs the levels with block size <= 512 per block in LDS (k_dnc_deep); the
     // emulator runs them with the global kernels (same parents and sizes)
