@@ -30,6 +30,33 @@ from denseopticalflowsegmentation3d_amd.frames import FrameParallel  # noqa: E40
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 GATHER_PER_FRAME = 64  # box records per frame in the gathered block
+DEEP_BLOCK = 512  # KRT depths with block size <= this run in LDS (k_dnc_deep), the rest globally
+
+# Algorithmic (compulsory) bytes per active lane of the probed kernels:
+# KDncCompress, per L edge of a depth: own label (4 B read), its parent (4 B read), its size
+# (4 B read), component size CS += (4 B read + 4 B write), max L rank MX (4 B read + 4 B write).
+KERNEL_BYTES = {"KDncCompress": 28}
+
+
+def ceil_log2(n):
+    k = 0
+    while (1 << k) < n:
+        k += 1
+    return k
+
+
+def dnc_L_edges(M):
+    """L edges (lanes doing work) of every global KRT depth launch: block size S > DEEP_BLOCK."""
+    out = []
+    S = 1 << ceil_log2(M)
+    while S > DEEP_BLOCK:
+        h, n = S // 2, 0
+        for s0 in range(0, M, S):
+            if s0 + h < M:
+                n += h
+        out.append(n)
+        S //= 2
+    return out
 
 
 def parse():
@@ -42,6 +69,8 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--cpu-frames", type=int, default=1, help="frames of the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-stages", action="store_true", help="skip the per-stage event timing pass")
+    ap.add_argument("--probe", default="KDncCompress", help="kernel timed with device events for the roofline")
+    ap.add_argument("--pmc", default=None, help="PMC summary JSON (tools/pmc_summary.py) for roofline.traffic")
     return ap.parse_args()
 
 
@@ -104,6 +133,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ctx.probe(a.probe)
+    ctx.probe_read()
     t0 = time.perf_counter()
     e0.record(stream)
     for _ in range(a.steps):
@@ -116,6 +147,8 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     ms_ev = e0.elapsed_time(e1)
+    probe_ms, probe_n = ctx.probe_read()
+    ctx.probe(None)
     t = torch.tensor([max(wall, ms_ev / 1e3)], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -123,8 +156,28 @@ def main():
     frames = world * B * a.steps
     value = frames * N / elapsed / 1e6
 
+    # roofline of the probed kernel: algorithmic bytes of its launches in the timed region over their
+    # device-event time (events recorded on the stream the kernel runs on)
+    roof = None
+    if probe_n:
+        per_launch = [n * B * KERNEL_BYTES[a.probe] for n in dnc_L_edges(N - 1)] if a.probe in KERNEL_BYTES else []
+        launches_per_batch = len(per_launch)
+        assert launches_per_batch and probe_n == launches_per_batch * a.steps, (probe_n, launches_per_batch)
+        alg = sum(per_launch) * a.steps
+        achieved = alg / (probe_ms / 1e3) / 1e9
+        traffic = None
+        if a.pmc and os.path.exists(a.pmc):
+            pm = json.load(open(a.pmc))
+            if pm.get("kernel") == a.probe and pm.get("batch") == B:
+                traffic = pm["hbm_bytes_per_launch"]
+        roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                "kernel": a.probe, "launches": probe_n, "avg_launch_us": round(probe_ms / probe_n * 1e3, 2),
+                "alg_bytes_per_launch": round(alg / probe_n), "alg_bytes_per_lane": KERNEL_BYTES[a.probe],
+                "path_input_roofline_frac": None}
+
     # per-stage device-event timing of extra profiled batches (not part of the timed region)
-    stages, roof = None, None
+    stages = None
     if not a.no_stages:
         ctx.profile(True)
         for _ in range(max(2, a.steps // 2)):
@@ -134,12 +187,8 @@ def main():
         ms, nb = ctx.profile_read()
         ctx.profile(False)
         stages = {k: round(v / nb, 3) for k, v in ms.items()}
-        # the path's input read (8 B/px, the north star's HBM roofline) over the measured batch time
-        t_batch = sum(v for v in ms.values()) / nb / 1e3
-        achieved = B * N * 8 / t_batch / 1e9
-        roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
-                "kernel": "whole path per batch (8 B/px flow read); see DESIGN.md §Roofline"}
+    if roof is not None:  # the north star's whole-path figure: 8 B/px input read over the wall time
+        roof["path_input_roofline_frac"] = round(B * a.steps * N * 8 / elapsed / 1e9 / HBM_PEAK_GBS, 8)
 
     if rank == 0:
         res = ctx.fetch(0, want_blur=False)

@@ -105,6 +105,20 @@ int32_t dofs_profile_read(dofs_ctx* ctx, double ms[8], int32_t* batches) {
     return ctx->check();
 }
 
+int32_t dofs_probe(dofs_ctx* ctx, const char* kernel) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    ctx->be.probe(kernel);
+    return DOFS_OK;
+}
+
+int32_t dofs_probe_read(dofs_ctx* ctx, double* ms, int64_t* launches) {
+    if (!ctx || !ms) return DOFS_ERR_INVALID_ARG;
+    ctx->drain();
+    const int64_t n = ctx->be.probe_read(ms);
+    if (launches) *launches = n;
+    return ctx->check();
+}
+
 int32_t dofs_lift(dofs_ctx* ctx, const float dir[2], const int32_t box[4], const float mat[9], const float inv[9],
                   const float inv_upper[9], int32_t cls, dofs_solution* out) {
     if (!ctx || cls < 0 || cls > 2 || !inv_upper) return DOFS_ERR_INVALID_ARG;

@@ -654,9 +654,52 @@ struct HipBackend {
     static int launch_static(void* s, int nf, int64_t n, const F& f) {
         return launch_on((hipStream_t)s, nf, n, f);
     }
+    // ---- kernel probe: device events around every launch of one named per-element kernel ----
+    std::string probe_name;
+    std::vector<std::array<hipEvent_t, 2>> probe_ev;
+    double probe_ms_acc = 0;
+    int64_t probe_launches = 0;
+    template <class F>
+    static const char* type_name() {
+        return __PRETTY_FUNCTION__;  // "... [F = dofs::KDncCompress]"
+    }
+    void probe(const char* name) { probe_name = name ? name : ""; }
+    int64_t probe_read(double* ms) {
+        for (auto& e : probe_ev) {
+            note(hipEventSynchronize(e[1]), "hipEventSynchronize");
+            float t = 0.f;
+            note(hipEventElapsedTime(&t, e[0], e[1]), "hipEventElapsedTime");
+            probe_ms_acc += t;
+            ++probe_launches;
+            pool.push_back(e[0]);
+            pool.push_back(e[1]);
+        }
+        probe_ev.clear();
+        *ms = probe_ms_acc;
+        const int64_t n = probe_launches;
+        probe_ms_acc = 0;
+        probe_launches = 0;
+        return n;
+    }
     template <class F>
     void launch(int nf, int64_t n, const F& f) {
+        bool probed = false;
+        if (!probe_name.empty() && n > 0 && nf > 0) {
+            const std::string tn = type_name<F>();
+            const size_t at = tn.find("F = dofs::");
+            probed = at != std::string::npos && tn.compare(at + 10, probe_name.size(), probe_name) == 0 &&
+                     (tn.size() == at + 10 + probe_name.size() || tn[at + 10 + probe_name.size()] == ']');
+        }
+        std::array<hipEvent_t, 2> ev{};
+        if (probed) {
+            ev = {ev_get(), ev_get()};
+            note(hipEventRecord(ev[0], stream), "hipEventRecord");
+        }
         if (launch_on(stream, nf, n, f) != DOFS_OK) note(hipErrorLaunchFailure, "kernel launch");
+        if (probed) {
+            note(hipEventRecord(ev[1], stream), "hipEventRecord");
+            probe_ev.push_back(ev);
+        }
     }
 
     static constexpr int64_t deep_block() { return kDeepS; }

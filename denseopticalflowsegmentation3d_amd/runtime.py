@@ -63,6 +63,10 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_profile.restype = C.c_int32
     L.dofs_profile_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), _ip]
     L.dofs_profile_read.restype = C.c_int32
+    L.dofs_probe.argtypes = [C.c_void_p, C.c_char_p]
+    L.dofs_probe.restype = C.c_int32
+    L.dofs_probe_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+    L.dofs_probe_read.restype = C.c_int32
     L.dofs_lift.argtypes = [C.c_void_p, _fp, _ip, _fp, _fp, _fp, C.c_int32, C.POINTER(DofsSolution)]
     L.dofs_lift.restype = C.c_int32
     L.dofs_lift_batch.argtypes = [C.c_void_p, C.c_int32, _fp, _ip, _ip, _fp, _fp, _fp, C.POINTER(DofsSolution)]
@@ -228,6 +232,17 @@ class Dofs:
         n = C.c_int32()
         self._err(self.lib.dofs_profile_read(self.ctx, ms, C.byref(n)), "dofs_profile_read")
         return {k: ms[i] for i, k in enumerate(self.STAGES)}, n.value
+
+    def probe(self, kernel: str | None) -> None:
+        """Time every launch of one per-element kernel (functor name, e.g. "KDncCompress") with device
+        events on the stream it runs on; None switches the probe off."""
+        self._err(self.lib.dofs_probe(self.ctx, (kernel or "").encode()), "dofs_probe")
+
+    def probe_read(self) -> tuple[float, int]:
+        """(accumulated ms, launches) of the probed kernel since the last read."""
+        ms, n = C.c_double(), C.c_int64()
+        self._err(self.lib.dofs_probe_read(self.ctx, C.byref(ms), C.byref(n)), "dofs_probe_read")
+        return ms.value, n.value
 
     def lift(self, direction, box, mat, inv, inv_upper, cls: int) -> dict:
         """get_bottom_variants on the GPU."""

@@ -188,6 +188,12 @@ int64_t dofs_batch_count(dofs_ctx* ctx);
 int32_t dofs_profile(dofs_ctx* ctx, int32_t enable);
 int32_t dofs_profile_read(dofs_ctx* ctx, double ms[8], int32_t* batches);
 
+/* Kernel probe: device events around every launch of the per-element kernel named `kernel` (its
+ * functor name in dofs_kernels.h, e.g. "KDncCompress"; NULL or "" = off), on the stream it runs on.
+ * dofs_probe_read returns the accumulated milliseconds and the launch count, then resets. */
+int32_t dofs_probe(dofs_ctx* ctx, const char* kernel);
+int32_t dofs_probe_read(dofs_ctx* ctx, double* ms, int64_t* launches);
+
 /* get_bottom_variants on the GPU (one candidate, or n candidates with per-candidate class). */
 int32_t dofs_lift(dofs_ctx* ctx, const float dir[2], const int32_t box[4], const float mat[9],
                   const float inv[9], const float inv_upper[9], int32_t cls, dofs_solution* out);

@@ -92,6 +92,11 @@ struct HostBackend {
     }
     void replay_long(const Ws& w, int r) { launch(w.d.B, w.d.N, KReplay{w, r, w.list_long, C_LONG}); }
     void profile(bool) {}
+    void probe(const char*) {}
+    int64_t probe_read(double* ms) {
+        *ms = 0;
+        return 0;
+    }
     void mark(int) {}
     int profile_read(double* ms) {
         for (int s = 0; s < 8; ++s) ms[s] = 0;
