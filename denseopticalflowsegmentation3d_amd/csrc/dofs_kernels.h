@@ -73,7 +73,6 @@ struct Ws {
     int* lu;
     int* lv;
     int* own;
-    int* lrr;
     int* parentE;
     // label / node space (stride NL)
     int* P;
@@ -474,13 +473,13 @@ struct KEdgeInit {
     }
 };
 
-struct KLabelInit {  // clean label state (P[x] = x, MX = -1, CS = 0), pixel sizes, root size
+struct KLabelInit {  // untagged label words (epoch 0), zero counters, pixel sizes, root size
     Ws w;
     DOFS_HD void operator()(int f, int64_t x) const {
         const Dims& d = w.d;
         const int64_t o = f * d.NL + x;
-        w.P[o] = (int)x;
-        w.MX[o] = -1;
+        w.P[o] = 0;  // epoch 0: a root at every depth
+        w.MX[o] = 0;
         w.CS[o] = 0;
         if (x < d.N) {
             w.SZ[o] = 1;
@@ -511,62 +510,97 @@ DOFS_HD inline bool dnc_is_R(int64_t i, int64_t S) { return (i & (S - 1)) >= (S 
 // contention on its root), ties by hash. Returns the label whose parent pointer this union set:
 // in a forest every edge hooks exactly one label and every non-root label is hooked by exactly one
 // edge, which gives each label a unique owner without atomics.
+//
+// Depth tags instead of cleanup passes: parent words are (tag | parent) and max-rank words
+// (tag | rank) with tag = the depth's epoch (1, 2, ... from the top depth down, above the label
+// bits). A word with another depth's tag reads as "root" / "untouched", so nothing a depth writes
+// needs restoring; the one counter (CS) is re-zeroed by the single L-root lane that consumes it.
+constexpr int kLabBits = 27;  // labels < N + M < 2^27 (H*W < 2^26)
+constexpr unsigned kLabMask = (1u << kLabBits) - 1;
+constexpr int kRankBits = 26;  // ranks < M < 2^26; epochs <= 31 keep (epoch << 26 | rank) >= 0
+constexpr int kRankMask = (1 << kRankBits) - 1;
+DOFS_HDM inline int dnc_epoch(int64_t M, int64_t S) {  // 1 at the top depth, +1 per halving
+    int top = 0, s = 0;
+    while (((int64_t)1 << top) < M) ++top;
+    while (((int64_t)1 << s) < S) ++s;
+    return top - s + 1;
+}
+DOFS_HD inline int dnc_find(int* P, int x, unsigned tag) {
+    for (;;) {
+        const unsigned v = (unsigned)dofs_ld(P + x);
+        if ((v & ~kLabMask) != tag) return x;
+        const int p = (int)(v & kLabMask);
+        const unsigned vp = (unsigned)dofs_ld(P + p);
+        if ((vp & ~kLabMask) != tag) return p;
+        const int gp = (int)(vp & kLabMask);
+        dofs_st(P + x, (int)(tag | (unsigned)gp));  // path halving
+        x = gp;
+    }
+}
 DOFS_HD inline bool dnc_above(const int* SZ, int a, int b) {  // a is hooked below b
     const int sa = SZ[a], sb = SZ[b];
     if (sa != sb) return sa < sb;
     return uf_above(a, b);
 }
-DOFS_HD inline int dnc_union(int* P, const int* SZ, int a, int b) {
+DOFS_HD inline int dnc_union(int* P, const int* SZ, int a, int b, unsigned tag) {
     for (;;) {
-        a = uf_find(P, a);
-        b = uf_find(P, b);
+        a = dnc_find(P, a, tag);
+        b = dnc_find(P, b, tag);
         if (a == b) return -1;  // unreachable: L-edges form a forest over the labels
         if (!dnc_above(SZ, a, b)) {
             int t = a;
             a = b;
             b = t;
         }
-        if (dofs_cas(P + a, a, b) == a) return a;
+        const int va = dofs_ld(P + a);
+        if (((unsigned)va & ~kLabMask) == tag) continue;  // hooked meanwhile
+        if (dofs_cas(P + a, va, (int)(tag | (unsigned)b)) == va) return a;
     }
 }
-DOFS_HD inline int walk_compress(int* P, int x) {  // no union runs concurrently: plain loads
+DOFS_HD inline int walk_compress(int* P, int x, unsigned tag) {  // no union runs concurrently
     int r = x;
-    for (int p = P[r]; p != r; p = P[r]) r = p;
+    for (unsigned v = (unsigned)P[r]; (v & ~kLabMask) == tag; v = (unsigned)P[r]) r = (int)(v & kLabMask);
     for (int y = x; y != r;) {
-        const int p = P[y];
-        if (p != r) P[y] = r;
+        const int p = (int)((unsigned)P[y] & kLabMask);
+        if (p != r) P[y] = (int)(tag | (unsigned)r);
         y = p;
     }
     return r;
+}
+DOFS_HD inline int dnc_root(const int* P, int x, unsigned tag) {  // after KDncCompress: one hop
+    const unsigned v = (unsigned)P[x];
+    return (v & ~kLabMask) == tag ? (int)(v & kLabMask) : x;
 }
 
 struct KDncUnion {
     Ws w;
     int64_t S;
+    int ep;
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
         if (!dnc_is_L(d, i, S)) return;
         const int64_t o = f * d.M + i;
         const int64_t lb = f * d.NL;
-        w.own[o] = dnc_union(w.P + lb, w.SZ + lb, w.lu[o], w.lv[o]);
+        w.own[o] = dnc_union(w.P + lb, w.SZ + lb, w.lu[o], w.lv[o], (unsigned)ep << kLabBits);
     }
 };
 
 struct KDncCompress {
     Ws w;
     int64_t S;
+    int ep;
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
         if (!dnc_is_L(d, i, S)) return;  // uniform per wave while S/2 >= 64 (aggregation below)
         const int64_t o = f * d.M + i;
         const int64_t lb = f * d.NL;
         const int h = w.own[o];
-        const int r = walk_compress(w.P + lb, h);
+        const int r = walk_compress(w.P + lb, h, (unsigned)ep << kLabBits);
         // component size over the labels hooked in it (the root label is added by the L-root
-        // edge) and the max L-edge rank; wave-aggregated: a big component's root is the key of
-        // most lanes at the top levels
+        // edge) and the max L-edge rank (depth-tagged); wave-aggregated: a big component's root is
+        // the key of most lanes at the top levels
         dofs_agg_add(w.CS + lb, r, w.SZ[lb + h], true);
-        dofs_agg_max(w.MX + lb, r, (int)i, true);
+        dofs_agg_max(w.MX + lb, r, (ep << kRankBits) | (int)i, true);
     }
 };
 
@@ -576,46 +610,28 @@ struct KDncCompress {
 struct KDncLRootRelabel {
     Ws w;
     int64_t S;
+    int ep;
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
         const int64_t o = f * d.M + i;
         const int64_t lb = f * d.NL;
+        const unsigned tag = (unsigned)ep << kLabBits;
+        const int mtag = ep << kRankBits;
         if (dnc_is_L(d, i, S)) {
-            const int r = w.P[lb + w.own[o]];
-            if (w.MX[lb + r] != (int)i) {
-                w.lrr[o] = -1;
-                return;
-            }
-            w.lrr[o] = r;
+            const int r = dnc_root(w.P + lb, w.own[o], tag);
+            if (w.MX[lb + r] != (mtag | (int)i)) return;
             w.SZ[lb + d.N + i] = w.CS[lb + r] + w.SZ[lb + r];
+            w.CS[lb + r] = 0;  // the only reader of this component's counter
             return;
         }
         if (!dnc_is_R(i, S)) return;
         for (int side = 0; side < 2; ++side) {
             int* lp = side ? (w.lv + o) : (w.lu + o);
             const int x = *lp;
-            const int r = w.P[lb + x];
-            // x is a label of this block's L forest <=> hooked (P[x] != x) or a touched root (MX set)
-            const int li = w.MX[lb + r];
-            if (r != x || li >= 0) *lp = (int)(d.N + li);
-        }
-    }
-};
-
-struct KDncCleanup {  // restore the clean label state (P[x] = x, MX = -1, CS = 0)
-    Ws w;
-    int64_t S;
-    DOFS_HD void operator()(int f, int64_t i) const {
-        const Dims& d = w.d;
-        if (!dnc_is_L(d, i, S)) return;
-        const int64_t o = f * d.M + i;
-        const int64_t lb = f * d.NL;
-        const int h = w.own[o];
-        w.P[lb + h] = h;
-        const int r = w.lrr[o];
-        if (r >= 0) {
-            w.MX[lb + r] = -1;
-            w.CS[lb + r] = 0;
+            const int r = dnc_root(w.P + lb, x, tag);
+            // x is a label of this block's L forest <=> hooked this depth or a touched root
+            const int m = w.MX[lb + r];
+            if (r != x || (m & ~kRankMask) == mtag) *lp = (int)(d.N + (m & kRankMask));
         }
     }
 };

@@ -119,7 +119,6 @@ struct Pipeline {
         w.lu = (int*)take(4 * B * M);
         w.lv = (int*)take(4 * B * M);
         w.own = (int*)take(4 * B * M);
-        w.lrr = (int*)take(4 * B * M);
         w.parentE = (int*)take(4 * B * M);
         w.P = (int*)take(4 * B * NL);
         w.CS = (int*)take(4 * B * NL);
@@ -223,10 +222,10 @@ struct Pipeline {
         be.launch(B, NL, KLabelInit{w});
         const int64_t deep = Backend::deep_block();  // levels with block size <= deep run per block
         for (int64_t S = (int64_t)1 << ceil_log2(M); S > deep; S >>= 1) {
-            be.launch(B, M, KDncUnion{w, S});
-            be.launch(B, M, KDncCompress{w, S});
-            be.launch(B, M, KDncLRootRelabel{w, S});
-            be.launch(B, M, KDncCleanup{w, S});
+            const int ep = dnc_epoch(M, S);
+            be.launch(B, M, KDncUnion{w, S, ep});
+            be.launch(B, M, KDncCompress{w, S, ep});
+            be.launch(B, M, KDncLRootRelabel{w, S, ep});
         }
         be.dnc_deep(w);
         be.launch(B, M, KDncParent{w});

@@ -84,10 +84,10 @@ struct HostBackend {
         int64_t top = 1;
         while (top < M) top <<= 1;
         for (int64_t S = std::min<int64_t>(512, top); S >= 2; S >>= 1) {
-            launch(w.d.B, M, KDncUnion{w, S});
-            launch(w.d.B, M, KDncCompress{w, S});
-            launch(w.d.B, M, KDncLRootRelabel{w, S});
-            launch(w.d.B, M, KDncCleanup{w, S});
+            const int ep = dnc_epoch(M, S);
+            launch(w.d.B, M, KDncUnion{w, S, ep});
+            launch(w.d.B, M, KDncCompress{w, S, ep});
+            launch(w.d.B, M, KDncLRootRelabel{w, S, ep});
         }
     }
     void replay_long(const Ws& w, int r) { launch(w.d.B, w.d.N, KReplay{w, r, w.list_long, C_LONG}); }
