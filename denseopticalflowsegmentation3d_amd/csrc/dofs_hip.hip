@@ -335,18 +335,24 @@ __global__ __launch_bounds__(192) void k_replay_long(Ws w, int round) {
 
 
 // ---------------------------------------------------------------------------------------------
-// K3 deep levels: once the divide-and-conquer block size is kDeepS (512 merges), every remaining
-// level of a block only involves that block's merges and the labels they touch, so one workgroup
-// runs all of them in LDS: the block's labels get local ids (slots of an LDS hash table), a
-// component created at merge t of the block gets local id kDeepHT + t, and the per-level union /
-// compress / L-root / relabel / cleanup phases of dofs_kernels.h (KDnc*) run between workgroup
-// barriers. Output: the final endpoint labels of the block's merges (their KRT children) and the sizes of its new
-// components — identical to the global kernels (the union-find shapes differ, results do not).
+// K3 deep levels: once the divide-and-conquer block size is kDeepS merges, every remaining level of
+// a block only involves that block's merges and the labels they touch, so one workgroup runs all
+// of them in LDS. The block's (at most 2*kDeepS) distinct labels get compact local ids — an LDS
+// hash table of the global labels, then a workgroup scan over its occupied slots — and a component
+// created at merge t of the block gets local id 2*kDeepS + t. The per-level union / compress /
+// L-root / relabel / cleanup phases of dofs_kernels.h (KDnc*) run between workgroup barriers.
+// Output: the final endpoint labels of the block's merges (their KRT children) and the sizes of
+// its new components — identical to the global kernels (union-find shapes differ, results do not).
 // ---------------------------------------------------------------------------------------------
-constexpr int kDeepS = 512;
-constexpr int kDeepHT = 2 * kDeepS * 2;  // hash slots (load factor <= 1/2)
-constexpr int kDeepL = kDeepHT + kDeepS;  // local label space
-constexpr int kDeepT = 256;               // threads per block
+#ifndef DOFS_DEEP_S
+#define DOFS_DEEP_S 2048
+#endif
+constexpr int kDeepS = DOFS_DEEP_S;
+constexpr int kDeepK = 2 * kDeepS;              // distinct labels of a block (two per merge)
+constexpr int kDeepL = kDeepK + kDeepS;         // local label space
+constexpr int kDeepHT = kDeepK + kDeepK / 2;    // hash slots (load factor <= 2/3)
+constexpr int kDeepT = kDeepS >= 2048 ? 1024 : 512;  // threads per block
+static_assert(kDeepL < 32768 && kDeepHT < 32768, "local ids are int16");
 
 __device__ inline int lds_ld(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ inline void lds_st(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
@@ -365,7 +371,8 @@ __device__ inline int lds_union(int* P, const int* SZ, int a, int b) {
         a = lds_find(P, a);
         b = lds_find(P, b);
         if (a == b) return -1;
-        if (!dnc_above(SZ, a, b)) {
+        const int sa = SZ[a], sb = SZ[b];
+        if (!(sa != sb ? sa < sb : uf_above(a, b))) {  // dnc_above on the LDS arrays
             const int t = a;
             a = b;
             b = t;
@@ -377,111 +384,138 @@ __device__ inline int lds_union(int* P, const int* SZ, int a, int b) {
     }
 }
 
+struct DeepShared {
+    int hkey[kDeepHT];    // global label in the slot (-1 empty)
+    short hval[kDeepHT];  // compact local id of the slot
+    int P[kDeepL], SZ[kDeepL], CS[kDeepL], MX[kDeepL];
+    short lu[kDeepS], lv[kDeepS], own[kDeepS], lrr[kDeepS];
+    int wsum[kDeepT / 64];
+};
+
 __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
-    __shared__ int keys[kDeepHT];
-    __shared__ int P[kDeepL], SZ[kDeepL], CS[kDeepL], MX[kDeepL];
-    __shared__ int lu[kDeepS], lv[kDeepS], own[kDeepS], lrr[kDeepS];
+    __shared__ DeepShared sh;
     const Dims& d = w.d;
     const int f = blockIdx.y;
     const int64_t s0 = (int64_t)blockIdx.x * kDeepS;
     if (s0 >= d.M) return;
     const int64_t lb = f * d.NL, eb = f * d.M;
     const int cnt = (int)((d.M - s0) < kDeepS ? (d.M - s0) : kDeepS);
-    for (int x = threadIdx.x; x < kDeepL; x += kDeepT) {
-        P[x] = x;
-        CS[x] = 0;
-        MX[x] = -1;
-        SZ[x] = 0;
-        if (x < kDeepHT) keys[x] = -1;
-    }
+    const int tid = threadIdx.x;
+    for (int x = tid; x < kDeepHT; x += kDeepT) sh.hkey[x] = -1;
     __syncthreads();
-    for (int t = threadIdx.x; t < cnt; t += kDeepT) {  // local ids: hash slots of the global labels
+    for (int t = tid; t < cnt; t += kDeepT) {  // hash the global labels
         for (int side = 0; side < 2; ++side) {
             const int g = side ? w.lv[eb + s0 + t] : w.lu[eb + s0 + t];
-            unsigned h = uf_prio(g) & (kDeepHT - 1);
+            int h = (int)(uf_prio(g) % (unsigned)kDeepHT);
             for (;;) {
                 int old = -1;
-                __hip_atomic_compare_exchange_strong(keys + h, &old, g, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                __hip_atomic_compare_exchange_strong(sh.hkey + h, &old, g, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (old == -1 || old == g) break;
-                h = (h + 1) & (kDeepHT - 1);
+                h = h + 1 == kDeepHT ? 0 : h + 1;
             }
-            if (side)
-                lv[t] = (int)h;
-            else
-                lu[t] = (int)h;
-            SZ[h] = w.SZ[lb + g];
+            (side ? sh.lv : sh.lu)[t] = (short)h;
         }
+    }
+    __syncthreads();
+    {  // compact ids: exclusive scan of slot occupancy (each thread a run of consecutive slots)
+        constexpr int per = (kDeepHT + kDeepT - 1) / kDeepT;
+        const int beg = tid * per, end = min(beg + per, kDeepHT);
+        int c = 0;
+        for (int x = beg; x < end; ++x) c += sh.hkey[x] != -1;
+        int incl = c;  // wave inclusive scan
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (__lane_id() >= o) incl += v;
+        }
+        if (__lane_id() == 63) sh.wsum[tid >> 6] = incl;
+        __syncthreads();
+        int base = incl - c;
+        for (int wv = 0; wv < (tid >> 6); ++wv) base += sh.wsum[wv];
+        for (int x = beg; x < end; ++x)
+            if (sh.hkey[x] != -1) {
+                sh.hval[x] = (short)base;
+                sh.SZ[base] = w.SZ[lb + sh.hkey[x]];
+                ++base;
+            }
+    }
+    for (int x = tid; x < kDeepL; x += kDeepT) {
+        sh.P[x] = x;
+        sh.CS[x] = 0;
+        sh.MX[x] = -1;
+    }
+    __syncthreads();
+    for (int t = tid; t < cnt; t += kDeepT) {
+        sh.lu[t] = sh.hval[sh.lu[t]];
+        sh.lv[t] = sh.hval[sh.lv[t]];
     }
     __syncthreads();
     for (int S = kDeepS; S >= 2; S >>= 1) {
         const int half = S >> 1;
         // union (L edges of sub-blocks whose R half exists)
-        for (int t = threadIdx.x; t < cnt; t += kDeepT) {
+        for (int t = tid; t < cnt; t += kDeepT) {
             const bool isL = (t & (S - 1)) < half && s0 + (t & ~(S - 1)) + half < d.M;
-            if (isL) own[t] = lds_union(P, SZ, lu[t], lv[t]);
+            if (isL) sh.own[t] = (short)lds_union(sh.P, sh.SZ, sh.lu[t], sh.lv[t]);
         }
         __syncthreads();
-        for (int t = threadIdx.x; t < cnt; t += kDeepT) {  // compress + aggregate
+        for (int t = tid; t < cnt; t += kDeepT) {  // compress + aggregate
             const bool isL = (t & (S - 1)) < half && s0 + (t & ~(S - 1)) + half < d.M;
             if (!isL) continue;
-            const int h = own[t];
+            const int h = sh.own[t];
             int r = h;
-            for (int p = lds_ld(P + r); p != r; p = lds_ld(P + r)) r = p;
+            for (int p = lds_ld(sh.P + r); p != r; p = lds_ld(sh.P + r)) r = p;
             for (int y = h; y != r;) {
-                const int p = lds_ld(P + y);
-                if (p != r) lds_st(P + y, r);
+                const int p = lds_ld(sh.P + y);
+                if (p != r) lds_st(sh.P + y, r);
                 y = p;
             }
-            atomicAdd(CS + r, SZ[h]);
-            atomicMax(MX + r, t);
+            atomicAdd(sh.CS + r, sh.SZ[h]);
+            atomicMax(sh.MX + r, t);
         }
         __syncthreads();
-        for (int t = threadIdx.x; t < cnt; t += kDeepT) {  // L-roots: sizes of the new components
+        for (int t = tid; t < cnt; t += kDeepT) {  // L-roots: sizes of the new components
             const bool isL = (t & (S - 1)) < half && s0 + (t & ~(S - 1)) + half < d.M;
             if (!isL) continue;
-            const int r = P[own[t]];
-            if (MX[r] != t) {
-                lrr[t] = -1;
+            const int r = sh.P[sh.own[t]];
+            if (sh.MX[r] != t) {
+                sh.lrr[t] = -1;
                 continue;
             }
-            lrr[t] = r;
-            const int sz = CS[r] + SZ[r];
-            SZ[kDeepHT + t] = sz;
+            sh.lrr[t] = (short)r;
+            const int sz = sh.CS[r] + sh.SZ[r];
+            sh.SZ[kDeepK + t] = sz;
             w.SZ[lb + d.N + s0 + t] = sz;
         }
         __syncthreads();
-        for (int t = threadIdx.x; t < cnt; t += kDeepT) {  // relabel R edges
+        for (int t = tid; t < cnt; t += kDeepT) {  // relabel R edges
             if ((t & (S - 1)) < half) continue;
             for (int side = 0; side < 2; ++side) {
-                const int x = side ? lv[t] : lu[t];
-                const int r = P[x];
-                const int li = MX[r];
-                if (r != x || li >= 0) {
-                    if (side)
-                        lv[t] = kDeepHT + li;
-                    else
-                        lu[t] = kDeepHT + li;
-                }
+                short* lp = side ? sh.lv : sh.lu;
+                const int x = lp[t];
+                const int r = sh.P[x];
+                const int li = sh.MX[r];
+                if (r != x || li >= 0) lp[t] = (short)(kDeepK + li);
             }
         }
         __syncthreads();
-        for (int t = threadIdx.x; t < cnt; t += kDeepT) {  // cleanup
+        for (int t = tid; t < cnt; t += kDeepT) {  // cleanup
             const bool isL = (t & (S - 1)) < half && s0 + (t & ~(S - 1)) + half < d.M;
             if (!isL) continue;
-            P[own[t]] = own[t];
-            const int r = lrr[t];
+            sh.P[sh.own[t]] = sh.own[t];
+            const int r = sh.lrr[t];
             if (r >= 0) {
-                MX[r] = -1;
-                CS[r] = 0;
+                sh.MX[r] = -1;
+                sh.CS[r] = 0;
             }
         }
         __syncthreads();
     }
-    for (int t = threadIdx.x; t < cnt; t += kDeepT) {  // final labels (the edge's KRT children), global ids
-        const int a = lu[t], b = lv[t];
-        w.lu[eb + s0 + t] = a < kDeepHT ? keys[a] : (int)(d.N + s0 + (a - kDeepHT));
-        w.lv[eb + s0 + t] = b < kDeepHT ? keys[b] : (int)(d.N + s0 + (b - kDeepHT));
+    // final labels (the edge's KRT children) as global ids: a local id below kDeepK was never
+    // relabeled, so it is still the edge's own input label
+    for (int t = tid; t < cnt; t += kDeepT) {
+        const int a = sh.lu[t], b = sh.lv[t];
+        if (a >= kDeepK) w.lu[eb + s0 + t] = (int)(d.N + s0 + (a - kDeepK));
+        if (b >= kDeepK) w.lv[eb + s0 + t] = (int)(d.N + s0 + (b - kDeepK));
     }
 }
 

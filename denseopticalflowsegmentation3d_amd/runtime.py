@@ -16,7 +16,7 @@ from .abi import (DofsBoxRecord, DofsEvent, DofsParams, DofsResult, DofsSnapshot
                   solution_dict)
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "_build", "libdofs_hip.so")
+LIB_PATH = os.environ.get("DOFS_LIB") or os.path.join(_PKG, "_build", "libdofs_hip.so")
 _LIBS: dict[str, C.CDLL] = {}
 
 _fp = C.POINTER(C.c_float)

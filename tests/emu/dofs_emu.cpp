@@ -78,12 +78,12 @@ struct HostBackend {
     }
     // the HIP build runs the levels with block size <= 512 per block in LDS (k_dnc_deep); the
     // emulator runs them with the global kernels (same parents and sizes)
-    static constexpr int64_t deep_block() { return 512; }
+    static constexpr int64_t deep_block() { return 2048; }
     void dnc_deep(const Ws& w) {
         const int64_t M = w.d.M;
         int64_t top = 1;
         while (top < M) top <<= 1;
-        for (int64_t S = std::min<int64_t>(512, top); S >= 2; S >>= 1) {
+        for (int64_t S = std::min<int64_t>(deep_block(), top); S >= 2; S >>= 1) {
             const int ep = dnc_epoch(M, S);
             launch(w.d.B, M, KDncUnion{w, S, ep});
             launch(w.d.B, M, KDncCompress{w, S, ep});
