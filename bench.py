@@ -35,7 +35,7 @@ DEEP_BLOCK = int(os.environ.get("DOFS_DEEP_S", "2048"))  # KRT depths with block
 # Algorithmic (compulsory) bytes per active lane of the probed kernels:
 # KDncCompress, per L edge of a depth: own label (4 B read), its parent (4 B read), its size
 # (4 B read), component size CS += (4 B read + 4 B write), max L rank MX (4 B read + 4 B write).
-KERNEL_BYTES = {"KDncCompress": 28}
+KERNEL_BYTES = {"KDncCompress": 28, "k_dnc_compress": 28}
 
 
 def ceil_log2(n):
@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--cpu-frames", type=int, default=1, help="frames of the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-stages", action="store_true", help="skip the per-stage event timing pass")
-    ap.add_argument("--probe", default="KDncCompress", help="kernel timed with device events for the roofline")
+    ap.add_argument("--probe", default="k_dnc_compress", help="kernel timed with device events for the roofline")
     ap.add_argument("--pmc", default=None, help="PMC summary JSON (tools/pmc_summary.py) for roofline.traffic")
     return ap.parse_args()
 

@@ -519,6 +519,59 @@ __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// K3 global depths, compress + aggregate (KDncCompress with workgroup pre-aggregation): agent-scope
+// atomics execute at the memory side (MI355X_MICROARCH.md §Global float atomics; random 4-byte
+// atomics measured at ~27 G/s by tools/atomic_micro.hip), so the 1024 lanes of a workgroup first
+// combine their (component size, max L rank) contributions per root in an LDS hash table, and one
+// lane per distinct root issues the two global atomics.
+// ---------------------------------------------------------------------------------------------
+constexpr int kAggT = 1024, kAggHT = 2048;
+__global__ __launch_bounds__(kAggT) void k_dnc_compress(Ws w, int64_t S, int ep) {
+    __shared__ int hk[kAggHT], hcs[kAggHT], hmx[kAggHT];
+    const Dims& d = w.d;
+    const int f = blockIdx.y;
+    const int64_t lb = f * d.NL;
+    const unsigned tag = (unsigned)ep << kLabBits;
+    const int mtag = ep << kRankBits;
+    const int tid = threadIdx.x;
+    for (int x = tid; x < kAggHT; x += kAggT) {
+        hk[x] = -1;
+        hcs[x] = 0;
+        hmx[x] = 0;
+    }
+    __syncthreads();
+    for (int64_t base = (int64_t)blockIdx.x * kAggT; base < d.M; base += (int64_t)gridDim.x * kAggT) {
+        const int64_t i = base + tid;
+        if (i < d.M && dnc_is_L(d, i, S)) {
+            const int h = w.own[f * d.M + i];
+            const int r = walk_compress(w.P + lb, h, tag);
+            int slot = (int)(uf_prio(r) & (kAggHT - 1));
+            for (;;) {
+                int old = -1;
+                __hip_atomic_compare_exchange_strong(hk + slot, &old, r, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (old == -1 || old == r) break;
+                slot = (slot + 1) & (kAggHT - 1);
+            }
+            atomicAdd(hcs + slot, w.SZ[lb + h]);
+            atomicMax(hmx + slot, mtag | (int)i);
+        }
+        __syncthreads();
+        for (int x = tid; x < kAggHT; x += kAggT) {
+            const int k = hk[x];
+            if (k < 0) continue;
+            atomicAdd(w.CS + lb + k, hcs[x]);
+            const int m = hmx[x];
+            if (__hip_atomic_load(w.MX + lb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < m) atomicMax(w.MX + lb + k, m);
+            hk[x] = -1;
+            hcs[x] = 0;
+            hmx[x] = 0;
+        }
+        __syncthreads();
+    }
+}
+
 struct HipBackend {
     int device = 0;
     hipStream_t own = nullptr;
@@ -715,35 +768,62 @@ struct HipBackend {
         probe_launches = 0;
         return n;
     }
-    template <class F>
-    void launch(int nf, int64_t n, const F& f) {
-        bool probed = false;
-        if (!probe_name.empty() && n > 0 && nf > 0) {
-            const std::string tn = type_name<F>();
-            const size_t at = tn.find("F = dofs::");
-            probed = at != std::string::npos && tn.compare(at + 10, probe_name.size(), probe_name) == 0 &&
-                     (tn.size() == at + 10 + probe_name.size() || tn[at + 10 + probe_name.size()] == ']');
-        }
+    // run `fn` (which enqueues one kernel on `stream`) between probe events if `name` is probed
+    template <class Fn>
+    void timed(const std::string& name, Fn&& fn) {
+        const bool probed = !probe_name.empty() && name == probe_name;
         std::array<hipEvent_t, 2> ev{};
         if (probed) {
             ev = {ev_get(), ev_get()};
             note(hipEventRecord(ev[0], stream), "hipEventRecord");
         }
-        if (launch_on(stream, nf, n, f) != DOFS_OK) note(hipErrorLaunchFailure, "kernel launch");
+        fn();
         if (probed) {
             note(hipEventRecord(ev[1], stream), "hipEventRecord");
             probe_ev.push_back(ev);
         }
     }
+    template <class F>
+    static std::string functor_name() {  // "KDncUnion" from "... [F = dofs::KDncUnion]"
+        const std::string tn = type_name<F>();
+        const size_t at = tn.find("F = dofs::");
+        if (at == std::string::npos) return tn;
+        const size_t end = tn.find_first_of("];", at);
+        return tn.substr(at + 10, end == std::string::npos ? std::string::npos : end - at - 10);
+    }
+    template <class F>
+    void launch(int nf, int64_t n, const F& f) {
+        if (n <= 0 || nf <= 0) return;
+        auto fn = [&] {
+            if (launch_on(stream, nf, n, f) != DOFS_OK) note(hipErrorLaunchFailure, "kernel launch");
+        };
+        if (probe_name.empty())
+            fn();
+        else
+            timed(functor_name<F>(), fn);
+    }
 
     static constexpr int64_t deep_block() { return kDeepS; }
     void dnc_deep(const Ws& w) {
         const unsigned nb = (unsigned)((w.d.M + kDeepS - 1) / kDeepS);
-        hipLaunchKernelGGL(k_dnc_deep, dim3(nb, (unsigned)w.d.B), dim3(kDeepT), 0, stream, w);
+        timed("k_dnc_deep", [&] {
+            hipLaunchKernelGGL(k_dnc_deep, dim3(nb, (unsigned)w.d.B), dim3(kDeepT), 0, stream, w);
+        });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_dnc_deep launch");
     }
+    void dnc_compress(const Ws& w, int64_t S, int ep) {
+        int64_t gx = (w.d.M + kAggT - 1) / kAggT;
+        const int64_t cap = std::max<int64_t>(1, 4096 / w.d.B);
+        if (gx > cap) gx = cap;
+        timed("k_dnc_compress", [&] {
+            hipLaunchKernelGGL(k_dnc_compress, dim3((unsigned)gx, (unsigned)w.d.B), dim3(kAggT), 0, stream, w, S, ep);
+        });
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_dnc_compress launch");
+    }
     void replay_long(const Ws& w, int round) {
-        hipLaunchKernelGGL(k_replay_long, dim3(256u, (unsigned)w.d.B), dim3(192), 0, stream, w, round);
+        timed("k_replay_long", [&] {
+            hipLaunchKernelGGL(k_replay_long, dim3(256u, (unsigned)w.d.B), dim3(192), 0, stream, w, round);
+        });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_replay_long launch");
     }
 

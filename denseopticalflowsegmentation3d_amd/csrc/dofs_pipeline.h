@@ -224,7 +224,7 @@ struct Pipeline {
         for (int64_t S = (int64_t)1 << ceil_log2(M); S > deep; S >>= 1) {
             const int ep = dnc_epoch(M, S);
             be.launch(B, M, KDncUnion{w, S, ep});
-            be.launch(B, M, KDncCompress{w, S, ep});
+            be.dnc_compress(w, S, ep);  // KDncCompress (HIP: workgroup-aggregated atomics)
             be.launch(B, M, KDncLRootRelabel{w, S, ep});
         }
         be.dnc_deep(w);

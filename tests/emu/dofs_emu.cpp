@@ -90,6 +90,7 @@ struct HostBackend {
             launch(w.d.B, M, KDncLRootRelabel{w, S, ep});
         }
     }
+    void dnc_compress(const Ws& w, int64_t S, int ep) { launch(w.d.B, w.d.M, KDncCompress{w, S, ep}); }
     void replay_long(const Ws& w, int r) { launch(w.d.B, w.d.N, KReplay{w, r, w.list_long, C_LONG}); }
     void profile(bool) {}
     void probe(const char*) {}

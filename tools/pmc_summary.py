@@ -27,7 +27,7 @@ def per_dispatch(d, kernel, counter):
     vals = {}
     for r in rows(d):
         name = r.get("Kernel_Name", "")
-        if f"dofs::{kernel}" not in name or r.get("Counter_Name") != counter:
+        if not (f"dofs::{kernel}>" in name or f"dofs::{kernel}(" in name) or r.get("Counter_Name") != counter:
             continue
         vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return list(vals.values())

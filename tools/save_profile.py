@@ -27,7 +27,8 @@ for cnt in ("fetch", "write"):
         wr = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
         wr.writeheader()
         wr.writerows(rows)
-stats = [r for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv"))) if f"dofs::{kernel}>" in r["Name"]]
+stats = [r for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv")))
+         if f"dofs::{kernel}>" in r["Name"] or f"dofs::{kernel}(" in r["Name"]]
 tb = json.loads(open(os.path.join(dst, "trace_bench.json")).read())
 rp_avg = float(stats[0]["AverageNs"]) / 1e3
 ev_avg = tb["roofline"]["avg_launch_us"]
