@@ -5,6 +5,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <stdlib.h>
+
 #include <string>
 #include <vector>
 
@@ -181,7 +183,11 @@ struct Context {
     void* evA[2] = {nullptr, nullptr};
     void* evDone[2] = {nullptr, nullptr};
 
+    bool serial = false;
+
     explicit Context(int device) : be(device), p0(be), p1(be) {
+        const char* e = getenv("DOFS_SERIAL");
+        serial = e && e[0] == '1';
         sA = be.new_stream();
         sB = be.new_stream();
         evIn = be.new_event();
@@ -255,7 +261,8 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
 
     void* caller = be.cur_stream();
     void* sa = cx->sA;
-    void* sb = be.profiling() ? cx->sA : cx->sB;  // stage timing runs the phases back to back
+    // stage timing (and DOFS_SERIAL=1, for clean per-kernel profiles) runs the phases back to back
+    void* sb = (be.profiling() || cx->serial) ? cx->sA : cx->sB;
     be.record(cx->evIn, caller);
     be.wait(sa, cx->evIn);
     if (cx->used[s]) be.wait(sa, cx->evDone[s]);

@@ -139,11 +139,13 @@ constexpr int kLongOk = 8;
 struct LongShared {
     ChainRec chain[2][2][64];  // [wave][buffer][step]
     SideRec side[2][64];       // [buffer][step]
+    int go;                    // blocked step: 1 = its light child completed (continue), 0 = park
 };
+constexpr unsigned long long kSpinTicks = 5000000ull;  // 50 ms of s_memrealtime (100 MHz)
 
 // Resolve position p for wave `wv`. Returns the meta flags (kLongOk when the inputs are ready).
 __device__ inline int long_resolve(const Ws& w, int64_t lb, int p, int top, int round, int wv, ChainRec* cr,
-                                   SideRec* sr, B4* lbb) {
+                                   SideRec* sr, B4* lbb, int accept = -1) {
     lbb->x0 = lbb->y0 = 0x7fff;  // neutral for the bbox scan (positions past the stop)
     lbb->x1 = lbb->y1 = -1;
     if (p < top) return 0;
@@ -153,7 +155,9 @@ __device__ inline int long_resolve(const Ws& w, int64_t lb, int p, int top, int 
     int lrank = 0, lroot = in.lb;
     if (in.meta & kStepDyn) {
         const int lq = in.lb;
-        if (w.ready[lb + lq] >= round) return meta;  // light child completes in a later round
+        // light child not complete in an earlier round (or, at `accept`, in this one: its producer's
+        // release was acquired by this workgroup)
+        if (w.ready[lb + lq] >= (p == accept ? round + 1 : round)) return meta;
         if (wv < 2) {
             wb = (wv ? w.Rmy[lb + lq] : w.Rmx[lb + lq]) * (float)in.la;
         } else {
@@ -202,7 +206,7 @@ __device__ inline B4 bb_shfl_up(B4 b, int delta) {
     return r;
 }
 
-__device__ void replay_long_path(const Ws& w, int f, int jj, int round, LongShared& sh) {
+__device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can_wait, LongShared& sh) {
     const Dims& d = w.d;
     const int j = w.list_long[f * d.N + jj];
     int* curp = w.cur + f * d.N + j;
@@ -301,19 +305,52 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, LongShar
                 w.Rroot[lb + p] = oroot;
             }
         }
-        if (n < 64 || finished) {
-            // all waves stop at the same step (same flags); the top's readiness is read only in
-            // later rounds (kernel boundary), so one wave publishes it
-            if (wv == 2 && lane == 0) {
-                if (finished) {
-                    w.ready[lb + q - n + 1] = round;
-                    *curp = -1;
+        if (finished) {
+            // publish the path top: every wave's output stores, then one agent-scope release, then
+            // the flag (a consumer spinning in this round acquires before reading the outputs)
+            __syncthreads();
+            if (threadIdx.x == 128) {
+                *curp = -1;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                __hip_atomic_store(w.ready + lb + top, round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            return;
+        }
+        if (n < 64) {
+            // blocked at position pb: its light child is a heavy-path top not complete in an earlier
+            // round. A long path (kPendLong) may complete in this round: wait for it (bounded), then
+            // continue; a short path or a path that parked this round: park until the next round.
+            const int pb = q - n;
+            __syncthreads();
+            if (threadIdx.x == 128) {
+                const int lq = w.In[lb + pb].lb;
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                int rd;
+                for (;;) {
+                    rd = __hip_atomic_load(w.ready + lb + lq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (!can_wait || rd <= round || rd == kIntMax || rd == kParkBase - round) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) break;
+                    __builtin_amdgcn_s_sleep(8);
+                }
+                const int go = rd <= round;
+                sh.go = go;
+                if (go) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 } else {
-                    *curp = q - n;
+                    *curp = pb;
+                    __hip_atomic_store(w.ready + lb + top, kParkBase - round, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             __syncthreads();
-            return;
+            if (!sh.go) return;
+            q = pb;  // re-resolve the chunk from the blocked step into the buffer just consumed
+            meta = long_resolve(w, lb, q - lane, top, round, wv, &cr, &sr, &lbb, pb);
+            if (wv < 2)
+                sh.chain[wv][cb][lane] = cr;
+            else
+                sh.side[cb][lane] = sr;
+            continue;
         }
         q -= 64;
         cb ^= 1;
@@ -330,7 +367,9 @@ __global__ __launch_bounds__(192) void k_replay_long(Ws w, int round) {
     __shared__ LongShared sh;
     const int f = blockIdx.y;
     const int n = w.C(f)[C_LONG];
-    for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path(w, f, jj, round, sh);
+    // waiting on another long path is safe only when every long path has its own workgroup
+    const bool can_wait = n <= (int)gridDim.x;
+    for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path(w, f, jj, round, can_wait, sh);
 }
 
 

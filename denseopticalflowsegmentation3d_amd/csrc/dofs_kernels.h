@@ -745,6 +745,10 @@ struct KLeafOrder {
 };
 
 constexpr int kLongPath = 256;  // heavy paths at least this long go to the wave-cooperative replay
+// ready[] at a heavy-path top: the round its path completed, or one of these pending states (all
+// compare >= any round, i.e. "not ready", for the short-path replay)
+constexpr int kPendLong = kIntMax - 1;  // long path, not complete
+constexpr int kParkBase = kIntMax - 2;  // long path stopped in round r: kParkBase - r
 
 
 struct KPathInit {
@@ -787,8 +791,10 @@ struct KPathInit {
                 const int j = dofs_aadd(w.C(f) + C_PATHS, 1);
                 w.cur[f * d.N + j] = qb - 1;
                 w.ptop[f * d.N + j] = q;
-                if (qb - q >= kLongPath)
+                if (qb - q >= kLongPath) {
                     w.list_long[f * d.N + dofs_aadd(w.C(f) + C_LONG, 1)] = j;
+                    w.ready[lb + q] = kPendLong;
+                }
                 else
                     w.list_short[f * d.N + dofs_aadd(w.C(f) + C_SHORT, 1)] = j;
             }
