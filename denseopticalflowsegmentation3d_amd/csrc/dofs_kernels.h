@@ -73,13 +73,14 @@ struct Ws {
     int* lu;
     int* lv;
     int* own;
-    int* parentE;
+    unsigned char* hlB;  // merge i's light child is its end side B
     // label / node space (stride NL)
     int* P;
     int* CS;
     int* MX;
     int* SZ;
     unsigned long long* J;  // pointer jumping: (ancestor, offset sum) packed (jump_pack)
+    unsigned char* lite;    // node is a light child (or the root): the top of a heavy path
     int* pre;               // heavy-first preorder position
     int* ord;
     int* isleaf;
@@ -92,7 +93,6 @@ struct Ws {
     B4* Rbb;
     int* ready;
     // per pixel (stride N)
-    int* LP;
     int* leaf_order;
     int* cur;
     int* ptop;
@@ -468,10 +468,16 @@ struct KEdgeInit {
         w.EV[o] = (int)q;
         w.lu[o] = (int)p;
         w.lv[o] = (int)q;
-        w.parentE[o] = -1;
         w.own[o] = 0;
     }
 };
+
+// pointer-jumping word: (ancestor, offset sum) packed
+DOFS_HD inline unsigned long long jump_pack(int anc, int sum) {
+    return (unsigned long long)(unsigned)anc | ((unsigned long long)(unsigned)sum << 32);
+}
+DOFS_HD inline int jump_anc(unsigned long long v) { return (int)(unsigned)(v & 0xffffffffu); }
+DOFS_HD inline int jump_sum(unsigned long long v) { return (int)(unsigned)(v >> 32); }
 
 struct KLabelInit {  // untagged label words (epoch 0), zero counters, pixel sizes, root size
     Ws w;
@@ -483,9 +489,10 @@ struct KLabelInit {  // untagged label words (epoch 0), zero counters, pixel siz
         w.CS[o] = 0;
         if (x < d.N) {
             w.SZ[o] = 1;
-            w.LP[f * d.N + x] = kIntMax;
-        } else if (x == d.NL - 1) {  // KRT root = last merge: the whole frame
+        } else if (x == d.NL - 1) {  // KRT root = last merge: the whole frame (preorder 0, a path top)
             w.SZ[o] = (int)d.N;
+            w.J[o] = jump_pack(-1, 0);
+            w.lite[o] = 1;
         }
     }
 };
@@ -637,43 +644,37 @@ struct KDncLRootRelabel {
 };
 
 // Final labels (lu, lv) of edge i = its KRT children (start side A, end side B): every node gets
-// its parent from the one edge whose final label it is. A pixel's parent is its smallest-rank
-// incident MST edge (LP = 2 * rank + side, side 1 = the pixel is Edge::end).
+// its parent from the one edge whose final label it is. Here each merge also splits its children
+// into heavy (larger subtree; ties → A) and light, and seeds the heavy-first preorder's pointer
+// jumping (K4): a heavy child sits right after its parent (offset 1), the light one after the
+// parent's whole heavy subtree (offset 1 + 2*size(heavy) - 1). The light child starts a heavy path.
 struct KDncParent {
     Ws w;
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
-        const int64_t o = f * d.M + i;
-        for (int side = 0; side < 2; ++side) {
-            const int c = side ? w.lv[o] : w.lu[o];
-            if (c >= d.N)
-                w.parentE[f * d.M + (c - d.N)] = (int)i;
-            else
-                w.LP[f * d.N + c] = (int)(2 * i + side);
-        }
+        const int64_t o = f * d.M + i, lb = f * d.NL;
+        const int a = w.lu[o], b = w.lv[o];
+        const int sa = w.SZ[lb + a], sb = w.SZ[lb + b];
+        const bool lightB = sa >= sb;
+        const int h = lightB ? a : b, l = lightB ? b : a;
+        const int x = (int)(d.N + i);
+        w.J[lb + h] = jump_pack(x, 1);
+        w.J[lb + l] = jump_pack(x, 2 * (lightB ? sa : sb));
+        w.lite[lb + h] = 0;
+        w.lite[lb + l] = 1;
+        w.hlB[o] = lightB ? 1 : 0;
     }
 };
 
 // ---------------------------------------------------------------------------------------------
 // K4 — heavy-first preorder of the KRT (every heavy path becomes a contiguous range) via
-// pointer jumping over parent links with accumulated offsets.
+// pointer jumping over parent links with accumulated offsets (seeded by KDncParent).
 // ---------------------------------------------------------------------------------------------
-DOFS_HD inline int node_parent(const Ws& w, int f, int64_t x) {
-    const Dims& d = w.d;
-    if (x < d.N) {
-        const int c = w.LP[f * d.N + x];
-        return c == kIntMax ? -1 : (int)(d.N + (c >> 1));
-    }
-    const int p = w.parentE[f * d.M + (x - d.N)];
-    return p < 0 ? -1 : (int)(d.N + p);
-}
-// heavy child of internal node y (larger subtree; ties → start side A)
+// heavy child of internal node y (light side recorded by KDncParent)
 DOFS_HD inline int heavy_child(const Ws& w, int f, int y, int* light, int* light_is_B) {
-    const Dims& d = w.d;
-    const int64_t e = f * d.M + (y - d.N);
+    const int64_t e = f * w.d.M + (y - w.d.N);
     const int a = w.lu[e], b = w.lv[e];  // final labels = children
-    const int sa = w.SZ[f * d.NL + a], sb = w.SZ[f * d.NL + b];
-    if (sa >= sb) {
+    if (w.hlB[e]) {
         *light = b;
         *light_is_B = 1;
         return a;
@@ -682,28 +683,6 @@ DOFS_HD inline int heavy_child(const Ws& w, int f, int y, int* light, int* light
     *light_is_B = 0;
     return b;
 }
-
-DOFS_HD inline unsigned long long jump_pack(int anc, int sum) {
-    return (unsigned long long)(unsigned)anc | ((unsigned long long)(unsigned)sum << 32);
-}
-DOFS_HD inline int jump_anc(unsigned long long v) { return (int)(unsigned)(v & 0xffffffffu); }
-DOFS_HD inline int jump_sum(unsigned long long v) { return (int)(unsigned)(v >> 32); }
-
-struct KTreeInit {
-    Ws w;
-    DOFS_HD void operator()(int f, int64_t x) const {
-        const Dims& d = w.d;
-        const int64_t o = f * d.NL + x;
-        const int p = node_parent(w, f, x);
-        int off = 0;
-        if (p >= 0) {
-            int lt, lb;
-            const int h = heavy_child(w, f, p, &lt, &lb);
-            off = (h == (int)x) ? 1 : 1 + (2 * w.SZ[f * d.NL + h] - 1);
-        }
-        w.J[o] = jump_pack(p, off);
-    }
-};
 
 // In-place asynchronous pointer jumping. Invariant: J[x] = (a, s) with s = the sum of the offsets
 // from x (inclusive) up to its ancestor a (exclusive); a = -1 once s reaches the root. Every
@@ -758,12 +737,7 @@ struct KPathInit {
         const Dims& d = w.d;
         const int64_t lb = f * d.NL;
         const int q = pre[lb + x];
-        const int p = node_parent(w, f, x);
-        bool top = true;
-        if (p >= 0) {
-            int lt, lB;
-            top = heavy_child(w, f, p, &lt, &lB) != (int)x;
-        }
+        const bool top = w.lite[lb + x] != 0;
         if (x >= d.N) {
             int lt, lB;
             const int h = heavy_child(w, f, (int)x, &lt, &lB);

@@ -119,12 +119,13 @@ struct Pipeline {
         w.lu = (int*)take(4 * B * M);
         w.lv = (int*)take(4 * B * M);
         w.own = (int*)take(4 * B * M);
-        w.parentE = (int*)take(4 * B * M);
+        w.hlB = (unsigned char*)take(B * M);
         w.P = (int*)take(4 * B * NL);
         w.CS = (int*)take(4 * B * NL);
         w.MX = (int*)take(4 * B * NL);
         w.SZ = (int*)take(4 * B * NL);
         w.J = (unsigned long long*)take(8 * B * NL);
+        w.lite = (unsigned char*)take(B * NL);
         w.pre = (int*)take(4 * B * NL);
         w.ord = (int*)take(4 * B * NL);
         w.isleaf = (int*)take(4 * B * NL);
@@ -136,7 +137,6 @@ struct Pipeline {
         w.Rroot = (int*)take(4 * B * NL);
         w.Rbb = (B4*)take(sizeof(B4) * B * NL);
         w.ready = (int*)take(4 * B * NL);
-        w.LP = (int*)take(4 * B * N);
         w.leaf_order = (int*)take(4 * B * N);
         w.cur = (int*)take(4 * B * N);
         w.ptop = (int*)take(4 * B * N);
@@ -232,7 +232,6 @@ struct Pipeline {
 
         be.mark(4);
         // K4 heavy-first preorder (pointer jumping)
-        be.launch(B, NL, KTreeInit{w});
         const int J = ceil_log2(NL) + 1;
         for (int t = 0; t < J; ++t) be.launch(B, NL, KJump{w.J, NL});
         pre = w.pre;
