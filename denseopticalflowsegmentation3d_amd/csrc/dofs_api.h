@@ -168,6 +168,7 @@ struct Context {
     };
     Backend be;
     Pipeline<Backend> p0, p1;
+    Pipeline<Backend> pband;  // row-band minimum spanning forests (api_band_msf)
     std::string err;
     void* d_in = nullptr;
     size_t d_in_bytes = 0;
@@ -185,7 +186,7 @@ struct Context {
 
     bool serial = false;
 
-    explicit Context(int device) : be(device), p0(be), p1(be) {
+    explicit Context(int device) : be(device), p0(be), p1(be), pband(be) {
         const char* e = getenv("DOFS_SERIAL");
         serial = e && e[0] == '1';
         sA = be.new_stream();
@@ -235,7 +236,8 @@ struct Context {
 // the input; results are joined by api_fetch / api_events / api_records_copy.
 template <class Backend>
 int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int H, int W, const float persp[9],
-            const float inv[9], const float inv_upper[27], const dofs_params* params) {
+            const float inv[9], const float inv_upper[27], const dofs_params* params,
+            const unsigned char* allow = nullptr) {
     if (B <= 0 || H <= 0 || W <= 0 || !persp || !inv || !inv_upper) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
     if (H > 32767 || W > 32767) return cx->fail(DOFS_ERR_INVALID_ARG, "H and W must be < 32768");
     if ((int64_t)H * W >= (1 << 26)) return cx->fail(DOFS_ERR_INVALID_ARG, "H*W must be < 2^26");
@@ -267,7 +269,9 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     be.wait(sa, cx->evIn);
     if (cx->used[s]) be.wait(sa, cx->evDone[s]);
     be.use(sa);
+    P.w.allow = allow;
     P.run_a(d_flow, fstride);
+    P.w.allow = nullptr;
     be.record(cx->evA[s], sa);
     if (sb != sa) be.wait(sb, cx->evA[s]);
     be.use(sb);
@@ -283,6 +287,36 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     m.H = H;
     m.W = W;
     m.prm = prm;
+    return cx->check();
+}
+
+// One row band's minimum spanning forest (intra-frame sharding): flow rows
+// [row0, row0 + rows) of an H x W frame must contain the band [r0, r1) and its blur halo.
+// Synchronous on the caller's stream; uses a workspace of its own.
+template <class Backend>
+int api_band_msf(Context<Backend>* cx, const F2* d_rows, int row0, int rows, int H, int W, int r0, int r1,
+                 const dofs_params* params, unsigned char* d_mask) {
+    if (!d_rows || !d_mask || H <= 0 || W <= 0 || r0 < 0 || r1 > H || r0 >= r1 || rows <= 0)
+        return cx->fail(DOFS_ERR_INVALID_ARG, "bad band");
+    if ((int64_t)H * W >= (1 << 26) || H > 32767 || W > 32767) return cx->fail(DOFS_ERR_INVALID_ARG, "frame too large");
+    dofs_params prm;
+    if (params)
+        prm = *params;
+    else
+        default_params(&prm);
+    float taps[kMaxTaps];
+    const int R = gaussian_taps(prm.blur_sigma, taps) / 2;
+    const int need0 = r0 - R < 0 ? 0 : r0 - R, need1 = r1 + R > H ? H : r1 + R;
+    if (row0 > need0 || row0 + rows < need1 || row0 < 0 || row0 + rows > H)
+        return cx->fail(DOFS_ERR_INVALID_ARG, "flow rows must cover the band and its blur halo");
+    const int nbr8 = prm.neighbor == 8 ? 1 : 0;
+    Pipeline<Backend>& P = cx->pband;  // its own workspace: batches in flight are untouched
+    if (!P.reserve(Pipeline<Backend>::dims_for(1, rows, W, nbr8))) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    const float z9[9] = {0};
+    const float z27[27] = {0};
+    P.set_params(prm, z9, z9, z27);
+    P.run_band(d_rows, row0, rows, H, r0, r1, d_mask);
+    cx->be.sync();
     return cx->check();
 }
 

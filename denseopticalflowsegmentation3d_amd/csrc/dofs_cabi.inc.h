@@ -64,6 +64,23 @@ int32_t dofs_segment_batch_device(dofs_ctx* ctx, const float* d_flow, int32_t B,
     return dofs::api_run(ctx, (const dofs::F2*)d_flow, (int64_t)H * W, B, H, W, persp, inv, inv_upper, params);
 }
 
+int32_t dofs_band_msf_device(dofs_ctx* ctx, const float* d_flow_rows, int32_t row0, int32_t rows, int32_t H,
+                             int32_t W, int32_t band_r0, int32_t band_r1, const dofs_params* params,
+                             uint8_t* d_mask, void* stream) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    ctx->be.set_stream(stream);
+    return dofs::api_band_msf(ctx, (const dofs::F2*)d_flow_rows, row0, rows, H, W, band_r0, band_r1, params, d_mask);
+}
+
+int32_t dofs_segment_masked_device(dofs_ctx* ctx, const float* d_flow, int32_t H, int32_t W,
+                                   const uint8_t* d_allowed, const float persp[9], const float inv[9],
+                                   const float inv_upper[27], const dofs_params* params, void* stream) {
+    if (!ctx || !d_flow || !d_allowed) return DOFS_ERR_INVALID_ARG;
+    ctx->be.set_stream(stream);
+    return dofs::api_run(ctx, (const dofs::F2*)d_flow, (int64_t)H * W, 1, H, W, persp, inv, inv_upper, params,
+                         d_allowed);
+}
+
 int32_t dofs_batch_fetch(dofs_ctx* ctx, int32_t frame, dofs_result* out) {
     if (!ctx) return DOFS_ERR_INVALID_ARG;
     return dofs::api_fetch(ctx, frame, out);

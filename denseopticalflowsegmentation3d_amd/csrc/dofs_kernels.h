@@ -49,7 +49,8 @@ struct Ws {
     Dims d;
     // inputs
     const F2* flow;
-    int64_t flow_fstride;  // F2 elements between frames of the input
+    int64_t flow_fstride;          // F2 elements between frames of the input
+    const unsigned char* allow;    // optional: bit k of allow[p] = edge (p, k) may be in the MST
     // blur
     F2* tmp;
     F2* blur;
@@ -168,6 +169,11 @@ DOFS_HD inline double bitsd(unsigned long long u) {
     return c.d;
 }
 
+// Edge (s, k) is a candidate of the MST search (all edges, or the allowed subset of a sharded frame)
+DOFS_HD inline bool edge_allowed(const Ws& w, int f, int64_t s, int k) {
+    return !w.allow || ((w.allow[f * w.d.N + s] >> k) & 1);
+}
+
 // cv::borderInterpolate(p, len, BORDER_REFLECT_101)
 DOFS_HD inline int reflect101(int p, int len) {
     if ((unsigned)p < (unsigned)len) return p;
@@ -224,6 +230,31 @@ struct KBlurCol {
         o.x = sx;
         o.y = sy;
         w.blur[f * w.d.N + i] = o;
+    }
+};
+
+// Column pass of a row band [r0, r0 + d.H) of an image of height Himg, from row-filtered rows
+// [row0, row0 + rows) that include the blur halo: identical to KBlurCol on the whole image.
+struct KBlurColBand {
+    Ws w;
+    int Himg, row0, r0;
+    DOFS_HD void operator()(int f, int64_t i) const {
+        const int W = w.d.W;
+        const int y = r0 + (int)(i / W), x = (int)(i % W);
+        const F2* t = w.tmp;
+        const int r = w.bn / 2;
+        F2 c = t[(int64_t)(y - row0) * W + x];
+        float sx = w.bk[r] * c.x + 0.0f, sy = w.bk[r] * c.y + 0.0f;
+        for (int j = 1; j <= r; ++j) {
+            F2 a = t[(int64_t)(reflect101(y + j, Himg) - row0) * W + x];
+            F2 b = t[(int64_t)(reflect101(y - j, Himg) - row0) * W + x];
+            sx += w.bk[r + j] * (a.x + b.x);
+            sy += w.bk[r + j] * (a.y + b.y);
+        }
+        F2 o;
+        o.x = sx;
+        o.y = sy;
+        w.blur[i] = o;
     }
 };
 
@@ -299,6 +330,7 @@ struct KBoruvkaFirst {
         unsigned long long best = ~0ull;
         unsigned bidx = kNoEdge;
         auto take = [&](int64_t s, int k, int64_t e) {
+            if (!edge_allowed(w, f, s, k)) return;
             const unsigned long long wb = dbits(edge_weight(b, s, e));
             const unsigned idx = (unsigned)(4 * s + k);
             if (wb < best || (wb == best && idx < bidx)) {
@@ -342,7 +374,7 @@ struct KBoruvkaMinW {
         const int cp = comp[p];
         bool any = false;
         for (int k = 0; k < 4; ++k) {
-            if (!edge_exists(d, x, y, k)) continue;
+            if (!edge_exists(d, x, y, k) || !edge_allowed(w, f, p, k)) continue;
             const int64_t q = edge_end(d, p, k);
             const int cq = comp[q];
             if (cp == cq) continue;
@@ -368,7 +400,7 @@ struct KBoruvkaMinI {
         unsigned* bi = w.bi + f * d.N;
         const int cp = comp[p];
         for (int k = 0; k < 4; ++k) {
-            if (!edge_exists(d, x, y, k)) continue;
+            if (!edge_exists(d, x, y, k) || !edge_allowed(w, f, p, k)) continue;
             const int64_t q = edge_end(d, p, k);
             const int cq = comp[q];
             if (cp == cq) continue;
@@ -429,6 +461,12 @@ struct KBoruvkaRelabel {
 // ---------------------------------------------------------------------------------------------
 // MST edge list in emission order, then (after the radix sort) in Kruskal order.
 // ---------------------------------------------------------------------------------------------
+struct KMaskOut {  // a band's minimum spanning forest as per-pixel emitted-edge bits
+    Ws w;
+    unsigned char* mask;
+    DOFS_HD void operator()(int, int64_t p) const { mask[p] = (unsigned char)w.mstbits[p]; }
+};
+
 struct KMstCount {
     Ws w;
     DOFS_HD void operator()(int f, int64_t p) const {

@@ -172,6 +172,50 @@ struct Pipeline {
         w.overlay_min_score = prm.overlay_min_score;
     }
 
+    // K2 Borůvka MST under (weight, emission index) of the frames in w (edges limited to w.allow)
+    void boruvka() {
+        const Dims& d = w.d;
+        const int B = d.B;
+        const int64_t N = d.N;
+        be.launch(B, N, KBoruvkaInit{w});
+        const int R = std::min(ceil_log2(N) + 2, kRoundsMax - 1);
+        for (int r = 0; r < R; ++r) {
+            if (r == 0) {
+                be.launch(B, N, KBoruvkaFirst{w});
+            } else {
+                be.launch(B, N, KBoruvkaReset{w, r});
+                be.launch(B, N, KBoruvkaMinW{w, r});
+                be.launch(B, N, KBoruvkaMinI{w, r});
+            }
+            be.launch(B, N, KBoruvkaHook{w, r});
+            be.launch(B, N, KBoruvkaCompress{w, r});
+            be.launch(B, N, KBoruvkaRelabel{w, r});
+        }
+    }
+
+    // Minimum spanning forest of the row band [r0, r1) of an H x W frame (edges with both ends in the
+    // band), from device flow rows [row0, row0 + rows) that include the blur halo; writes the
+    // forest's edges as per-pixel emitted-edge bits (mask[(y - r0) * W + x]). The caller reserved
+    // dims_for(1, rows, W, nbr8).
+    void run_band(const F2* flow_rows, int row0, int rows, int H, int r0, int r1, unsigned char* mask) {
+        const int nbr8 = w.d.nbr8;
+        Ws wr = w;
+        wr.d = dims_for(1, rows, w.d.W, nbr8);
+        wr.flow = flow_rows;
+        wr.flow_fstride = (int64_t)rows * w.d.W;
+        be.launch(1, wr.d.N, KBlurRow{wr});
+        w.d = dims_for(1, r1 - r0, w.d.W, nbr8);
+        w.allow = nullptr;
+        be.launch(1, w.d.N, KBlurColBand{w, H, row0, r0});
+        be.memset(w.ctr, 0, sizeof(int) * kCounters);
+        if (w.d.N > 1) {
+            boruvka();
+        } else {
+            be.memset(w.mstbits, 0, sizeof(int));
+        }
+        be.launch(1, w.d.N, KMaskOut{w, mask});
+    }
+
     // Phase A (graph): blur, MST, Kruskal order, KRT, preorder, replay inputs — on B frames of
     // device-resident flow (frame stride fstride F2 elements). Throughput-bound.
     void run_a(const F2* flow, int64_t fstride) {
@@ -195,21 +239,7 @@ struct Pipeline {
         }
 
         be.mark(1);
-        // K2 Borůvka MST under (weight, emission index)
-        be.launch(B, N, KBoruvkaInit{w});
-        const int R = std::min(ceil_log2(N) + 2, kRoundsMax - 1);
-        for (int r = 0; r < R; ++r) {
-            if (r == 0) {
-                be.launch(B, N, KBoruvkaFirst{w});
-            } else {
-                be.launch(B, N, KBoruvkaReset{w, r});
-                be.launch(B, N, KBoruvkaMinW{w, r});
-                be.launch(B, N, KBoruvkaMinI{w, r});
-            }
-            be.launch(B, N, KBoruvkaHook{w, r});
-            be.launch(B, N, KBoruvkaCompress{w, r});
-            be.launch(B, N, KBoruvkaRelabel{w, r});
-        }
+        boruvka();
         be.mark(2);
         be.launch(B, N, KMstCount{w});
         be.scan_excl(w.cnt, w.off, N, B);

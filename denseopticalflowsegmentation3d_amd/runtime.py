@@ -49,6 +49,12 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_segment_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, _fp, _fp, _fp,
                                             C.POINTER(DofsParams), C.c_void_p]
     L.dofs_segment_batch_device.restype = C.c_int32
+    L.dofs_band_msf_device.argtypes = [C.c_void_p, C.c_void_p] + [C.c_int32] * 6 + [C.POINTER(DofsParams), C.c_void_p,
+                                                                                C.c_void_p]
+    L.dofs_band_msf_device.restype = C.c_int32
+    L.dofs_segment_masked_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, _fp, _fp, _fp,
+                                             C.POINTER(DofsParams), C.c_void_p]
+    L.dofs_segment_masked_device.restype = C.c_int32
     L.dofs_batch_fetch.argtypes = [C.c_void_p, C.c_int32, C.POINTER(DofsResult)]
     L.dofs_batch_fetch.restype = C.c_int32
     L.dofs_batch_records_device.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _ip]
@@ -193,6 +199,27 @@ class Dofs:
         rc = self.lib.dofs_segment_batch_device(self.ctx, C.c_void_p(d_flow), B, H, W, _p(p), _p(i), _p(u),
                                                 C.byref(params or default_params()), C.c_void_p(stream or 0))
         self._err(rc, "dofs_segment_batch_device")
+        self._last_hw = (H, W)
+        return int(self.lib.dofs_batch_count(self.ctx)) - 1
+
+    def band_msf_device(self, d_rows: int, row0: int, rows: int, H: int, W: int, r0: int, r1: int, d_mask: int,
+                        params: DofsParams | None = None, stream: int | None = None) -> None:
+        """Minimum spanning forest of rows [r0, r1) of an H x W frame as per-pixel edge bits (device
+        uint8 (r1 - r0) x W), from device flow rows [row0, row0 + rows) covering the band + blur halo."""
+        rc = self.lib.dofs_band_msf_device(self.ctx, C.c_void_p(d_rows), row0, rows, H, W, r0, r1,
+                                           C.byref(params or default_params()), C.c_void_p(d_mask),
+                                           C.c_void_p(stream or 0))
+        self._err(rc, "dofs_band_msf_device")
+
+    def segment_masked_device(self, d_flow: int, H: int, W: int, d_allowed: int, persp, inv, inv_upper,
+                              params: DofsParams | None = None, stream: int | None = None) -> int:
+        """One device frame with the MST search limited to the allowed edges (device uint8 H x W edge bits).
+        Asynchronous; returns the batch id (read with fetch / events / records_*)."""
+        p, i, u = self._mats(persp, inv, inv_upper)
+        rc = self.lib.dofs_segment_masked_device(self.ctx, C.c_void_p(d_flow), H, W, C.c_void_p(d_allowed), _p(p),
+                                                 _p(i), _p(u), C.byref(params or default_params()),
+                                                 C.c_void_p(stream or 0))
+        self._err(rc, "dofs_segment_masked_device")
         self._last_hw = (H, W)
         return int(self.lib.dofs_batch_count(self.ctx)) - 1
 

@@ -168,6 +168,27 @@ int32_t dofs_segment_batch_device(dofs_ctx* ctx, const float* d_flow, int32_t B,
                                   const float persp[9], const float inv[9], const float inv_upper[27],
                                   const dofs_params* params, void* stream);
 int32_t dofs_batch_fetch(dofs_ctx* ctx, int32_t frame, dofs_result* out);
+
+/* Intra-frame sharding of the MST stage (BASELINE config 5: one large frame split
+ * into row bands across GPUs). The global MST (graph.cpp:519-531 accepts exactly it) is contained in
+ * the union of every row band's minimum spanning forest and the edges crossing band boundaries.
+ *
+ * dofs_band_msf_device: the minimum spanning forest of band rows [band_r0, band_r1) of an H x W
+ * frame (edges with both endpoints in the band), from device flow rows [row0, row0 + rows) that
+ * cover the band plus the blur halo (blur radius rows each side, clamped to the frame); writes
+ * d_mask[(y - band_r0) * W + x] = bit k set for each forest edge emitted by pixel (x, y) (k: 0 left,
+ * 1 up, 2 up-left, 3 down-left). Synchronous on `stream`.
+ *
+ * dofs_segment_masked_device: get_segmented_array on one device frame whose MST search is limited
+ * to the edges allowed by d_allowed (H x W bytes, same bit layout) — the OR of the band forests and
+ * every band-crossing edge gives results identical to dofs_segment_batch_device. Asynchronous, as a
+ * one-frame batch (read with dofs_batch_fetch / dofs_events / dofs_batch_records_*). */
+int32_t dofs_band_msf_device(dofs_ctx* ctx, const float* d_flow_rows, int32_t row0, int32_t rows, int32_t H,
+                             int32_t W, int32_t band_r0, int32_t band_r1, const dofs_params* params,
+                             uint8_t* d_mask, void* stream);
+int32_t dofs_segment_masked_device(dofs_ctx* ctx, const float* d_flow, int32_t H, int32_t W,
+                                   const uint8_t* d_allowed, const float persp[9], const float inv[9],
+                                   const float inv_upper[27], const dofs_params* params, void* stream);
 /* Device pointers to the last batch's fixed-capacity box records (B × capacity records, frame-major;
  * unused records have slot == -1) and per-frame counters (device int32, 64 per frame, the snapshot
  * count at index 4). Waits for the batch; valid until the next-but-one batch is issued. */
