@@ -458,6 +458,7 @@ int api_lift_batch(Context<Backend>* cx, int n, const float* dirs, const int* bo
         return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
     for (int i = 0; i < n; ++i)
         if (cls[i] < 0 || cls[i] > 2) return cx->fail(DOFS_ERR_INVALID_ARG, "cls must be 0..2");
+    cx->be.use_own();
     const size_t b_dirs = sizeof(F2) * n, b_box = 16 * (size_t)n, b_cls = 4 * (size_t)n,
                  b_out = sizeof(dofs_solution) * n;
     const size_t o_box = (b_dirs + 255) & ~(size_t)255;

@@ -47,7 +47,7 @@ int32_t dofs_segment(dofs_ctx* ctx, const float* flow_uv, int32_t H, int32_t W, 
                      const float persp[9], const float inv[9], const float inv_upper[27], const dofs_params* params,
                      dofs_result* out) {
     if (!ctx) return DOFS_ERR_INVALID_ARG;
-    ctx->be.set_stream(nullptr);
+    ctx->be.use_own();
     return dofs::api_segment(ctx, flow_uv, H, W, row_stride_bytes, persp, inv, inv_upper, params, out);
 }
 

@@ -655,9 +655,14 @@ struct HipBackend {
     }
     bool ok() const { return last == hipSuccess; }
     std::string error() const { return msg; }
+    // caller stream of the device-resident API: NULL is the default (null) stream, as in HIP
     void set_stream(void* s) {
         (void)hipSetDevice(device);
-        stream = s ? (hipStream_t)s : own;
+        stream = (hipStream_t)s;
+    }
+    void use_own() {  // host-buffer API: the context's private stream
+        (void)hipSetDevice(device);
+        stream = own;
     }
 
     void* cur_stream() const { return stream; }

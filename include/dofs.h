@@ -158,7 +158,7 @@ int32_t dofs_segment(dofs_ctx* ctx, const float* flow_uv, int32_t H, int32_t W, 
 int32_t dofs_events(dofs_ctx* ctx, int32_t frame, dofs_event* events, int64_t capacity);
 
 /* Frame-parallel batch on device-resident input: d_flow = B×H×W×2 float32 (device pointer),
- * stream = hipStream_t or NULL (the context's stream). Asynchronous: the batch is ordered after the
+ * stream = hipStream_t or NULL (the default stream, as in HIP). Asynchronous: the batch is ordered after the
  * work already queued on `stream`, and `stream` is ordered after the batch has consumed d_flow.
  * Batches alternate between two device workspaces and run as a two-stage pipeline (graph stage,
  * then replay + scoring stage), so consecutive calls overlap. Batch ids count calls from 0; the

@@ -59,6 +59,7 @@ struct HostBackend {
     bool ok() const { return true; }
     std::string error() const { return std::string(); }
     void set_stream(void*) {}
+    void use_own() {}
     void* cur_stream() const { return nullptr; }
     void use(void*) {}
     void* new_stream() { return nullptr; }
