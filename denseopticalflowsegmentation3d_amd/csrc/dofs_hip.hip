@@ -559,6 +559,87 @@ __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// K2 Borůvka rounds >= 1, per-component minimum edge (KBoruvkaMinW / KBoruvkaMinI with workgroup
+// pre-aggregation): one workgroup per 32x8 pixel tile, whose components are few (they are
+// contiguous regions), combines its lanes' candidate edges per component in an LDS hash table and
+// issues one global atomic per distinct component — instead of one per candidate edge endpoint.
+// pass 0: minimum weight bits; pass 1: minimum emission index among the edges of that weight.
+// ---------------------------------------------------------------------------------------------
+constexpr int kTileX = 32, kTileY = 8, kMinHT = 1024;
+__global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass) {
+    __shared__ int hk[kMinHT];
+    __shared__ unsigned long long hv[kMinHT];
+    __shared__ int any;
+    const Dims& d = w.d;
+    const int f = blockIdx.y;
+    if (pass == 0 ? (r > 0 && !w.C(f)[C_ACT + r - 1]) : !w.C(f)[C_ACT + r]) return;
+    const int tiles_x = (d.W + kTileX - 1) / kTileX;
+    const int tiles = tiles_x * ((d.H + kTileY - 1) / kTileY);
+    const int* comp = w.comp + f * d.N;
+    const F2* b = w.blur + f * d.N;
+    unsigned long long* bw = w.bw + f * d.N;
+    unsigned* bi = w.bi + f * d.N;
+    const int tid = threadIdx.x;
+    for (int x = tid; x < kMinHT; x += 256) {
+        hk[x] = -1;
+        hv[x] = ~0ull;
+    }
+    if (tid == 0) any = 0;
+    __syncthreads();
+    auto put = [&](int key, unsigned long long v) {
+        int slot = (int)(uf_prio(key) & (kMinHT - 1));
+        for (;;) {
+            int old = -1;
+            __hip_atomic_compare_exchange_strong(hk + slot, &old, key, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (old == -1 || old == key) break;
+            slot = (slot + 1) & (kMinHT - 1);
+        }
+        atomicMin(hv + slot, v);
+    };
+    for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
+        const int x = (t % tiles_x) * kTileX + (tid % kTileX), y = (t / tiles_x) * kTileY + tid / kTileX;
+        if (x < d.W && y < d.H) {
+            const int64_t p = (int64_t)y * d.W + x;
+            const int cp = comp[p];
+            bool mine = false;
+            for (int k = 0; k < 4; ++k) {
+                if (!edge_exists(d, x, y, k) || !edge_allowed(w, f, p, k)) continue;
+                const int64_t q = edge_end(d, p, k);
+                const int cq = comp[q];
+                if (cp == cq) continue;
+                const unsigned long long wb = dbits(edge_weight(b, p, q));
+                mine = true;
+                if (pass == 0) {
+                    put(cp, wb);
+                    put(cq, wb);
+                } else {
+                    const unsigned idx = (unsigned)(4 * p + k);
+                    if (wb == bw[cp]) put(cp, idx);
+                    if (wb == bw[cq]) put(cq, idx);
+                }
+            }
+            if (mine && pass == 0) any = 1;
+        }
+        __syncthreads();
+        for (int x = tid; x < kMinHT; x += 256) {
+            const int key = hk[x];
+            if (key < 0) continue;
+            const unsigned long long v = hv[x];
+            if (pass == 0) {
+                if (v < bw[key]) atomicMin(bw + key, v);
+            } else {
+                if ((unsigned)v < bi[key]) atomicMin(bi + key, (unsigned)v);
+            }
+            hk[x] = -1;
+            hv[x] = ~0ull;
+        }
+        __syncthreads();
+    }
+    if (pass == 0 && tid == 0 && any) w.C(f)[C_ACT + r] = 1;
+}
+
+// ---------------------------------------------------------------------------------------------
 // K3 global depths, compress + aggregate (KDncCompress with workgroup pre-aggregation): agent-scope
 // atomics execute at the memory side (MI355X_MICROARCH.md §Global float atomics; random 4-byte
 // atomics measured at ~27 G/s by tools/atomic_micro.hip), so the 1024 lanes of a workgroup first
@@ -854,6 +935,14 @@ struct HipBackend {
             hipLaunchKernelGGL(k_dnc_deep, dim3(nb, (unsigned)w.d.B), dim3(kDeepT), 0, stream, w);
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_dnc_deep launch");
+    }
+    void boruvka_min(const Ws& w, int r, int pass) {
+        const int64_t tiles = (int64_t)((w.d.W + kTileX - 1) / kTileX) * ((w.d.H + kTileY - 1) / kTileY);
+        const int64_t gx = std::min<int64_t>(tiles, std::max<int64_t>(1, grid_cap() / w.d.B));
+        timed(pass ? "k_boruvka_min_i" : "k_boruvka_min_w", [&] {
+            hipLaunchKernelGGL(k_boruvka_min, dim3((unsigned)gx, (unsigned)w.d.B), dim3(256), 0, stream, w, r, pass);
+        });
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_boruvka_min launch");
     }
     void dnc_compress(const Ws& w, int64_t S, int ep) {
         int64_t gx = (w.d.M + kAggT - 1) / kAggT;

@@ -184,8 +184,8 @@ struct Pipeline {
                 be.launch(B, N, KBoruvkaFirst{w});
             } else {
                 be.launch(B, N, KBoruvkaReset{w, r});
-                be.launch(B, N, KBoruvkaMinW{w, r});
-                be.launch(B, N, KBoruvkaMinI{w, r});
+                be.boruvka_min(w, r, 0);  // KBoruvkaMinW (HIP: workgroup-aggregated per tile)
+                be.boruvka_min(w, r, 1);  // KBoruvkaMinI
             }
             be.launch(B, N, KBoruvkaHook{w, r});
             be.launch(B, N, KBoruvkaCompress{w, r});

@@ -91,6 +91,12 @@ struct HostBackend {
             launch(w.d.B, M, KDncLRootRelabel{w, S, ep});
         }
     }
+    void boruvka_min(const Ws& w, int r, int pass) {
+        if (pass == 0)
+            launch(w.d.B, w.d.N, KBoruvkaMinW{w, r});
+        else
+            launch(w.d.B, w.d.N, KBoruvkaMinI{w, r});
+    }
     void dnc_compress(const Ws& w, int64_t S, int ep) { launch(w.d.B, w.d.M, KDncCompress{w, S, ep}); }
     void replay_long(const Ws& w, int r) { launch(w.d.B, w.d.N, KReplay{w, r, w.list_long, C_LONG}); }
     void profile(bool) {}
