@@ -976,18 +976,76 @@ struct HipBackend {
         }
         return t->p;
     }
-    // exclusive prefix sum of each frame's segment [f*n, (f+1)*n)
+    // exclusive prefix sum of each frame's segment [f*n, (f+1)*n): one scan over all frames, then
+    // each frame's running total at its start is subtracted (one launch sequence, not one per frame)
+    struct KFrameStart {
+        const int* out;
+        int* start;
+        int64_t n;
+        __device__ void operator()(int f, int64_t) const { start[f] = out[f * n]; }
+    };
+    struct KFrameRebase {
+        int* out;
+        const int* start;
+        int64_t n;
+        __device__ void operator()(int f, int64_t i) const { out[f * n + i] -= start[f]; }
+    };
     void scan_excl(const int* in, int* out, int64_t n, int nf) {
-        for (int f = 0; f < nf; ++f) {
-            size_t bytes = 0;
-            note(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in + f * n, out + f * n, (int)n, stream), "scan size");
-            void* t = temp(bytes);
-            note(hipcub::DeviceScan::ExclusiveSum(t, bytes, in + f * n, out + f * n, (int)n, stream), "scan");
+        const int64_t tot = n * nf;
+        size_t bytes = 0;
+        note(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, (int)tot, stream), "scan size");
+        const size_t sb = (bytes + 255) & ~(size_t)255;
+        char* t = (char*)temp(sb + sizeof(int) * (size_t)nf);
+        note(hipcub::DeviceScan::ExclusiveSum(t, bytes, in, out, (int)tot, stream), "scan");
+        if (nf > 1) {
+            int* start = (int*)(t + sb);
+            launch_on(stream, nf, 1, KFrameStart{out, start, n});
+            launch_on(stream, nf, n, KFrameRebase{out, start, n});
         }
     }
-    // stable LSD radix sort of (key, value) pairs by the 64-bit key, per frame
-    void sort_pairs(const unsigned long long* kin, unsigned long long* kout, const unsigned* vin, unsigned* vout,
-                    int64_t n, int nf) {
+    // stable LSD radix sort of (key, value) pairs by the 64-bit key, per frame. All frames at once
+    // when the frame id fits above the value bits: sort every pair by key, then stably by frame id
+    // (held in the value's top bits, with the key riding along as the value), then unpack.
+    struct KPackFrame {
+        unsigned* v;
+        int64_t n;
+        int ib;
+        __device__ void operator()(int f, int64_t i) const { v[f * n + i] |= (unsigned)f << ib; }
+    };
+    struct KUnpackFrame {
+        const unsigned* vin;
+        unsigned* vout;
+        const unsigned long long* kin;
+        unsigned long long* kout;
+        int64_t n;
+        unsigned mask;
+        __device__ void operator()(int f, int64_t i) const {
+            const int64_t o = f * n + i;
+            vout[o] = vin[o] & mask;
+            kout[o] = kin[o];
+        }
+    };
+    void sort_pairs(unsigned long long* kin, unsigned long long* kout, unsigned* vin, unsigned* vout, int64_t n,
+                    int nf, int value_bits) {
+        int fb = 0;
+        while ((1 << fb) < nf) ++fb;
+        const int64_t tot = n * nf;
+        if (nf > 1 && value_bits + fb <= 32 && tot < ((int64_t)1 << 31)) {
+            launch_on(stream, nf, n, KPackFrame{vin, n, value_bits});
+            size_t b1 = 0, b2 = 0;
+            note(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, kin, kout, vin, vout, (int)tot, 0, 64, stream),
+                 "sort size");
+            note(hipcub::DeviceRadixSort::SortPairs(nullptr, b2, vout, vin, kout, kin, (int)tot, value_bits,
+                                                    value_bits + fb, stream),
+                 "sort size");
+            void* t = temp(std::max(b1, b2));
+            note(hipcub::DeviceRadixSort::SortPairs(t, b1, kin, kout, vin, vout, (int)tot, 0, 64, stream), "sort");
+            note(hipcub::DeviceRadixSort::SortPairs(t, b2, vout, vin, kout, kin, (int)tot, value_bits,
+                                                    value_bits + fb, stream),
+                 "sort frames");
+            launch_on(stream, nf, n, KUnpackFrame{vin, vout, kin, kout, n, (1u << value_bits) - 1u});
+            return;
+        }
         for (int f = 0; f < nf; ++f) {
             size_t bytes = 0;
             note(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kin + f * n, kout + f * n, vin + f * n, vout + f * n,

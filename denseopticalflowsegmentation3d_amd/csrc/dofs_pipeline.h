@@ -244,7 +244,7 @@ struct Pipeline {
         be.launch(B, N, KMstCount{w});
         be.scan_excl(w.cnt, w.off, N, B);
         be.launch(B, N, KMstEmit{w});
-        be.sort_pairs(w.key_in, w.key_out, w.val_in, w.val_out, M, B);  // Kruskal order
+        be.sort_pairs(w.key_in, w.key_out, w.val_in, w.val_out, M, B, ceil_log2(4 * N));  // Kruskal order
 
         be.mark(3);
         // K3 Kruskal reconstruction tree

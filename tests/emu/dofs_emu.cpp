@@ -131,7 +131,7 @@ struct HostBackend {
         }
     }
     void sort_pairs(const unsigned long long* kin, unsigned long long* kout, const unsigned* vin, unsigned* vout,
-                    int64_t n, int nf) {
+                    int64_t n, int nf, int) {
         std::vector<int64_t> ix((size_t)n);
         for (int f = 0; f < nf; ++f) {
             std::iota(ix.begin(), ix.end(), 0);
