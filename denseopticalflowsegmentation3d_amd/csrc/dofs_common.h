@@ -6,6 +6,7 @@
 //   dofs_ld / dofs_st                relaxed agent-scope load / store of an int
 //   dofs_ld64 / dofs_st64            relaxed agent-scope load / store of a 64-bit word
 //   dofs_cas / dofs_exch             agent-scope compare-and-swap / exchange of an int
+//   dofs_cas64                       agent-scope compare-and-swap of a 64-bit word
 //   dofs_amin_u64 / dofs_amax_u64    agent-scope atomic min / max of a uint64
 //   dofs_amin / dofs_amax / dofs_aadd / dofs_aor   agent-scope atomics on int
 //   dofs_amin_u32                    agent-scope atomic min of a uint32

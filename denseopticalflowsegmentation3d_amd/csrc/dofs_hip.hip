@@ -26,6 +26,12 @@ __device__ inline int dofs_cas(int* p, int expected, int v) {
     return old;
 }
 __device__ inline int dofs_exch(int* p, int v) { return atomicExch(p, v); }
+__device__ inline unsigned long long dofs_cas64(unsigned long long* p, unsigned long long expected,
+                                                unsigned long long v) {
+    unsigned long long old = expected;
+    __hip_atomic_compare_exchange_strong(p, &old, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return old;
+}
 __device__ inline unsigned long long dofs_ld64(unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -665,7 +671,8 @@ __global__ __launch_bounds__(kAggT) void k_dnc_compress(Ws w, int64_t S, int ep)
         const int64_t i = base + tid;
         if (i < d.M && dnc_is_L(d, i, S)) {
             const int h = w.own[f * d.M + i];
-            const int r = walk_compress(w.P + lb, h, tag);
+            int szh;
+            const int r = walk_compress(w.P + lb, h, tag, &szh);
             int slot = (int)(uf_prio(r) & (kAggHT - 1));
             for (;;) {
                 int old = -1;
@@ -674,7 +681,7 @@ __global__ __launch_bounds__(kAggT) void k_dnc_compress(Ws w, int64_t S, int ep)
                 if (old == -1 || old == r) break;
                 slot = (slot + 1) & (kAggHT - 1);
             }
-            atomicAdd(hcs + slot, w.SZ[lb + h]);
+            atomicAdd(hcs + slot, szh);
             atomicMax(hmx + slot, mtag | (int)i);
         }
         __syncthreads();

@@ -76,7 +76,7 @@ struct Ws {
     int* own;
     unsigned char* hlB;  // merge i's light child is its end side B
     // label / node space (stride NL)
-    int* P;
+    unsigned long long* P;  // KRT label words (link | size << 32)
     int* CS;
     int* MX;
     int* SZ;
@@ -522,16 +522,19 @@ struct KLabelInit {  // untagged label words (epoch 0), zero counters, pixel siz
     DOFS_HD void operator()(int f, int64_t x) const {
         const Dims& d = w.d;
         const int64_t o = f * d.NL + x;
-        w.P[o] = 0;  // epoch 0: a root at every depth
         w.MX[o] = 0;
         w.CS[o] = 0;
+        int sz = 0;
         if (x < d.N) {
+            sz = 1;
             w.SZ[o] = 1;
         } else if (x == d.NL - 1) {  // KRT root = last merge: the whole frame (preorder 0, a path top)
-            w.SZ[o] = (int)d.N;
+            sz = (int)d.N;
+            w.SZ[o] = sz;
             w.J[o] = jump_pack(-1, 0);
             w.lite[o] = 1;
         }
+        w.P[o] = (unsigned long long)(unsigned)sz << 32;  // link word epoch 0: a root at every depth
     }
 };
 
@@ -570,50 +573,66 @@ DOFS_HDM inline int dnc_epoch(int64_t M, int64_t S) {  // 1 at the top depth, +1
     while (((int64_t)1 << s) < S) ++s;
     return top - s + 1;
 }
-DOFS_HD inline int dnc_find(int* P, int x, unsigned tag) {
+// Label word (64-bit): low half = link (tag | parent), high half = the label's component size, so
+// a find step reads a label's parent and size in one access (the union's size comparison and the
+// compress pass's size sum need no separate load).
+DOFS_HD inline unsigned lab_link(unsigned long long v) { return (unsigned)v; }
+DOFS_HD inline int lab_size(unsigned long long v) { return (int)(v >> 32); }
+DOFS_HD inline void lab_set_link(unsigned long long* P, int x, unsigned link) {  // low half only
+    dofs_st((int*)(P + x), (int)link);
+}
+DOFS_HD inline int dnc_find(unsigned long long* P, int x, unsigned tag, unsigned long long* word) {
     for (;;) {
-        const unsigned v = (unsigned)dofs_ld(P + x);
-        if ((v & ~kLabMask) != tag) return x;
-        const int p = (int)(v & kLabMask);
-        const unsigned vp = (unsigned)dofs_ld(P + p);
-        if ((vp & ~kLabMask) != tag) return p;
-        const int gp = (int)(vp & kLabMask);
-        dofs_st(P + x, (int)(tag | (unsigned)gp));  // path halving
+        const unsigned long long v = dofs_ld64(P + x);
+        if ((lab_link(v) & ~kLabMask) != tag) {
+            *word = v;
+            return x;
+        }
+        const int p = (int)(lab_link(v) & kLabMask);
+        const unsigned long long vp = dofs_ld64(P + p);
+        if ((lab_link(vp) & ~kLabMask) != tag) {
+            *word = vp;
+            return p;
+        }
+        const int gp = (int)(lab_link(vp) & kLabMask);
+        lab_set_link(P, x, tag | (unsigned)gp);  // path halving
         x = gp;
     }
 }
-DOFS_HD inline bool dnc_above(const int* SZ, int a, int b) {  // a is hooked below b
-    const int sa = SZ[a], sb = SZ[b];
-    if (sa != sb) return sa < sb;
-    return uf_above(a, b);
-}
-DOFS_HD inline int dnc_union(int* P, const int* SZ, int a, int b, unsigned tag) {
+DOFS_HD inline int dnc_union(unsigned long long* P, int a, int b, unsigned tag) {
     for (;;) {
-        a = dnc_find(P, a, tag);
-        b = dnc_find(P, b, tag);
+        unsigned long long va, vb;
+        a = dnc_find(P, a, tag, &va);
+        b = dnc_find(P, b, tag, &vb);
         if (a == b) return -1;  // unreachable: L-edges form a forest over the labels
-        if (!dnc_above(SZ, a, b)) {
-            int t = a;
+        const int sa = lab_size(va), sb = lab_size(vb);
+        if (!(sa != sb ? sa < sb : uf_above(a, b))) {  // a is hooked below b
+            const int t = a;
             a = b;
             b = t;
+            va = vb;
         }
-        const int va = dofs_ld(P + a);
-        if (((unsigned)va & ~kLabMask) == tag) continue;  // hooked meanwhile
-        if (dofs_cas(P + a, va, (int)(tag | (unsigned)b)) == va) return a;
+        const unsigned long long nv = (va & 0xFFFFFFFF00000000ull) | (tag | (unsigned)b);
+        if (dofs_cas64(P + a, va, nv) == va) return a;
     }
 }
-DOFS_HD inline int walk_compress(int* P, int x, unsigned tag) {  // no union runs concurrently
+DOFS_HD inline int walk_compress(unsigned long long* P, int x, unsigned tag, int* size_x) {
+    unsigned long long v = P[x];  // no union runs concurrently: plain loads
+    *size_x = lab_size(v);
     int r = x;
-    for (unsigned v = (unsigned)P[r]; (v & ~kLabMask) == tag; v = (unsigned)P[r]) r = (int)(v & kLabMask);
+    while ((lab_link(v) & ~kLabMask) == tag) {
+        r = (int)(lab_link(v) & kLabMask);
+        v = P[r];
+    }
     for (int y = x; y != r;) {
-        const int p = (int)((unsigned)P[y] & kLabMask);
-        if (p != r) P[y] = (int)(tag | (unsigned)r);
+        const int p = (int)(lab_link(P[y]) & kLabMask);
+        if (p != r) ((unsigned*)(P + y))[0] = tag | (unsigned)r;
         y = p;
     }
     return r;
 }
-DOFS_HD inline int dnc_root(const int* P, int x, unsigned tag) {  // after KDncCompress: one hop
-    const unsigned v = (unsigned)P[x];
+DOFS_HD inline int dnc_root(const unsigned long long* P, int x, unsigned tag) {  // after compress: one hop
+    const unsigned v = lab_link(P[x]);
     return (v & ~kLabMask) == tag ? (int)(v & kLabMask) : x;
 }
 
@@ -626,7 +645,7 @@ struct KDncUnion {
         if (!dnc_is_L(d, i, S)) return;
         const int64_t o = f * d.M + i;
         const int64_t lb = f * d.NL;
-        w.own[o] = dnc_union(w.P + lb, w.SZ + lb, w.lu[o], w.lv[o], (unsigned)ep << kLabBits);
+        w.own[o] = dnc_union(w.P + lb, w.lu[o], w.lv[o], (unsigned)ep << kLabBits);
     }
 };
 
@@ -640,11 +659,12 @@ struct KDncCompress {
         const int64_t o = f * d.M + i;
         const int64_t lb = f * d.NL;
         const int h = w.own[o];
-        const int r = walk_compress(w.P + lb, h, (unsigned)ep << kLabBits);
+        int szh;
+        const int r = walk_compress(w.P + lb, h, (unsigned)ep << kLabBits, &szh);
         // component size over the labels hooked in it (the root label is added by the L-root
         // edge) and the max L-edge rank (depth-tagged); wave-aggregated: a big component's root is
         // the key of most lanes at the top levels
-        dofs_agg_add(w.CS + lb, r, w.SZ[lb + h], true);
+        dofs_agg_add(w.CS + lb, r, szh, true);
         dofs_agg_max(w.MX + lb, r, (ep << kRankBits) | (int)i, true);
     }
 };
@@ -665,8 +685,10 @@ struct KDncLRootRelabel {
         if (dnc_is_L(d, i, S)) {
             const int r = dnc_root(w.P + lb, w.own[o], tag);
             if (w.MX[lb + r] != (mtag | (int)i)) return;
-            w.SZ[lb + d.N + i] = w.CS[lb + r] + w.SZ[lb + r];
+            const int sz = w.CS[lb + r] + lab_size(w.P[lb + r]);
             w.CS[lb + r] = 0;  // the only reader of this component's counter
+            ((int*)(w.P + lb + d.N + i))[1] = sz;  // the new label's size (high half of its word)
+            w.SZ[lb + d.N + i] = sz;
             return;
         }
         if (!dnc_is_R(i, S)) return;

@@ -120,7 +120,7 @@ struct Pipeline {
         w.lv = (int*)take(4 * B * M);
         w.own = (int*)take(4 * B * M);
         w.hlB = (unsigned char*)take(B * M);
-        w.P = (int*)take(4 * B * NL);
+        w.P = (unsigned long long*)take(8 * B * NL);
         w.CS = (int*)take(4 * B * NL);
         w.MX = (int*)take(4 * B * NL);
         w.SZ = (int*)take(4 * B * NL);

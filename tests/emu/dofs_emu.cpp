@@ -27,6 +27,11 @@ inline int dofs_exch(int* p, int v) {
     return o;
 }
 inline unsigned long long dofs_ld64(unsigned long long* p) { return *p; }
+inline unsigned long long dofs_cas64(unsigned long long* p, unsigned long long e, unsigned long long v) {
+    const unsigned long long o = *p;
+    if (o == e) *p = v;
+    return o;
+}
 inline void dofs_st64(unsigned long long* p, unsigned long long v) { *p = v; }
 inline void dofs_amin_u64(unsigned long long* p, unsigned long long v) { *p = std::min(*p, v); }
 inline void dofs_amax_u64(unsigned long long* p, unsigned long long v) { *p = std::max(*p, v); }
