@@ -189,6 +189,8 @@ struct Context {
     explicit Context(int device) : be(device), p0(be), p1(be), pband(be) {
         const char* e = getenv("DOFS_SERIAL");
         serial = e && e[0] == '1';
+        const char* sp = getenv("DOFS_SPLIT");
+        p0.preorder_in_b = p1.preorder_in_b = sp && sp[0] == '1';
         sA = be.new_stream();
         sB = be.new_stream();
         evIn = be.new_event();

@@ -54,6 +54,7 @@ struct Pipeline {
     Dims cap{};  // allocated shape
     int* pre = nullptr;
     int64_t snap_cap = 4096;
+    bool preorder_in_b = false;  // pipeline split: K4 at the end of phase A (default) or start of B
 
     explicit Pipeline(Backend& b) : be(b) { memset(&w, 0, sizeof(w)); }
     ~Pipeline() {
@@ -260,8 +261,15 @@ struct Pipeline {
         be.dnc_deep(w);
         be.launch(B, M, KDncParent{w});
 
+        if (!preorder_in_b) preorder();
+    }
+
+    // K4 heavy-first preorder (pointer jumping) and the replay's per-position inputs
+    void preorder() {
+        const Dims& d = w.d;
+        const int B = d.B;
+        const int64_t N = d.N, NL = d.NL;
         be.mark(4);
-        // K4 heavy-first preorder (pointer jumping)
         const int J = ceil_log2(NL) + 1;
         for (int t = 0; t < J; ++t) be.launch(B, NL, KJump{w.J, NL});
         pre = w.pre;
@@ -278,6 +286,7 @@ struct Pipeline {
         const int B = d.B;
         const int64_t N = d.N, M = d.M;
         if (M <= 0) return;
+        if (preorder_in_b) preorder();
         be.mark(5);
         // K5 bottom-up replay of Forest::merge along heavy paths
         const int RR = ceil_log2(N) + 2;
