@@ -672,7 +672,7 @@ __global__ __launch_bounds__(kAggT) void k_dnc_compress(Ws w, int64_t S, int ep)
         if (i < d.M && dnc_is_L(d, i, S)) {
             const int h = w.own[f * d.M + i];
             int szh;
-            const int r = walk_compress(w.lab(ep, f), h, tag, &szh);
+            const int r = walk_compress(w.P + lb, h, tag, &szh);
             int slot = (int)(uf_prio(r) & (kAggHT - 1));
             for (;;) {
                 int old = -1;

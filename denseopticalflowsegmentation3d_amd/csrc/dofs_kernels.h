@@ -76,8 +76,7 @@ struct Ws {
     int* own;
     unsigned char* hlB;  // merge i's light child is its end side B
     // label / node space (stride NL)
-    unsigned long long* P;   // KRT label words (link | size << 32) of the even depth epochs
-    unsigned long long* P2;  // ... of the odd ones
+    unsigned long long* P;  // KRT label words (link | size << 32)
     int* CS;
     int* MX;
     int* SZ;
@@ -124,7 +123,6 @@ struct Ws {
     double min_convexity[3];
 
     DOFS_HD int* C(int f) const { return ctr + (int64_t)f * kCounters; }
-    DOFS_HD unsigned long long* lab(int ep, int f) const { return ((ep & 1) ? P2 : P) + (int64_t)f * d.NL; }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -537,7 +535,6 @@ struct KLabelInit {  // untagged label words (epoch 0), zero counters, pixel siz
             w.lite[o] = 1;
         }
         w.P[o] = (unsigned long long)(unsigned)sz << 32;  // link word epoch 0: a root at every depth
-        w.P2[o] = (unsigned long long)(unsigned)sz << 32;
     }
 };
 
@@ -639,48 +636,16 @@ DOFS_HD inline int dnc_root(const unsigned long long* P, int x, unsigned tag) { 
     return (v & ~kLabMask) == tag ? (int)(v & kLabMask) : x;
 }
 
-// One global depth S (epoch ep) in one pass per merge, preceded by the completion of the previous
-// depth Sp (epoch ep - 1): an L edge of depth Sp whose rank is its component's max (an L-root)
-// records the component size; an R edge of depth Sp relabels its endpoints to the components' new
-// labels. Then, if it is an L edge of depth S, the merge unions its endpoint labels. Consecutive
-// depths use the two label-word arrays alternately, so depth Sp's words stay intact while depth S
-// links. (S = 0: only complete Sp; Sp = 0: the top depth.)
-struct KDncLevel {
+struct KDncUnion {
     Ws w;
     int64_t S;
     int ep;
-    int64_t Sp;
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
+        if (!dnc_is_L(d, i, S)) return;
         const int64_t o = f * d.M + i;
         const int64_t lb = f * d.NL;
-        if (Sp) {
-            const int epp = ep - 1;
-            unsigned long long* Pp = w.lab(epp, f);
-            const unsigned tag = (unsigned)epp << kLabBits;
-            const int mtag = epp << kRankBits;
-            if (dnc_is_L(d, i, Sp)) {
-                const int r = dnc_root(Pp, w.own[o], tag);
-                if (w.MX[lb + r] == (mtag | (int)i)) {
-                    const int sz = w.CS[lb + r] + lab_size(Pp[r]);
-                    w.CS[lb + r] = 0;  // the only reader of this component's counter
-                    const int64_t x = d.N + i;
-                    ((int*)(w.lab(0, f) + x))[1] = sz;  // the new label's size (high half of its words)
-                    ((int*)(w.lab(1, f) + x))[1] = sz;
-                    w.SZ[lb + x] = sz;
-                }
-            } else if (dnc_is_R(i, Sp)) {
-                for (int side = 0; side < 2; ++side) {
-                    int* lp = side ? (w.lv + o) : (w.lu + o);
-                    const int x = *lp;
-                    const int r = dnc_root(Pp, x, tag);
-                    // x is a label of this block's L forest <=> hooked at depth Sp or a touched root
-                    const int m = w.MX[lb + r];
-                    if (r != x || (m & ~kRankMask) == mtag) *lp = (int)(d.N + (m & kRankMask));
-                }
-            }
-        }
-        if (S && dnc_is_L(d, i, S)) w.own[o] = dnc_union(w.lab(ep, f), w.lu[o], w.lv[o], (unsigned)ep << kLabBits);
+        w.own[o] = dnc_union(w.P + lb, w.lu[o], w.lv[o], (unsigned)ep << kLabBits);
     }
 };
 
@@ -695,12 +660,46 @@ struct KDncCompress {
         const int64_t lb = f * d.NL;
         const int h = w.own[o];
         int szh;
-        const int r = walk_compress(w.lab(ep, f), h, (unsigned)ep << kLabBits, &szh);
+        const int r = walk_compress(w.P + lb, h, (unsigned)ep << kLabBits, &szh);
         // component size over the labels hooked in it (the root label is added by the L-root
         // edge) and the max L-edge rank (depth-tagged); wave-aggregated: a big component's root is
         // the key of most lanes at the top levels
         dofs_agg_add(w.CS + lb, r, szh, true);
         dofs_agg_max(w.MX + lb, r, (ep << kRankBits) | (int)i, true);
+    }
+};
+
+// After KDncCompress (roots final, hooked labels point at them): an L edge whose rank is its
+// component's max (an L-root) gets the component size; an R edge relabels its endpoints to the
+// components' new labels.
+struct KDncLRootRelabel {
+    Ws w;
+    int64_t S;
+    int ep;
+    DOFS_HD void operator()(int f, int64_t i) const {
+        const Dims& d = w.d;
+        const int64_t o = f * d.M + i;
+        const int64_t lb = f * d.NL;
+        const unsigned tag = (unsigned)ep << kLabBits;
+        const int mtag = ep << kRankBits;
+        if (dnc_is_L(d, i, S)) {
+            const int r = dnc_root(w.P + lb, w.own[o], tag);
+            if (w.MX[lb + r] != (mtag | (int)i)) return;
+            const int sz = w.CS[lb + r] + lab_size(w.P[lb + r]);
+            w.CS[lb + r] = 0;  // the only reader of this component's counter
+            ((int*)(w.P + lb + d.N + i))[1] = sz;  // the new label's size (high half of its word)
+            w.SZ[lb + d.N + i] = sz;
+            return;
+        }
+        if (!dnc_is_R(i, S)) return;
+        for (int side = 0; side < 2; ++side) {
+            int* lp = side ? (w.lv + o) : (w.lu + o);
+            const int x = *lp;
+            const int r = dnc_root(w.P + lb, x, tag);
+            // x is a label of this block's L forest <=> hooked this depth or a touched root
+            const int m = w.MX[lb + r];
+            if (r != x || (m & ~kRankMask) == mtag) *lp = (int)(d.N + (m & kRankMask));
+        }
     }
 };
 

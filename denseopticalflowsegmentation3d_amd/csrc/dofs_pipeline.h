@@ -122,7 +122,6 @@ struct Pipeline {
         w.own = (int*)take(4 * B * M);
         w.hlB = (unsigned char*)take(B * M);
         w.P = (unsigned long long*)take(8 * B * NL);
-        w.P2 = (unsigned long long*)take(8 * B * NL);
         w.CS = (int*)take(4 * B * NL);
         w.MX = (int*)take(4 * B * NL);
         w.SZ = (int*)take(4 * B * NL);
@@ -253,15 +252,12 @@ struct Pipeline {
         be.launch(B, M, KEdgeInit{w});
         be.launch(B, NL, KLabelInit{w});
         const int64_t deep = Backend::deep_block();  // levels with block size <= deep run per block
-        int64_t Sp = 0;
-        int ep = 0;
         for (int64_t S = (int64_t)1 << ceil_log2(M); S > deep; S >>= 1) {
-            ep = dnc_epoch(M, S);
-            be.launch(B, M, KDncLevel{w, S, ep, Sp});  // completes depth Sp, links depth S
-            be.dnc_compress(w, S, ep);                 // KDncCompress (HIP: workgroup-aggregated atomics)
-            Sp = S;
+            const int ep = dnc_epoch(M, S);
+            be.launch(B, M, KDncUnion{w, S, ep});
+            be.dnc_compress(w, S, ep);  // KDncCompress (HIP: workgroup-aggregated atomics)
+            be.launch(B, M, KDncLRootRelabel{w, S, ep});
         }
-        if (Sp) be.launch(B, M, KDncLevel{w, 0, ep + 1, Sp});  // completes the last global depth
         be.dnc_deep(w);
         be.launch(B, M, KDncParent{w});
 

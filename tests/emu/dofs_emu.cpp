@@ -82,22 +82,19 @@ struct HostBackend {
     void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height) {
         for (size_t r = 0; r < height; ++r) memcpy((char*)dst + r * dpitch, (const char*)src + r * spitch, width);
     }
-    // the HIP build runs the levels with block size <= 2048 per block in LDS (k_dnc_deep); the
+    // the HIP build runs the levels with block size <= 512 per block in LDS (k_dnc_deep); the
     // emulator runs them with the global kernels (same parents and sizes)
     static constexpr int64_t deep_block() { return 2048; }
     void dnc_deep(const Ws& w) {
         const int64_t M = w.d.M;
         int64_t top = 1;
         while (top < M) top <<= 1;
-        int64_t Sp = 0;
-        int ep = 0;
         for (int64_t S = std::min<int64_t>(deep_block(), top); S >= 2; S >>= 1) {
-            ep = dnc_epoch(M, S);
-            launch(w.d.B, M, KDncLevel{w, S, ep, Sp});
-            dnc_compress(w, S, ep);
-            Sp = S;
+            const int ep = dnc_epoch(M, S);
+            launch(w.d.B, M, KDncUnion{w, S, ep});
+            launch(w.d.B, M, KDncCompress{w, S, ep});
+            launch(w.d.B, M, KDncLRootRelabel{w, S, ep});
         }
-        if (Sp) launch(w.d.B, M, KDncLevel{w, 0, ep + 1, Sp});
     }
     void boruvka_min(const Ws& w, int r, int pass) {
         if (pass == 0)
