@@ -749,16 +749,21 @@ DOFS_HD inline int heavy_child(const Ws& w, int f, int y, int* light, int* light
 // 64-bit snapshot of J[a] satisfies it too, so x may jump over a with whatever value of J[a] it
 // reads, in any order: each round at least halves every remaining distance, as the synchronous
 // double-buffered form does, at half the traffic (one array, converged nodes idle).
-struct KJump {
+struct KJump {  // `hops` jumps per launch (each on the freshest ancestor word it reads)
     unsigned long long* J;
     int64_t NL;
+    int hops;
     DOFS_HD void operator()(int f, int64_t x) const {
         const int64_t o = f * NL + x;
-        const unsigned long long v = dofs_ld64(J + o);
-        const int a = jump_anc(v);
-        if (a < 0) return;
-        const unsigned long long u = dofs_ld64(J + f * NL + a);
-        dofs_st64(J + o, jump_pack(jump_anc(u), jump_sum(v) + jump_sum(u)));
+        unsigned long long v = dofs_ld64(J + o);
+        if (jump_anc(v) < 0) return;
+        for (int h = 0; h < hops; ++h) {
+            const int a = jump_anc(v);
+            if (a < 0) break;
+            const unsigned long long u = dofs_ld64(J + f * NL + a);
+            v = jump_pack(jump_anc(u), jump_sum(v) + jump_sum(u));
+        }
+        dofs_st64(J + o, v);
     }
 };
 

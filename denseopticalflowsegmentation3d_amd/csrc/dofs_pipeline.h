@@ -270,8 +270,11 @@ struct Pipeline {
         const int B = d.B;
         const int64_t N = d.N, NL = d.NL;
         be.mark(4);
-        const int J = ceil_log2(NL) + 1;
-        for (int t = 0; t < J; ++t) be.launch(B, NL, KJump{w.J, NL});
+        // two hops per launch at least triple every node's jump distance (the second hop may read
+        // an ancestor word not yet advanced in this launch), so 3^launches >= NL reaches every root
+        int launches = 0;
+        for (int64_t span = 1; span < NL; span *= 3) ++launches;
+        for (int t = 0; t < launches; ++t) be.launch(B, NL, KJump{w.J, NL, 2});
         pre = w.pre;
         be.launch(B, NL, KOrd{w});
         be.scan_excl(w.isleaf, w.lscan, NL, B);
