@@ -30,7 +30,7 @@ from denseopticalflowsegmentation3d_amd.frames import FrameParallel  # noqa: E40
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 GATHER_PER_FRAME = 64  # box records per frame in the gathered block
-DEEP_BLOCK = int(os.environ.get("DOFS_DEEP_S", "2048"))  # KRT depths with block size <= this run in LDS (k_dnc_deep), the rest globally
+DEEP_BLOCK = int(os.environ.get("DOFS_DEEP_S", "4096"))  # KRT depths with block size <= this run in LDS (k_dnc_deep), the rest globally
 
 # Algorithmic (compulsory) bytes per active lane of the probed kernels:
 # KDncCompress, per L edge of a depth: own label (4 B read), its parent (4 B read), its size

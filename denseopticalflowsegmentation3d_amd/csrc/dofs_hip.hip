@@ -437,14 +437,10 @@ struct DeepShared {
     int wsum[kDeepT / 64];
 };
 
-__global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
-    __shared__ DeepShared sh;
+// all depths of one block [s0, s0 + cnt) (cnt <= kDeepS) of frame f, in LDS
+__device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int cnt) {
     const Dims& d = w.d;
-    const int f = blockIdx.y;
-    const int64_t s0 = (int64_t)blockIdx.x * kDeepS;
-    if (s0 >= d.M) return;
     const int64_t lb = f * d.NL, eb = f * d.M;
-    const int cnt = (int)((d.M - s0) < kDeepS ? (d.M - s0) : kDeepS);
     const int tid = threadIdx.x;
     for (int x = tid; x < kDeepHT; x += kDeepT) sh.hkey[x] = -1;
     __syncthreads();
@@ -562,6 +558,127 @@ __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
         if (a >= kDeepK) w.lu[eb + s0 + t] = (int)(d.N + s0 + (a - kDeepK));
         if (b >= kDeepK) w.lv[eb + s0 + t] = (int)(d.N + s0 + (b - kDeepK));
     }
+}
+
+// The depth above the deep block size (block of kDeepTop = 2 kDeepS merges), in LDS too: only its
+// L half's labels (<= kDeepK) enter the union-find; an R-half endpoint is relabelled if the LDS hash
+// finds its label among them (a label touched by an L edge is in a component with an L edge).
+constexpr int kDeepTop = 2 * kDeepS;
+constexpr int kTopL = kDeepK + kDeepS;
+struct TopShared {
+    int hkey[kDeepHT];
+    short hval[kDeepHT];
+    int P[kTopL], SZ[kTopL], CS[kTopL], MX[kTopL];
+    short lu[kDeepS], lv[kDeepS], own[kDeepS];
+    int wsum[kDeepT / 64];
+};
+__device__ inline int top_lookup(const TopShared& sh, int g) {  // hash slot of label g, or -1
+    int h = (int)(uf_prio(g) % (unsigned)kDeepHT);
+    for (;;) {
+        const int k = sh.hkey[h];
+        if (k == g) return h;
+        if (k == -1) return -1;
+        h = h + 1 == kDeepHT ? 0 : h + 1;
+    }
+}
+__device__ void top_level(const Ws& w, TopShared& sh, int f, int64_t s0, int cnt) {
+    const Dims& d = w.d;
+    const int64_t lb = f * d.NL, eb = f * d.M;
+    const int tid = threadIdx.x;
+    const int nl = kDeepS;  // L half (the R half [kDeepS, cnt) is non-empty)
+    for (int x = tid; x < kDeepHT; x += kDeepT) sh.hkey[x] = -1;
+    __syncthreads();
+    for (int t = tid; t < nl; t += kDeepT) {
+        for (int side = 0; side < 2; ++side) {
+            const int g = side ? w.lv[eb + s0 + t] : w.lu[eb + s0 + t];
+            int h = (int)(uf_prio(g) % (unsigned)kDeepHT);
+            for (;;) {
+                int old = -1;
+                __hip_atomic_compare_exchange_strong(sh.hkey + h, &old, g, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (old == -1 || old == g) break;
+                h = h + 1 == kDeepHT ? 0 : h + 1;
+            }
+            (side ? sh.lv : sh.lu)[t] = (short)h;
+        }
+    }
+    __syncthreads();
+    {  // compact ids (as in deep_block)
+        constexpr int per = (kDeepHT + kDeepT - 1) / kDeepT;
+        const int beg = tid * per, end = min(beg + per, kDeepHT);
+        int c = 0;
+        for (int x = beg; x < end; ++x) c += sh.hkey[x] != -1;
+        int incl = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (__lane_id() >= o) incl += v;
+        }
+        if (__lane_id() == 63) sh.wsum[tid >> 6] = incl;
+        __syncthreads();
+        int base = incl - c;
+        for (int wv = 0; wv < (tid >> 6); ++wv) base += sh.wsum[wv];
+        for (int x = beg; x < end; ++x)
+            if (sh.hkey[x] != -1) {
+                sh.hval[x] = (short)base;
+                sh.SZ[base] = w.SZ[lb + sh.hkey[x]];
+                ++base;
+            }
+    }
+    for (int x = tid; x < kTopL; x += kDeepT) {
+        sh.P[x] = x;
+        sh.CS[x] = 0;
+        sh.MX[x] = -1;
+    }
+    __syncthreads();
+    for (int t = tid; t < nl; t += kDeepT) {
+        sh.lu[t] = sh.hval[sh.lu[t]];
+        sh.lv[t] = sh.hval[sh.lv[t]];
+    }
+    __syncthreads();
+    for (int t = tid; t < nl; t += kDeepT) sh.own[t] = (short)lds_union(sh.P, sh.SZ, sh.lu[t], sh.lv[t]);
+    __syncthreads();
+    for (int t = tid; t < nl; t += kDeepT) {  // compress + aggregate
+        const int h = sh.own[t];
+        int r = h;
+        for (int p = lds_ld(sh.P + r); p != r; p = lds_ld(sh.P + r)) r = p;
+        for (int y = h; y != r;) {
+            const int p = lds_ld(sh.P + y);
+            if (p != r) lds_st(sh.P + y, r);
+            y = p;
+        }
+        atomicAdd(sh.CS + r, sh.SZ[h]);
+        atomicMax(sh.MX + r, t);
+    }
+    __syncthreads();
+    for (int t = tid; t < nl; t += kDeepT) {  // L-roots: sizes of the new components
+        const int r = sh.P[sh.own[t]];
+        if (sh.MX[r] == t) w.SZ[lb + d.N + s0 + t] = sh.CS[r] + sh.SZ[r];
+    }
+    for (int t = nl + tid; t < cnt; t += kDeepT) {  // relabel the R half in global memory
+        for (int side = 0; side < 2; ++side) {
+            int* gp = side ? (w.lv + eb + s0 + t) : (w.lu + eb + s0 + t);
+            const int h = top_lookup(sh, *gp);
+            if (h < 0) continue;
+            const int x = sh.hval[h];
+            const int r = sh.P[x];
+            *gp = (int)(d.N + s0 + sh.MX[r]);
+        }
+    }
+    __syncthreads();
+}
+
+constexpr size_t kDeepSmem = sizeof(DeepShared) > sizeof(TopShared) ? sizeof(DeepShared) : sizeof(TopShared);
+__global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
+    __shared__ __attribute__((aligned(16))) char smem[kDeepSmem];
+    const Dims& d = w.d;
+    const int f = blockIdx.y;
+    const int64_t s0 = (int64_t)blockIdx.x * kDeepTop;
+    if (s0 >= d.M) return;
+    const int cnt = (int)((d.M - s0) < kDeepTop ? (d.M - s0) : kDeepTop);
+    if (cnt > kDeepS) top_level(w, *reinterpret_cast<TopShared*>(smem), f, s0, cnt);
+    deep_block(w, *reinterpret_cast<DeepShared*>(smem), f, s0, cnt < kDeepS ? cnt : kDeepS);
+    __syncthreads();
+    if (cnt > kDeepS) deep_block(w, *reinterpret_cast<DeepShared*>(smem), f, s0 + kDeepS, cnt - kDeepS);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -935,9 +1052,9 @@ struct HipBackend {
             timed(functor_name<F>(), fn);
     }
 
-    static constexpr int64_t deep_block() { return kDeepS; }
+    static constexpr int64_t deep_block() { return kDeepTop; }
     void dnc_deep(const Ws& w) {
-        const unsigned nb = (unsigned)((w.d.M + kDeepS - 1) / kDeepS);
+        const unsigned nb = (unsigned)((w.d.M + kDeepTop - 1) / kDeepTop);
         timed("k_dnc_deep", [&] {
             hipLaunchKernelGGL(k_dnc_deep, dim3(nb, (unsigned)w.d.B), dim3(kDeepT), 0, stream, w);
         });

@@ -84,7 +84,7 @@ struct HostBackend {
     }
     // the HIP build runs the levels with block size <= 512 per block in LDS (k_dnc_deep); the
     // emulator runs them with the global kernels (same parents and sizes)
-    static constexpr int64_t deep_block() { return 2048; }
+    static constexpr int64_t deep_block() { return 4096; }
     void dnc_deep(const Ws& w) {
         const int64_t M = w.d.M;
         int64_t top = 1;
