@@ -4,7 +4,7 @@ set -u
 export TMPDIR=/tmp
 O=gpurun_out/measure
 rm -rf $O; mkdir -p $O
-B=${B:-32}
+B=${B:-96}
 K=${K:-k_dnc_compress}
 BENCH="bench.py --steps 3 --warmup 1 --batch $B --cpu-frames 0 --no-stages"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python $BENCH > $O/pmc_fetch.log 2>&1; rc=$?; echo "pmc fetch rc=$rc"; if [ $rc -ne 0 ]; then tail -5 $O/pmc_fetch.log; exit $rc; fi
