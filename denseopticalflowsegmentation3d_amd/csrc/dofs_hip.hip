@@ -786,11 +786,13 @@ __global__ __launch_bounds__(kAggT) void k_dnc_compress(Ws w, int64_t S, int ep)
     __syncthreads();
     for (int64_t base = (int64_t)blockIdx.x * kAggT; base < d.M; base += (int64_t)gridDim.x * kAggT) {
         const int64_t i = base + tid;
-        if (i < d.M && dnc_is_L(d, i, S)) {
+        const bool act = i < d.M && dnc_is_L(d, i, S);
+        int r = -1, slot = 0;
+        if (act) {
             const int h = w.own[f * d.M + i];
             int szh;
-            const int r = walk_compress(w.P + lb, h, tag, &szh);
-            int slot = (int)(uf_prio(r) & (kAggHT - 1));
+            r = walk_compress(w.P + lb, h, tag, &szh);
+            slot = (int)(uf_prio(r) & (kAggHT - 1));
             for (;;) {
                 int old = -1;
                 __hip_atomic_compare_exchange_strong(hk + slot, &old, r, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
@@ -802,6 +804,9 @@ __global__ __launch_bounds__(kAggT) void k_dnc_compress(Ws w, int64_t S, int ep)
             atomicMax(hmx + slot, mtag | (int)i);
         }
         __syncthreads();
+        // only the workgroup's max rank of a component can be the component's max (its L-root):
+        // own = the root for those candidates, -1 for the others (KDncLRootRelabel skips them)
+        if (act) w.own[f * d.M + i] = hmx[slot] == (mtag | (int)i) ? r : -1;
         for (int x = tid; x < kAggHT; x += kAggT) {
             const int k = hk[x];
             if (k < 0) continue;

@@ -666,6 +666,7 @@ struct KDncCompress {
         // the key of most lanes at the top levels
         dofs_agg_add(w.CS + lb, r, szh, true);
         dofs_agg_max(w.MX + lb, r, (ep << kRankBits) | (int)i, true);
+        w.own[o] = r;  // L-root candidate: its component's root (the HIP pass keeps per-workgroup maxima only)
     }
 };
 
@@ -683,8 +684,8 @@ struct KDncLRootRelabel {
         const unsigned tag = (unsigned)ep << kLabBits;
         const int mtag = ep << kRankBits;
         if (dnc_is_L(d, i, S)) {
-            const int r = dnc_root(w.P + lb, w.own[o], tag);
-            if (w.MX[lb + r] != (mtag | (int)i)) return;
+            const int r = w.own[o];  // candidate's root (-1: not the max rank of its component)
+            if (r < 0 || w.MX[lb + r] != (mtag | (int)i)) return;
             const int sz = w.CS[lb + r] + lab_size(w.P[lb + r]);
             w.CS[lb + r] = 0;  // the only reader of this component's counter
             ((int*)(w.P + lb + d.N + i))[1] = sz;  // the new label's size (high half of its word)
