@@ -369,12 +369,12 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can
     }
 }
 
-__global__ __launch_bounds__(192) void k_replay_long(Ws w, int round) {
+__global__ __launch_bounds__(192) void k_replay_long(Ws w, int round, int wait) {
     __shared__ LongShared sh;
     const int f = blockIdx.y;
     const int n = w.C(f)[C_LONG];
     // waiting on another long path is safe only when every long path has its own workgroup
-    const bool can_wait = n <= (int)gridDim.x;
+    const bool can_wait = wait && n <= (int)gridDim.x;
     for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path(w, f, jj, round, can_wait, sh);
 }
 
@@ -1082,9 +1082,17 @@ struct HipBackend {
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_dnc_compress launch");
     }
+    static bool long_wait() {  // DOFS_LONG_WAIT=0: park instead of waiting on a running long path
+        static const bool on = [] {
+            const char* e = getenv("DOFS_LONG_WAIT");
+            return !(e && e[0] == '0');
+        }();
+        return on;
+    }
     void replay_long(const Ws& w, int round) {
         timed("k_replay_long", [&] {
-            hipLaunchKernelGGL(k_replay_long, dim3(256u, (unsigned)w.d.B), dim3(192), 0, stream, w, round);
+            hipLaunchKernelGGL(k_replay_long, dim3(256u, (unsigned)w.d.B), dim3(192), 0, stream, w, round,
+                               long_wait() ? 1 : 0);
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_replay_long launch");
     }
