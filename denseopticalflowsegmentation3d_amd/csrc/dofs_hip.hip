@@ -726,22 +726,26 @@ __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass) {
             const int64_t p = (int64_t)y * d.W + x;
             const int cp = comp[p];
             bool mine = false;
+            unsigned long long own_best = ~0ull;  // this pixel's candidates for its own component,
+            unsigned long long cpw = ~0ull;       // reduced in registers first
             for (int k = 0; k < 4; ++k) {
                 if (!edge_exists(d, x, y, k) || !edge_allowed(w, f, p, k)) continue;
                 const int64_t q = edge_end(d, p, k);
                 const int cq = comp[q];
                 if (cp == cq) continue;
                 const unsigned long long wb = dbits(edge_weight(b, p, q));
+                if (pass && !mine) cpw = bw[cp];
                 mine = true;
                 if (pass == 0) {
-                    put(cp, wb);
+                    own_best = wb < own_best ? wb : own_best;
                     put(cq, wb);
                 } else {
                     const unsigned idx = (unsigned)(4 * p + k);
-                    if (wb == bw[cp]) put(cp, idx);
+                    if (wb == cpw) own_best = idx < own_best ? idx : own_best;
                     if (wb == bw[cq]) put(cq, idx);
                 }
             }
+            if (own_best != ~0ull) put(cp, own_best);
             if (mine && pass == 0) any = 1;
         }
         __syncthreads();
