@@ -688,7 +688,7 @@ __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
 // issues one global atomic per distinct component — instead of one per candidate edge endpoint.
 // pass 0: minimum weight bits; pass 1: minimum emission index among the edges of that weight.
 // ---------------------------------------------------------------------------------------------
-constexpr int kTileX = 32, kTileY = 8, kMinHT = 1024;
+constexpr int kTileX = 32, kTileY = 8, kMinHT = 512;
 __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass) {
     __shared__ int hk[kMinHT];
     __shared__ unsigned long long hv[kMinHT];
@@ -722,12 +722,13 @@ __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass) {
     };
     for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
         const int x = (t % tiles_x) * kTileX + (tid % kTileX), y = (t / tiles_x) * kTileY + tid / kTileX;
-        if (x < d.W && y < d.H) {
+        int cp = -1;
+        unsigned long long own_best = ~0ull;  // this pixel's candidates for its own component,
+        if (x < d.W && y < d.H) {             // reduced in registers first
             const int64_t p = (int64_t)y * d.W + x;
-            const int cp = comp[p];
+            cp = comp[p];
             bool mine = false;
-            unsigned long long own_best = ~0ull;  // this pixel's candidates for its own component,
-            unsigned long long cpw = ~0ull;       // reduced in registers first
+            unsigned long long cpw = ~0ull;
             for (int k = 0; k < 4; ++k) {
                 if (!edge_exists(d, x, y, k) || !edge_allowed(w, f, p, k)) continue;
                 const int64_t q = edge_end(d, p, k);
@@ -745,8 +746,24 @@ __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass) {
                     if (wb == bw[cq]) put(cq, idx);
                 }
             }
-            if (own_best != ~0ull) put(cp, own_best);
             if (mine && pass == 0) any = 1;
+        }
+        {  // the lanes of a wave mostly share the component (a tile row of a contiguous region): one
+           // put for the first such lane's component, reduced across the lanes that share it
+            const bool has = own_best != ~0ull;
+            const unsigned long long on = __ballot(has);
+            if (on) {
+                const int leader = __ffsll((long long)on) - 1;
+                const int c0 = __shfl(cp, leader, 64);
+                const bool same = has && cp == c0;
+                unsigned long long m = same ? own_best : ~0ull;
+                for (int o = 32; o >= 1; o >>= 1) {
+                    const unsigned long long v = __shfl_xor(m, o, 64);
+                    m = v < m ? v : m;
+                }
+                if (__lane_id() == leader) put(c0, m);
+                if (has && !same) put(cp, own_best);
+            }
         }
         __syncthreads();
         for (int x = tid; x < kMinHT; x += 256) {
