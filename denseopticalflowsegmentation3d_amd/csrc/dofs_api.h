@@ -191,8 +191,10 @@ struct Context {
         serial = e && e[0] == '1';
         const char* sp = getenv("DOFS_SPLIT");
         p0.preorder_in_b = p1.preorder_in_b = sp && sp[0] == '1';
-        sA = be.new_stream();
-        sB = be.new_stream();
+        const char* pr = getenv("DOFS_PRIO");  // experiment: 1 = graph stage urgent, replay stage least
+        const bool prio = pr && pr[0] == '1';
+        sA = be.new_stream(prio ? 1 : 0);
+        sB = be.new_stream(prio ? -1 : 0);
         evIn = be.new_event();
         for (int s = 0; s < 2; ++s) {
             evA[s] = be.new_event();

@@ -898,9 +898,13 @@ struct HipBackend {
 
     void* cur_stream() const { return stream; }
     void use(void* s) { stream = (hipStream_t)s; }
-    void* new_stream() {
+    // prio: 0 = default, > 0 = the device's greatest (most urgent) priority, < 0 = its least
+    void* new_stream(int prio = 0) {
         hipStream_t st = nullptr;
-        note(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+        int least = 0, greatest = 0;
+        (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+        const int p = prio > 0 ? greatest : (prio < 0 ? least : 0);
+        note(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, p), "hipStreamCreate");
         if (st) streams.push_back(st);
         return st;
     }

@@ -67,7 +67,7 @@ struct HostBackend {
     void use_own() {}
     void* cur_stream() const { return nullptr; }
     void use(void*) {}
-    void* new_stream() { return nullptr; }
+    void* new_stream(int = 0) { return nullptr; }
     void* new_event() { return nullptr; }
     void record(void*, void*) {}
     void wait(void*, void*) {}
