@@ -754,7 +754,9 @@ struct KJump {  // `hops` jumps per launch (each on the freshest ancestor word i
     unsigned long long* J;
     int64_t NL;
     int hops;
-    DOFS_HD void operator()(int f, int64_t x) const {
+    int64_t first;  // node range [first, NL): the merge nodes (leaves are resolved by KJumpLeaf)
+    DOFS_HD void operator()(int f, int64_t k) const {
+        const int64_t x = first + k;
         const int64_t o = f * NL + x;
         unsigned long long v = dofs_ld64(J + o);
         if (jump_anc(v) < 0) return;
@@ -765,6 +767,18 @@ struct KJump {  // `hops` jumps per launch (each on the freshest ancestor word i
             v = jump_pack(jump_anc(u), jump_sum(v) + jump_sum(u));
         }
         dofs_st64(J + o, v);
+    }
+};
+
+struct KJumpLeaf {  // a pixel (leaf) hangs off a merge: one jump once the merges have converged
+    unsigned long long* J;
+    int64_t NL;
+    DOFS_HD void operator()(int f, int64_t x) const {
+        const int64_t o = f * NL + x;
+        const unsigned long long v = J[o];
+        const int a = jump_anc(v);
+        if (a < 0) return;
+        J[o] = jump_pack(-1, jump_sum(v) + jump_sum(J[f * NL + a]));
     }
 };
 

@@ -270,11 +270,13 @@ struct Pipeline {
         const int B = d.B;
         const int64_t N = d.N, NL = d.NL;
         be.mark(4);
-        // two hops per launch at least triple every node's jump distance (the second hop may read
-        // an ancestor word not yet advanced in this launch), so 3^launches >= NL reaches every root
+        // merge nodes only (the leaves hang off them): two hops per launch at least triple every
+        // node's jump distance (the second hop may read an ancestor word not yet advanced in this
+        // launch), so 3^launches >= M reaches every root
         int launches = 0;
-        for (int64_t span = 1; span < NL; span *= 3) ++launches;
-        for (int t = 0; t < launches; ++t) be.launch(B, NL, KJump{w.J, NL, 2});
+        for (int64_t span = 1; span < d.M; span *= 3) ++launches;
+        for (int t = 0; t < launches; ++t) be.launch(B, d.M, KJump{w.J, NL, 2, N});
+        be.launch(B, N, KJumpLeaf{w.J, NL});
         pre = w.pre;
         be.launch(B, NL, KOrd{w});
         be.scan_excl(w.isleaf, w.lscan, NL, B);
