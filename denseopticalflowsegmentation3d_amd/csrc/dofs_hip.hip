@@ -227,12 +227,10 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can
     int rank = 0, root = 0;
     B4 bb;
     bb.x0 = bb.y0 = bb.x1 = bb.y1 = 0;
-    if (wv == 0) m = w.Rmx[lb + q + 1];
-    if (wv == 1) m = w.Rmy[lb + q + 1];
-    if (wv == 2) {
-        rank = w.Rrank[lb + q + 1];
-        root = w.Rroot[lb + q + 1];
-        bb = w.Rbb[lb + q + 1];
+    {
+        float mx, my;
+        path_start(w, f, q + 1, &mx, &my, &rank, &root, &bb);
+        m = wv == 0 ? mx : my;
     }
     int cb = 0;
     ChainRec cr;

@@ -852,18 +852,9 @@ struct KPathInit {
                 else
                     w.list_short[f * d.N + dofs_aadd(w.C(f) + C_SHORT, 1)] = j;
             }
-        } else {
-            const F2 v = w.blur[f * d.N + x];
-            w.Rmx[lb + q] = v.x;
-            w.Rmy[lb + q] = v.y;
-            w.Rrank[lb + q] = 0;
-            w.Rroot[lb + q] = (int)x;
-            B4 b;
-            b.x0 = b.x1 = (int16_t)(x % d.W);
-            b.y0 = b.y1 = (int16_t)(x / d.W);
-            w.Rbb[lb + q] = b;
-            w.ready[lb + q] = -1;
         }
+        // leaves: nothing — a path's bottom leaf state is read from the flow by the replay itself
+        // (path_start), a light leaf's inputs are in its parent's StepIn
     }
 };
 
@@ -893,6 +884,29 @@ DOFS_HD inline void step_merge(RunState& s, float fs, float wbx, float wby, doub
 // child not completed in an earlier round is met (resumed next round) or the path top is done.
 // `list`/`count` select the short-path or the long-path list (the HIP build replays long paths
 // with the two-wave kernel of dofs_hip.hip instead; same state, same results).
+// State at preorder position qb (just below a path cursor): a leaf's singleton set (its blurred
+// flow, rank 0, root = itself, its pixel as bbox), or a merge's replay outputs.
+DOFS_HD inline void path_start(const Ws& w, int f, int64_t qb, float* mx, float* my, int* rank, int* root, B4* bb) {
+    const Dims& d = w.d;
+    const int64_t lb = f * d.NL;
+    const int x = w.ord[lb + qb];
+    if (x < d.N) {
+        const F2 v = w.blur[f * d.N + x];
+        *mx = v.x;
+        *my = v.y;
+        *rank = 0;
+        *root = x;
+        bb->x0 = bb->x1 = (int16_t)(x % d.W);
+        bb->y0 = bb->y1 = (int16_t)(x / d.W);
+        return;
+    }
+    *mx = w.Rmx[lb + qb];
+    *my = w.Rmy[lb + qb];
+    *rank = w.Rrank[lb + qb];
+    *root = w.Rroot[lb + qb];
+    *bb = w.Rbb[lb + qb];
+}
+
 struct KReplay {
     Ws w;
     int round;
@@ -907,11 +921,7 @@ struct KReplay {
         if (q < 0) return;
         const int64_t lb = f * d.NL;
         RunState s;
-        s.mx = w.Rmx[lb + q + 1];
-        s.my = w.Rmy[lb + q + 1];
-        s.rank = w.Rrank[lb + q + 1];
-        s.root = w.Rroot[lb + q + 1];
-        s.bb = w.Rbb[lb + q + 1];
+        path_start(w, f, q + 1, &s.mx, &s.my, &s.rank, &s.root, &s.bb);
         for (;;) {
             const StepIn in = w.In[lb + q];
             float wbx = in.wbx, wby = in.wby;
