@@ -810,11 +810,12 @@ constexpr int kPendLong = kIntMax - 1;  // long path, not complete
 constexpr int kParkBase = kIntMax - 2;  // long path stopped in round r: kParkBase - r
 
 
-struct KPathInit {
+struct KPathInit {  // one lane per merge node x = N + k
     Ws w;
     const int* pre;
-    DOFS_HD void operator()(int f, int64_t x) const {
+    DOFS_HD void operator()(int f, int64_t k) const {
         const Dims& d = w.d;
+        const int64_t x = d.N + k;
         const int64_t lb = f * d.NL;
         const int q = pre[lb + x];
         const bool top = w.lite[lb + x] != 0;

@@ -281,7 +281,7 @@ struct Pipeline {
         be.launch(B, NL, KOrd{w});
         be.scan_excl(w.isleaf, w.lscan, NL, B);
         be.launch(B, N, KLeafOrder{w, pre});
-        be.launch(B, NL, KPathInit{w, pre});
+        be.launch(B, d.M, KPathInit{w, pre});
     }
 
     // Phase B (replay + scoring): the order-dependent replay is latency-bound (a few waves per
