@@ -185,10 +185,13 @@ struct Context {
     void* evDone[2] = {nullptr, nullptr};
 
     bool serial = false;
+    bool skip_b = false;  // DOFS_SKIP_B=1: measurement only — graph stage alone, results invalid
 
     explicit Context(int device) : be(device), p0(be), p1(be), pband(be) {
         const char* e = getenv("DOFS_SERIAL");
         serial = e && e[0] == '1';
+        const char* sk = getenv("DOFS_SKIP_B");
+        skip_b = sk && sk[0] == '1';
         const char* sp = getenv("DOFS_SPLIT");
         p0.preorder_in_b = p1.preorder_in_b = sp && sp[0] == '1';
         const char* pr = getenv("DOFS_PRIO");  // experiment: 1 = graph stage urgent, replay stage least
@@ -279,7 +282,7 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     be.record(cx->evA[s], sa);
     if (sb != sa) be.wait(sb, cx->evA[s]);
     be.use(sb);
-    P.run_b();
+    if (!cx->skip_b) P.run_b();
     be.record(cx->evDone[s], sb);
     be.wait(caller, cx->evA[s]);
     be.use(caller);
