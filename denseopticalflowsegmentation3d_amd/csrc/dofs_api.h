@@ -192,6 +192,8 @@ struct Context {
         serial = e && e[0] == '1';
         const char* sk = getenv("DOFS_SKIP_B");
         skip_b = sk && sk[0] == '1';
+        const char* sm = getenv("DOFS_SKIPMASK");
+        p0.skip_mask = p1.skip_mask = sm ? atoi(sm) : 0;
         const char* sp = getenv("DOFS_SPLIT");
         p0.preorder_in_b = p1.preorder_in_b = sp && sp[0] == '1';
         const char* pr = getenv("DOFS_PRIO");  // experiment: 1 = graph stage urgent, replay stage least

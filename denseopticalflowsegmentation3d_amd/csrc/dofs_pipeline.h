@@ -54,7 +54,8 @@ struct Pipeline {
     Dims cap{};  // allocated shape
     int* pre = nullptr;
     int64_t snap_cap = 4096;
-    bool preorder_in_b = false;  // pipeline split: K4 at the end of phase A (default) or start of B
+    bool preorder_in_b = false;
+    int skip_mask = 0;  // measurement only (DOFS_SKIPMASK): 1 short replay, 2 long replay, 4 lift  // pipeline split: K4 at the end of phase A (default) or start of B
 
     explicit Pipeline(Backend& b) : be(b) { memset(&w, 0, sizeof(w)); }
     ~Pipeline() {
@@ -296,15 +297,15 @@ struct Pipeline {
         // K5 bottom-up replay of Forest::merge along heavy paths
         const int RR = ceil_log2(N) + 2;
         for (int r = 0; r < RR; ++r) {
-            be.launch(B, N, KReplay{w, r, w.list_short, C_SHORT});
-            be.replay_long(w, r);  // HIP: two-wave kernel; emulator: KReplay on the long list
+            if (!(skip_mask & 1)) be.launch(B, N, KReplay{w, r, w.list_short, C_SHORT});
+            if (!(skip_mask & 2)) be.replay_long(w, r);  // HIP: three-wave kernel; emulator: KReplay
         }
 
         be.mark(6);
         // K6 new_merge filters, lifting, per-slot arg-max, snapshots
         be.launch(B, M, KFilter{w, pre});
         be.launch(B, N, KSlotInit{w});
-        be.launch(B, M, KLift{w, pre});
+        if (!(skip_mask & 4)) be.launch(B, M, KLift{w, pre});
         be.launch(B, M, KSlotEvent{w, pre});
         be.launch(B, N, KSlotFlag{w});
         be.scan_excl(w.sflag, w.soff, N, B);
