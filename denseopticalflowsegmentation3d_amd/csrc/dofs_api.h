@@ -159,49 +159,55 @@ struct KSynth {
 
 template <class Backend>
 struct Context {
-    // Two workspaces used alternately by consecutive batches. A batch runs phase A (graph) on
-    // stream sA and phase B (replay + scoring) on stream sB, so batch k's phase B overlaps batch
-    // k+1's phase A. A workspace is reused only after its previous batch's phase B (evDone) ended.
+    // Workspaces used in turn by consecutive batches (kSlots, DOFS_SLOTS=2 for two). A batch runs
+    // phase A (graph) on stream sA and phase B (replay + scoring) on stream sB, so batch k's phase B
+    // overlaps the next batches' phase A. A workspace is reused only after its previous batch's
+    // phase B (evDone) ended: with three, the latency-bound phase B of batch k may run as long as
+    // the phase A of batches k+1 and k+2 together before it holds the graph stage up.
+    static constexpr int kSlots = 3;
     struct Meta {
         int B = 0, H = 0, W = 0;
         dofs_params prm;
     };
     Backend be;
-    Pipeline<Backend> p0, p1;
+    Pipeline<Backend> p0, p1, p2;
     Pipeline<Backend> pband;  // row-band minimum spanning forests (api_band_msf)
     std::string err;
     void* d_in = nullptr;
     size_t d_in_bytes = 0;
     void* d_scratch = nullptr;
     size_t d_scratch_bytes = 0;
-    int64_t nbatch = 0;  // batches issued; batch id b used workspace b & 1
+    int64_t nbatch = 0;  // batches issued; batch id b uses workspace b % nslots
+    int nslots = kSlots;
     int64_t snap_cap = 4096;
-    bool used[2] = {false, false};
-    Meta meta[2];
+    bool used[kSlots] = {false, false, false};
+    Meta meta[kSlots];
     void* sA = nullptr;
     void* sB = nullptr;
     void* evIn = nullptr;
-    void* evA[2] = {nullptr, nullptr};
-    void* evDone[2] = {nullptr, nullptr};
+    void* evA[kSlots] = {nullptr, nullptr, nullptr};
+    void* evDone[kSlots] = {nullptr, nullptr, nullptr};
 
     bool serial = false;
     bool skip_b = false;  // DOFS_SKIP_B=1: measurement only — graph stage alone, results invalid
 
-    explicit Context(int device) : be(device), p0(be), p1(be), pband(be) {
+    explicit Context(int device) : be(device), p0(be), p1(be), p2(be), pband(be) {
+        const char* ns = getenv("DOFS_SLOTS");
+        if (ns && (ns[0] == '2' || ns[0] == '3')) nslots = ns[0] - '0';
         const char* e = getenv("DOFS_SERIAL");
         serial = e && e[0] == '1';
         const char* sk = getenv("DOFS_SKIP_B");
         skip_b = sk && sk[0] == '1';
         const char* sm = getenv("DOFS_SKIPMASK");
-        p0.skip_mask = p1.skip_mask = sm ? atoi(sm) : 0;
+        p0.skip_mask = p1.skip_mask = p2.skip_mask = sm ? atoi(sm) : 0;
         const char* sp = getenv("DOFS_SPLIT");
-        p0.preorder_in_b = p1.preorder_in_b = sp && sp[0] == '1';
+        p0.preorder_in_b = p1.preorder_in_b = p2.preorder_in_b = sp && sp[0] == '1';
         const char* pr = getenv("DOFS_PRIO");  // experiment: 1 = graph stage urgent, replay stage least
         const bool prio = pr && pr[0] == '1';
         sA = be.new_stream(prio ? 1 : 0);
         sB = be.new_stream(prio ? -1 : 0);
         evIn = be.new_event();
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < kSlots; ++s) {
             evA[s] = be.new_event();
             evDone[s] = be.new_event();
         }
@@ -211,15 +217,16 @@ struct Context {
         if (d_in) be.free(d_in);
         if (d_scratch) be.free(d_scratch);
     }
-    Pipeline<Backend>& pipe(int slot) { return slot ? p1 : p0; }
+    Pipeline<Backend>& pipe(int slot) { return slot == 0 ? p0 : (slot == 1 ? p1 : p2); }
+    int slot_of(int64_t id) const { return (int)(id % nslots); }
     bool have_batch() const { return nbatch > 0; }
-    int last_slot() const { return (int)((nbatch - 1) & 1); }
-    // valid batch ids for result access: the last two issued
-    bool live(int64_t id) const { return id >= 0 && id < nbatch && id >= nbatch - 2; }
+    int last_slot() const { return slot_of(nbatch - 1); }
+    // valid batch ids for result access: the last nslots issued
+    bool live(int64_t id) const { return id >= 0 && id < nbatch && id >= nbatch - nslots; }
     // make the current stream wait for batch id's results
-    void join(int64_t id) { be.wait(be.cur_stream(), evDone[id & 1]); }
+    void join(int64_t id) { be.wait(be.cur_stream(), evDone[slot_of(id)]); }
     void drain() {
-        for (int s = 0; s < 2; ++s)
+        for (int s = 0; s < kSlots; ++s)
             if (used[s]) be.event_sync(evDone[s]);
     }
     void* scratch(size_t bytes) {
@@ -260,7 +267,7 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     Dims d = Pipeline<Backend>::dims_for(B, H, W, nbr8);
     Backend& be = cx->be;
     const int64_t id = cx->nbatch;
-    const int s = (int)(id & 1);
+    const int s = cx->slot_of(id);
     Pipeline<Backend>& P = cx->pipe(s);
     if (P.snap_cap != cx->snap_cap) {
         P.snap_cap = cx->snap_cap;
@@ -447,7 +454,7 @@ int api_segment(Context<Backend>* cx, const float* flow, int H, int W, size_t st
 template <class Backend>
 int api_records_copy(Context<Backend>* cx, int64_t batch, void* dst, int per_frame, void* stream) {
     if (!cx->live(batch) || !dst || per_frame < 0) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
-    const int slot = (int)(batch & 1);
+    const int slot = cx->slot_of(batch);
     const Ws& w = cx->pipe(slot).w;
     const int B = cx->meta[slot].B;
     const int k = per_frame < w.snap_cap ? per_frame : w.snap_cap;

@@ -160,9 +160,9 @@ int32_t dofs_events(dofs_ctx* ctx, int32_t frame, dofs_event* events, int64_t ca
 /* Frame-parallel batch on device-resident input: d_flow = B×H×W×2 float32 (device pointer),
  * stream = hipStream_t or NULL (the default stream, as in HIP). Asynchronous: the batch is ordered after the
  * work already queued on `stream`, and `stream` is ordered after the batch has consumed d_flow.
- * Batches alternate between two device workspaces and run as a two-stage pipeline (graph stage,
+ * Batches use three device workspaces in turn and run as a two-stage pipeline (graph stage,
  * then replay + scoring stage), so consecutive calls overlap. Batch ids count calls from 0; the
- * results of the last two batches stay readable (dofs_batch_records_copy_id); dofs_batch_fetch,
+ * results of the last three batches stay readable (dofs_batch_records_copy_id); dofs_batch_fetch,
  * dofs_events and dofs_batch_records_* read the last one. */
 int32_t dofs_segment_batch_device(dofs_ctx* ctx, const float* d_flow, int32_t B, int32_t H, int32_t W,
                                   const float persp[9], const float inv[9], const float inv_upper[27],
@@ -191,13 +191,13 @@ int32_t dofs_segment_masked_device(dofs_ctx* ctx, const float* d_flow, int32_t H
                                    const float inv_upper[27], const dofs_params* params, void* stream);
 /* Device pointers to the last batch's fixed-capacity box records (B × capacity records, frame-major;
  * unused records have slot == -1) and per-frame counters (device int32, 64 per frame, the snapshot
- * count at index 4). Waits for the batch; valid until the next-but-one batch is issued. */
+ * count at index 4). Waits for the batch; valid until three more batches are issued. */
 int32_t dofs_batch_records_device(dofs_ctx* ctx, void** d_records, void** d_counts, int32_t* capacity);
 
 /* Copy the batch's box records to a caller device buffer on `stream`: int32 counts[B] (snapshots per
  * frame), then B × per_frame dofs_box_record (the first per_frame records of each frame). */
 int32_t dofs_batch_records_copy(dofs_ctx* ctx, void* d_dst, int32_t per_frame, void* stream);
-/* Same for batch id `batch` (one of the last two issued); ordered after that batch on `stream`. */
+/* Same for batch id `batch` (one of the last three issued); ordered after that batch on `stream`. */
 int32_t dofs_batch_records_copy_id(dofs_ctx* ctx, int64_t batch, void* d_dst, int32_t per_frame,
                                    void* stream);
 /* Number of batches issued on ctx (the last batch id + 1). */

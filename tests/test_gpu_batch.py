@@ -68,8 +68,8 @@ def test_pipelined_batches_match_oracle(gpu, calib):
                 assert np.array_equal(g.labels, o.labels)
                 assert np.array_equal(g.snapshots["slot"], o.snapshots["slot"])
 
-    with pytest.raises(RuntimeError):  # only the last two batches stay readable
-        gpu.records_copy(blocks[0].data_ptr(), PER, stream=sh, batch=ids[0])
+    with pytest.raises(RuntimeError):  # only the last (three) batches stay readable
+        gpu.records_copy(blocks[0].data_ptr(), PER, stream=sh, batch=ids[0] - 1)
 
 
 def test_batch_records_device_pointers(gpu, calib):
