@@ -113,12 +113,14 @@ def main():
     runtime.synth_flow_device(flows.data_ptr(), B, H, W, seed0=rank * B, stream=sh)
     fp = FrameParallel(ctx, world, GATHER_PER_FRAME)
     pending = []
+    lag = ctx.batch_slots() - 1
 
-    # one step = submit a batch, then gather the records of the previous one (the context overlaps
-    # the previous batch's replay stage with this batch's graph stage); flush() gathers the last.
+    # one step = submit a batch, then gather the records of the batch submitted `lag` steps before
+    # (the context overlaps earlier batches' replay stages with this batch's graph stage); flush()
+    # gathers the rest.
     def step():
         pending.append(fp.submit(flows, persp, inv, up, params=prm, stream=sh))
-        if len(pending) > 1:
+        if len(pending) > lag:
             fp.collect(pending.pop(0), stream=sh)
 
     def flush():

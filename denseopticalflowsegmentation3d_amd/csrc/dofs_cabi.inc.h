@@ -108,6 +108,8 @@ int32_t dofs_batch_records_copy_id(dofs_ctx* ctx, int64_t batch, void* d_dst, in
 
 int64_t dofs_batch_count(dofs_ctx* ctx) { return ctx ? ctx->nbatch : -1; }
 
+int32_t dofs_batch_slots(dofs_ctx* ctx) { return ctx ? ctx->nslots : -1; }
+
 int32_t dofs_profile(dofs_ctx* ctx, int32_t enable) {
     if (!ctx) return DOFS_ERR_INVALID_ARG;
     ctx->be.profile(enable != 0);

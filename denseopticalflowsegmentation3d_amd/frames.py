@@ -63,7 +63,8 @@ class FrameParallel:
     fixed-size box records of every frame to every rank.
 
     `submit` only enqueues; `collect(batch)` gathers a batch's records. Collecting batch k after
-    submitting batch k+1 lets the context overlap k's replay stage with k+1's graph stage."""
+    submitting batch k + slots - 1 (ctx.batch_slots()) lets the context overlap k's replay stage
+    with the following batches' graph stages."""
 
     def __init__(self, ctx, world: int = 1, per_frame: int = 64):
         self.ctx, self.world, self.per_frame = ctx, world, per_frame
@@ -74,7 +75,8 @@ class FrameParallel:
         B, H, W = flows.shape[:3]
         bid = self.ctx.segment_batch_device(flows.data_ptr(), B, H, W, persp, inv, inv_upper, params=params,
                                             stream=stream)
-        self.frames = {k: v for k, v in self.frames.items() if k >= bid - 1}
+        keep = self.ctx.batch_slots() if hasattr(self.ctx, "batch_slots") else 2
+        self.frames = {k: v for k, v in self.frames.items() if k > bid - keep}
         self.frames[bid] = (B, flows.device)
         return bid
 

@@ -65,6 +65,8 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_batch_records_copy_id.restype = C.c_int32
     L.dofs_batch_count.argtypes = [C.c_void_p]
     L.dofs_batch_count.restype = C.c_int64
+    L.dofs_batch_slots.argtypes = [C.c_void_p]
+    L.dofs_batch_slots.restype = C.c_int32
     L.dofs_profile.argtypes = [C.c_void_p, C.c_int32]
     L.dofs_profile.restype = C.c_int32
     L.dofs_profile_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), _ip]
@@ -248,6 +250,10 @@ class Dofs:
 
     def batch_count(self) -> int:
         return int(self.lib.dofs_batch_count(self.ctx))
+
+    def batch_slots(self) -> int:
+        """Batches whose results stay readable (read batch k after submitting k + slots - 1)."""
+        return int(self.lib.dofs_batch_slots(self.ctx))
 
     STAGES = ("blur", "mst", "mst_sort", "krt", "preorder", "replay", "lift", "labels")
 

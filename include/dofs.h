@@ -202,6 +202,9 @@ int32_t dofs_batch_records_copy_id(dofs_ctx* ctx, int64_t batch, void* d_dst, in
                                    void* stream);
 /* Number of batches issued on ctx (the last batch id + 1). */
 int64_t dofs_batch_count(dofs_ctx* ctx);
+/* Number of batch workspaces (batches whose results stay readable; a caller that reads batch k's
+ * results after submitting batch k + slots - 1 keeps every stage of the pipeline busy). */
+int32_t dofs_batch_slots(dofs_ctx* ctx);
 
 /* Stage timing with device events (0 = off). Stages: 0 blur, 1 MST (Borůvka), 2 MST sort, 3 KRT,
  * 4 preorder, 5 replay, 6 lift + slots, 7 labels. dofs_profile_read returns the accumulated
