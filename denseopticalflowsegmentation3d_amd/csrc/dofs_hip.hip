@@ -1112,10 +1112,18 @@ struct HipBackend {
         }();
         return on;
     }
+    static int long_grid() {  // workgroups per frame of the long-path replay (DOFS_LONG_GRID)
+        static const int n = [] {
+            const char* e = getenv("DOFS_LONG_GRID");
+            const int v = e ? atoi(e) : 32;
+            return v > 0 ? v : 32;
+        }();
+        return n;
+    }
     void replay_long(const Ws& w, int round) {
         timed("k_replay_long", [&] {
-            hipLaunchKernelGGL(k_replay_long, dim3(256u, (unsigned)w.d.B), dim3(192), 0, stream, w, round,
-                               long_wait() ? 1 : 0);
+            hipLaunchKernelGGL(k_replay_long, dim3((unsigned)long_grid(), (unsigned)w.d.B), dim3(192), 0, stream, w,
+                               round, long_wait() ? 1 : 0);
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_replay_long launch");
     }
