@@ -1115,8 +1115,8 @@ struct HipBackend {
     static int long_grid() {  // workgroups per frame of the long-path replay (DOFS_LONG_GRID)
         static const int n = [] {
             const char* e = getenv("DOFS_LONG_GRID");
-            const int v = e ? atoi(e) : 32;
-            return v > 0 ? v : 32;
+            const int v = e ? atoi(e) : 256;
+            return v > 0 ? v : 256;
         }();
         return n;
     }
