@@ -143,19 +143,10 @@ struct SideRec {  // wave 2 step record (16 B)
 constexpr int kLongOk = 8;
 
 struct LongShared {
-    int go;  // blocked step: 1 = its light child completed (continue), 0 = park
+    ChainRec chain[2][2][64];  // [wave][buffer][step]
+    SideRec side[2][64];       // [buffer][step]
+    int go;                    // blocked step: 1 = its light child completed (continue), 0 = park
 };
-// lane k's value, broadcast (k wave-uniform): the step records stay in the registers of the lane
-// that resolved them — no LDS, so a long-path workgroup never keeps an LDS-heavy graph-stage kernel
-// (k_dnc_deep, 148 KB) off its CU
-__device__ inline int bcast_i(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
-__device__ inline float bcast_f(float v, int k) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k)); }
-__device__ inline double bcast_d(double v, int k) {
-    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, k);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), k);
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
 constexpr unsigned long long kSpinTicks = 5000000ull;  // 50 ms of s_memrealtime (100 MHz)
 
 // Resolve position p for wave `wv`. Returns the meta flags (kLongOk when the inputs are ready).
@@ -241,10 +232,15 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can
         path_start(w, f, q + 1, &mx, &my, &rank, &root, &bb);
         m = wv == 0 ? mx : my;
     }
+    int cb = 0;
     ChainRec cr;
     SideRec sr;
     B4 lbb;
     int meta = long_resolve(w, lb, q - lane, top, round, wv, &cr, &sr, &lbb);
+    if (wv < 2)
+        sh.chain[wv][cb][lane] = cr;
+    else
+        sh.side[cb][lane] = sr;
     for (;;) {
         ChainRec ncr;
         SideRec nsr;
@@ -257,21 +253,28 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can
         const int ft = tops ? __ffsll((long long)tops) - 1 : 64;
         const int finished = ft < fb;
         const int n = finished ? ft + 1 : fb;
-        // step k's record is broadcast from lane k; step k's output is kept in lane k
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS records have landed
+        __builtin_amdgcn_wave_barrier();
+        // the loops read their step records from LDS and keep step k's output in lane k (no LDS
+        // stores inside the loop, so the compiler can issue the record loads ahead of the chain)
         float om = 0.f;
         int orank = 0, oroot = 0;
         if (wv < 2) {
+            const ChainRec* c = sh.chain[wv][cb];
+#pragma unroll 8
             for (int k = 0; k < n; ++k) {
-                const float fs = bcast_f(cr.fs, k), wb = bcast_f(cr.wb, k);
-                const double r = bcast_d(cr.r, k);
-                m = (float)((double)(m * fs + wb) * r);
+                const ChainRec st = c[k];
+                m = (float)((double)(m * st.fs + st.wb) * st.r);
                 om = lane == k ? m : om;
             }
         } else {
+            const SideRec* c = sh.side[cb];
+#pragma unroll 8
             for (int k = 0; k < n; ++k) {
-                const int smeta = bcast_i(sr.meta, k), slrank = bcast_i(sr.lrank, k), slroot = bcast_i(sr.lroot, k);
-                const int nroot = (smeta & kStepB) ? (rank > slrank ? root : slroot) : (slrank > rank ? slroot : root);
-                rank = (rank == slrank) ? rank + 1 : (rank > slrank ? rank : slrank);
+                const SideRec st = c[k];
+                const int nroot = (st.meta & kStepB) ? (rank > st.lrank ? root : st.lroot)
+                                                     : (st.lrank > rank ? st.lroot : root);
+                rank = (rank == st.lrank) ? rank + 1 : (rank > st.lrank ? rank : st.lrank);
                 root = nroot;
                 orank = lane == k ? rank : orank;
                 oroot = lane == k ? root : oroot;
@@ -345,15 +348,22 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can
             }
             __syncthreads();
             if (!sh.go) return;
-            q = pb;  // re-resolve the chunk from the blocked step
+            q = pb;  // re-resolve the chunk from the blocked step into the buffer just consumed
             meta = long_resolve(w, lb, q - lane, top, round, wv, &cr, &sr, &lbb, pb);
+            if (wv < 2)
+                sh.chain[wv][cb][lane] = cr;
+            else
+                sh.side[cb][lane] = sr;
             continue;
         }
         q -= 64;
+        cb ^= 1;
         meta = nmeta;
         lbb = nlbb;
-        cr = ncr;
-        sr = nsr;
+        if (wv < 2)
+            sh.chain[wv][cb][lane] = ncr;
+        else
+            sh.side[cb][lane] = nsr;
     }
 }
 
