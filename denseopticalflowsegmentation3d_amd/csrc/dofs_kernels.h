@@ -120,6 +120,7 @@ struct Ws {
     int min_size;
     double score_threshold;
     double overlay_min_score;
+    int long_path;  // heavy paths at least this long run on the wave-cooperative replay
     double min_convexity[3];
 
     DOFS_HD int* C(int f) const { return ctr + (int64_t)f * kCounters; }
@@ -803,7 +804,7 @@ struct KLeafOrder {
     }
 };
 
-constexpr int kLongPath = 256;  // heavy paths at least this long go to the wave-cooperative replay
+constexpr int kLongPath = 256;  // default: heavy paths at least this long go to the wave-cooperative replay
 // ready[] at a heavy-path top: the round its path completed, or one of these pending states (all
 // compare >= any round, i.e. "not ready", for the short-path replay)
 constexpr int kPendLong = kIntMax - 1;  // long path, not complete
@@ -846,7 +847,7 @@ struct KPathInit {  // one lane per merge node x = N + k
                 const int j = dofs_aadd(w.C(f) + C_PATHS, 1);
                 w.cur[f * d.N + j] = qb - 1;
                 w.ptop[f * d.N + j] = q;
-                if (qb - q >= kLongPath) {
+                if (qb - q >= w.long_path) {
                     w.list_long[f * d.N + dofs_aadd(w.C(f) + C_LONG, 1)] = j;
                     w.ready[lb + q] = kPendLong;
                 }

@@ -55,7 +55,8 @@ struct Pipeline {
     int* pre = nullptr;
     int64_t snap_cap = 4096;
     bool preorder_in_b = false;
-    int skip_mask = 0;  // measurement only (DOFS_SKIPMASK): 1 short replay, 2 long replay, 4 lift  // pipeline split: K4 at the end of phase A (default) or start of B
+    int skip_mask = 0;
+    int long_path = kLongPath;  // measurement only (DOFS_SKIPMASK): 1 short replay, 2 long replay, 4 lift  // pipeline split: K4 at the end of phase A (default) or start of B
 
     explicit Pipeline(Backend& b) : be(b) { memset(&w, 0, sizeof(w)); }
     ~Pipeline() {
@@ -172,6 +173,7 @@ struct Pipeline {
         w.min_size = prm.min_size;
         w.score_threshold = prm.score_threshold;
         w.overlay_min_score = prm.overlay_min_score;
+        w.long_path = long_path;
     }
 
     // K2 Borůvka MST under (weight, emission index) of the frames in w (edges limited to w.allow)
