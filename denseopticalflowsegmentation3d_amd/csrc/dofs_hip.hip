@@ -161,9 +161,10 @@ __device__ inline int long_resolve(const Ws& w, int64_t lb, int p, int top, int 
     int lrank = 0, lroot = in.lb;
     if (in.meta & kStepDyn) {
         const int lq = in.lb;
-        // light child not complete in an earlier round (or, at `accept`, in this one: its producer's
-        // release was acquired by this workgroup)
-        if (w.ready[lb + lq] >= (p == accept ? round + 1 : round)) return meta;
+        // light child not complete in an earlier phase (or, at `accept`, in this one — the long-path
+        // pass 2*round+1 — whose producer's release this workgroup acquired)
+        const int phase = 2 * round + 1;
+        if (w.ready[lb + lq] >= (p == accept ? phase + 1 : phase)) return meta;
         if (wv < 2) {
             wb = (wv ? w.Rmy[lb + lq] : w.Rmx[lb + lq]) * (float)in.la;
         } else {
@@ -316,7 +317,7 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can
             if (threadIdx.x == 128) {
                 *curp = -1;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                __hip_atomic_store(w.ready + lb + top, round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(w.ready + lb + top, 2 * round + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             return;
         }
@@ -332,11 +333,11 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can
                 int rd;
                 for (;;) {
                     rd = __hip_atomic_load(w.ready + lb + lq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (!can_wait || rd <= round || rd == kIntMax || rd == kParkBase - round) break;
+                    if (!can_wait || rd <= 2 * round + 1 || rd == kIntMax || rd == kParkBase - round) break;
                     if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) break;
                     __builtin_amdgcn_s_sleep(8);
                 }
-                const int go = rd <= round;
+                const int go = rd <= 2 * round + 1;
                 sh.go = go;
                 if (go) {
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");

@@ -805,8 +805,8 @@ struct KLeafOrder {
 };
 
 constexpr int kLongPath = 256;  // default: heavy paths at least this long go to the wave-cooperative replay
-// ready[] at a heavy-path top: the round its path completed, or one of these pending states (all
-// compare >= any round, i.e. "not ready", for the short-path replay)
+// ready[] at a heavy-path top: the replay phase its path completed in, or one of these pending
+// states (all compare >= any phase, i.e. "not ready")
 constexpr int kPendLong = kIntMax - 1;  // long path, not complete
 constexpr int kParkBase = kIntMax - 2;  // long path stopped in round r: kParkBase - r
 
@@ -909,9 +909,11 @@ DOFS_HD inline void path_start(const Ws& w, int f, int64_t qb, float* mx, float*
     *bb = w.Rbb[lb + qb];
 }
 
+// Replay kernels run in phases: round r's short-path pass is phase 2r, its long-path pass 2r+1
+// (a path top's ready[] = the phase it completed in). A pass sees completions of earlier phases.
 struct KReplay {
     Ws w;
-    int round;
+    int phase;
     const int* list;
     int count;
     DOFS_HD void operator()(int f, int64_t jj) const {
@@ -931,7 +933,7 @@ struct KReplay {
             B4 lbb;
             if (in.meta & kStepDyn) {
                 const int lq = in.lb;
-                if (w.ready[lb + lq] >= round) {
+                if (w.ready[lb + lq] >= phase) {
                     *curp = q;
                     return;
                 }
@@ -951,7 +953,7 @@ struct KReplay {
             w.Rroot[lb + q] = s.root;
             w.Rbb[lb + q] = s.bb;
             if (in.meta & kStepTop) {
-                w.ready[lb + q] = round;
+                w.ready[lb + q] = phase;
                 *curp = -1;
                 return;
             }

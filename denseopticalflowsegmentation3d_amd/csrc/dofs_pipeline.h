@@ -299,7 +299,7 @@ struct Pipeline {
         // K5 bottom-up replay of Forest::merge along heavy paths
         const int RR = ceil_log2(N) + 2;
         for (int r = 0; r < RR; ++r) {
-            if (!(skip_mask & 1)) be.launch(B, N, KReplay{w, r, w.list_short, C_SHORT});
+            if (!(skip_mask & 1)) be.launch(B, N, KReplay{w, 2 * r, w.list_short, C_SHORT});
             if (!(skip_mask & 2)) be.replay_long(w, r);  // HIP: three-wave kernel; emulator: KReplay
         }
 

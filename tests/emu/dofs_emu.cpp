@@ -103,7 +103,7 @@ struct HostBackend {
             launch(w.d.B, w.d.N, KBoruvkaMinI{w, r});
     }
     void dnc_compress(const Ws& w, int64_t S, int ep) { launch(w.d.B, w.d.M, KDncCompress{w, S, ep}); }
-    void replay_long(const Ws& w, int r) { launch(w.d.B, w.d.N, KReplay{w, r, w.list_long, C_LONG}); }
+    void replay_long(const Ws& w, int r) { launch(w.d.B, w.d.N, KReplay{w, 2 * r + 1, w.list_long, C_LONG}); }
     void profile(bool) {}
     void probe(const char*) {}
     int64_t probe_read(double* ms) {
