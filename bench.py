@@ -161,7 +161,11 @@ def main():
     # roofline of the probed kernel: algorithmic bytes of its launches in the timed region over their
     # device-event time (events recorded on the stream the kernel runs on)
     roof = None
-    if probe_n:
+    probe = None
+    if probe_n and a.probe not in KERNEL_BYTES:  # a kernel without a roofline model: its time only
+        probe = {"kernel": a.probe, "ms_per_batch": round(probe_ms / a.steps, 3),
+                 "launches_per_batch": probe_n / a.steps}
+    elif probe_n:
         per_launch = [n * B * KERNEL_BYTES[a.probe] for n in dnc_L_edges(N - 1)] if a.probe in KERNEL_BYTES else []
         launches_per_batch = len(per_launch)
         assert launches_per_batch and probe_n == launches_per_batch * a.steps, (probe_n, launches_per_batch)
@@ -215,6 +219,8 @@ def main():
             "stages_ms_per_batch": stages,
             "cpu_baseline": None,
         }
+        if probe is not None:
+            out["probe"] = probe
         if world == 1 and a.cpu_frames > 0:
             out["cpu_baseline"] = cpu_baseline(H, W, a.cpu_frames)
         print(json.dumps(out), flush=True)

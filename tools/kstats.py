@@ -8,8 +8,8 @@ rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 25
 for r in rows[:n]:
-    m = re.search(r"dofs::(\w+)", r["Name"][10:]) or re.search(r"(\w+)", r["Name"])
-    nm = m.group(1)
+    m = re.search(r"^(?:void )?(?:dofs::)?([\w:]+?)[<(]", r["Name"]) or re.search(r"(\w+)", r["Name"])
+    nm = m.group(1).split("::")[-1]
     if nm == "k_generic":
         m2 = re.search(r"k_generic<dofs::(\w+)>", r["Name"])
         nm = m2.group(1) if m2 else nm
