@@ -10,8 +10,9 @@
 //   dofs_amin_u64 / dofs_amax_u64    agent-scope atomic min / max of a uint64
 //   dofs_amin / dofs_amax / dofs_aadd / dofs_aor   agent-scope atomics on int
 //   dofs_amin_u32                    agent-scope atomic min of a uint32
-//   dofs_agg_size_bbox / dofs_agg_max / dofs_agg_min   keyed atomic updates that a backend may
-//                                    aggregate across the lanes of a wave sharing one key
+//   dofs_agg_size_bbox / dofs_agg_max / dofs_agg_min / dofs_agg_max_u64   keyed atomic updates
+//                                    that a backend may aggregate across the lanes of a wave sharing
+//                                    one key (called by every lane of the launch, `act` = participates)
 // dofs_hip.hip maps them to HIP atomics on gfx950; the test-only host emulator maps them to plain
 // sequential operations.
 #pragma once

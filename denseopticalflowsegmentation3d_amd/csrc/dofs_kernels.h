@@ -1018,23 +1018,27 @@ struct KLift {
     const int* pre;
     DOFS_HD void operator()(int f, int64_t j) const {
         const Dims& d = w.d;
-        if (j >= w.C(f)[C_CAND]) return;
-        const int i = w.cand[f * d.M + j];
-        const NodeVal v = node_val(w, pre, f, d.N + i);
-        double* cs = w.cscore + f * d.M + j;
-        *cs = -1.0;
-        const double rect_area = (double)((v.x1 - v.x0 + 1) * (v.y1 - v.y0 + 1));
-        const double convexity = v.size / rect_area;
-        int cls;
-        const double score = event_score(w, v, &cls, nullptr);
-        if (score == -1) return;
-        dofs_aadd(w.C(f) + C_SCORED, 1);
-        const double minc = w.min_convexity[cls];
-        if (convexity < minc) return;
-        if (!(score > w.score_threshold)) return;
-        dofs_aadd(w.C(f) + C_QUAL, 1);
-        *cs = score;
-        dofs_amax_u64(w.sbest + f * d.N + v.root, dbits(score));
+        // no early return: every lane reaches the keyed max, which aggregates a wave's lanes of one
+        // slot (a frame's largest cluster root takes most of its candidate events)
+        bool qual = false;
+        int root = 0;
+        double score = -1.0;
+        if (j < w.C(f)[C_CAND]) {
+            const int i = w.cand[f * d.M + j];
+            const NodeVal v = node_val(w, pre, f, d.N + i);
+            const double rect_area = (double)((v.x1 - v.x0 + 1) * (v.y1 - v.y0 + 1));
+            const double convexity = v.size / rect_area;
+            int cls;
+            score = event_score(w, v, &cls, nullptr);
+            root = v.root;
+            if (score != -1) {
+                dofs_aadd(w.C(f) + C_SCORED, 1);
+                qual = !(convexity < w.min_convexity[cls]) && score > w.score_threshold;
+                if (qual) dofs_aadd(w.C(f) + C_QUAL, 1);
+            }
+            w.cscore[f * d.M + j] = qual ? score : -1.0;
+        }
+        dofs_agg_max_u64(w.sbest + f * d.N, root, dbits(score), qual);
     }
 };
 

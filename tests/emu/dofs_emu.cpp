@@ -50,6 +50,9 @@ inline void dofs_agg_add(int* base, int key, int val, bool act) {
 inline void dofs_agg_max(int* base, int key, int val, bool act) {
     if (act) base[key] = std::max(base[key], val);
 }
+inline void dofs_agg_max_u64(unsigned long long* base, int key, unsigned long long val, bool act) {
+    if (act) base[key] = std::max(base[key], val);
+}
 inline void dofs_agg_min(int* base, int key, int val, bool act) {
     if (act) base[key] = std::min(base[key], val);
 }
