@@ -102,10 +102,12 @@ __device__ inline void agg_minmax(int* base, int key, int val, bool act) {
     }
 }
 __device__ inline void dofs_agg_max(int* base, int key, int val, bool act) { agg_minmax<true>(base, key, val, act); }
-// Keyed u64 max where a few keys are very hot (the slot arg-max of KLift: one cluster root takes
-// most candidate events of a frame). Up to four distinct keys of the wave are reduced in registers
-// and written with one atomic each; an atomic is skipped when the stored maximum is not lower.
-__device__ inline void dofs_agg_max_u64(unsigned long long* base, int key, unsigned long long val, bool act) {
+// Keyed u64 max / min where a few keys are very hot (the slot arg-max of KLift: one cluster root
+// takes most candidate events of a frame). Up to four distinct keys of the wave are reduced in registers and written with
+// one atomic each; an atomic is skipped when the stored value is already at least as good.
+template <bool kMax>
+__device__ inline void agg_u64(unsigned long long* base, int key, unsigned long long val, bool act) {
+    auto better = [](unsigned long long a, unsigned long long c) { return kMax ? a > c : a < c; };
     const unsigned long long present = __ballot(1);
     if (present == ~0ull) {
         unsigned long long on = __ballot(act);
@@ -113,11 +115,13 @@ __device__ inline void dofs_agg_max_u64(unsigned long long* base, int key, unsig
             const int leader = __ffsll((long long)on) - 1;
             const int k0 = __shfl(key, leader, 64);
             const bool same = act && key == k0;
-            const unsigned long long v =
-                wave_reduce(same ? val : 0ull, [](unsigned long long a, unsigned long long c) { return a > c ? a : c; });
+            const unsigned long long v = wave_reduce(same ? val : (kMax ? 0ull : ~0ull),
+                                                     [&](unsigned long long a, unsigned long long c) {
+                                                         return better(a, c) ? a : c;
+                                                     });
             if (wave_lane() == leader) {
                 const unsigned long long cur = __hip_atomic_load(base + k0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (cur < v) atomicMax(base + k0, v);
+                if (better(v, cur)) kMax ? atomicMax(base + k0, v) : atomicMin(base + k0, v);
             }
             act = act && !same;
             on = __ballot(act);
@@ -125,11 +129,12 @@ __device__ inline void dofs_agg_max_u64(unsigned long long* base, int key, unsig
     }
     if (act) {
         const unsigned long long cur = __hip_atomic_load(base + key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur < val) atomicMax(base + key, val);
+        if (better(val, cur)) kMax ? atomicMax(base + key, val) : atomicMin(base + key, val);
     }
 }
-
-__device__ inline void dofs_agg_min(int* base, int key, int val, bool act) { agg_minmax<false>(base, key, val, act); }
+__device__ inline void dofs_agg_max_u64(unsigned long long* base, int key, unsigned long long val, bool act) {
+    agg_u64<true>(base, key, val, act);
+}
 
 #include "dofs_kernels.h"
 
