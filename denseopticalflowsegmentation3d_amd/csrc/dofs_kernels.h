@@ -811,16 +811,20 @@ constexpr int kPendLong = kIntMax - 1;  // long path, not complete
 constexpr int kParkBase = kIntMax - 2;  // long path stopped in round r: kParkBase - r
 
 
-struct KPathInit {  // one lane per merge node x = N + k
+struct KPathInit {  // one lane per merge node x = N + k; path ids and lists through the list taker
     Ws w;
     const int* pre;
-    DOFS_HD void operator()(int f, int64_t k) const {
+    static constexpr bool kBlockTake = true;
+    template <class T>
+    DOFS_HD void operator()(int f, int64_t k, bool valid, T& t) const {
         const Dims& d = w.d;
         const int64_t x = d.N + k;
         const int64_t lb = f * d.NL;
-        const int q = pre[lb + x];
-        const bool top = w.lite[lb + x] != 0;
-        if (x >= d.N) {
+        bool top = false, islong = false;
+        int q = 0, qb = 0;
+        if (valid) {
+            q = pre[lb + x];
+            top = w.lite[lb + x] != 0;
             int lt, lB;
             const int h = heavy_child(w, f, (int)x, &lt, &lB);
             StepIn in;
@@ -840,20 +844,23 @@ struct KPathInit {  // one lane per merge node x = N + k
                 in.lb = pre[lb + lt];
             }
             w.In[lb + q] = in;
-            w.ready[lb + q] = kIntMax;
             if (top) {  // heavy path [q, bottom): its bottom leaf is the first leaf after q in preorder
                 const int leaf = w.leaf_order[f * d.N + w.lscan[lb + q]];
-                const int qb = pre[lb + leaf];
-                const int j = dofs_aadd(w.C(f) + C_PATHS, 1);
-                w.cur[f * d.N + j] = qb - 1;
-                w.ptop[f * d.N + j] = q;
-                if (qb - q >= w.long_path) {
-                    w.list_long[f * d.N + dofs_aadd(w.C(f) + C_LONG, 1)] = j;
-                    w.ready[lb + q] = kPendLong;
-                }
-                else
-                    w.list_short[f * d.N + dofs_aadd(w.C(f) + C_SHORT, 1)] = j;
+                qb = pre[lb + leaf];
+                islong = qb - q >= w.long_path;
             }
+            w.ready[lb + q] = islong ? kPendLong : kIntMax;
+        }
+        const int j = t.take(w.C(f) + C_PATHS, top);
+        const int jl = t.take(w.C(f) + C_LONG, islong);
+        const int js = t.take(w.C(f) + C_SHORT, top && !islong);
+        if (top) {
+            w.cur[f * d.N + j] = qb - 1;
+            w.ptop[f * d.N + j] = q;
+            if (islong)
+                w.list_long[f * d.N + jl] = j;
+            else
+                w.list_short[f * d.N + js] = j;
         }
         // leaves: nothing — a path's bottom leaf state is read from the flow by the replay itself
         // (path_start), a light leaf's inputs are in its parent's StepIn
@@ -992,19 +999,21 @@ DOFS_HD inline double vec_norm(float x, float y) {  // cv::norm(Vec2f)
     return sqrt(s);
 }
 
-struct KFilter {
+struct KFilter {  // appends candidates through the backend's list taker (called by every lane)
     Ws w;
     const int* pre;
-    DOFS_HD void operator()(int f, int64_t i) const {
+    static constexpr bool kBlockTake = true;
+    template <class T>
+    DOFS_HD void operator()(int f, int64_t i, bool valid, T& t) const {
         const Dims& d = w.d;
-        const NodeVal v = node_val(w, pre, f, d.N + i);
-        if (v.size < w.min_size) return;
-        const int y = v.root / d.W;
-        if (y < d.H / 10) return;
-        const double move = vec_norm(v.mx, v.my);
-        if (move < 3 * (y + 1) / (double)d.H) return;
-        const int k = dofs_aadd(w.C(f) + C_CAND, 1);
-        w.cand[f * d.M + k] = (int)i;
+        bool c = false;
+        if (valid) {
+            const NodeVal v = node_val(w, pre, f, d.N + i);
+            const int y = v.root / d.W;
+            c = v.size >= w.min_size && y >= d.H / 10 && !(vec_norm(v.mx, v.my) < 3 * (y + 1) / (double)d.H);
+        }
+        const int k = t.take(w.C(f) + C_CAND, c);
+        if (c) w.cand[f * d.M + k] = (int)i;
     }
 };
 
@@ -1016,14 +1025,16 @@ DOFS_HD inline double event_score(const Ws& w, const NodeVal& v, int* cls, dofs_
 struct KLift {
     Ws w;
     const int* pre;
-    DOFS_HD void operator()(int f, int64_t j) const {
+    static constexpr bool kBlockTake = true;
+    template <class T>
+    DOFS_HD void operator()(int f, int64_t j, bool valid, T& t) const {
         const Dims& d = w.d;
-        // no early return: every lane reaches the keyed max, which aggregates a wave's lanes of one
-        // slot (a frame's largest cluster root takes most of its candidate events)
-        bool qual = false;
+        // no early return: every lane reaches the counters and the keyed max, which aggregates a
+        // wave's lanes of one slot (a frame's largest cluster root takes most of its candidate events)
+        bool scored = false, qual = false;
         int root = 0;
         double score = -1.0;
-        if (j < w.C(f)[C_CAND]) {
+        if (valid && j < w.C(f)[C_CAND]) {
             const int i = w.cand[f * d.M + j];
             const NodeVal v = node_val(w, pre, f, d.N + i);
             const double rect_area = (double)((v.x1 - v.x0 + 1) * (v.y1 - v.y0 + 1));
@@ -1031,13 +1042,12 @@ struct KLift {
             int cls;
             score = event_score(w, v, &cls, nullptr);
             root = v.root;
-            if (score != -1) {
-                dofs_aadd(w.C(f) + C_SCORED, 1);
-                qual = !(convexity < w.min_convexity[cls]) && score > w.score_threshold;
-                if (qual) dofs_aadd(w.C(f) + C_QUAL, 1);
-            }
+            scored = score != -1;
+            qual = scored && !(convexity < w.min_convexity[cls]) && score > w.score_threshold;
             w.cscore[f * d.M + j] = qual ? score : -1.0;
         }
+        t.take(w.C(f) + C_SCORED, scored);
+        t.take(w.C(f) + C_QUAL, qual);
         dofs_agg_max_u64(w.sbest + f * d.N, root, dbits(score), qual);
     }
 };

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <numeric>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #define DOFS_HD
@@ -118,10 +119,23 @@ struct HostBackend {
         for (int s = 0; s < 8; ++s) ms[s] = 0;
         return 0;
     }
+    struct HostTaker {  // list append: a plain counter
+        int take(int* ctr, bool want) { return want ? (*ctr)++ : -1; }
+    };
+    template <class F, class = void>
+    struct takes : std::false_type {};
+    template <class F>
+    struct takes<F, std::void_t<decltype(F::kBlockTake)>> : std::true_type {};
     template <class F>
     static int launch_static(void*, int nf, int64_t n, const F& f) {
+        HostTaker t;
         for (int fr = 0; fr < nf; ++fr)
-            for (int64_t i = 0; i < n; ++i) f(fr, i);
+            for (int64_t i = 0; i < n; ++i) {
+                if constexpr (takes<F>::value)
+                    f(fr, i, true, t);
+                else
+                    f(fr, i);
+            }
         return DOFS_OK;
     }
     template <class F>
