@@ -29,6 +29,26 @@ def _np_type(t):
     return np.dtype(t)
 
 
+class DofsFlowParams(C.Structure, _NpMixin):
+    """dofs_flow_params: calcOpticalFlowFarneback arguments (cpp/src/segment.cpp:101)."""
+    _fields_ = [
+        ("pyr_scale", C.c_double),
+        ("levels", C.c_int32),
+        ("winsize", C.c_int32),
+        ("iterations", C.c_int32),
+        ("poly_n", C.c_int32),
+        ("poly_sigma", C.c_double),
+        ("flags", C.c_int32),
+    ]
+
+
+def default_flow_params(**kw) -> "DofsFlowParams":
+    p = DofsFlowParams(0.5, 3, 15, 3, 5, 1.2, 0)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
 class DofsParams(C.Structure, _NpMixin):
     _fields_ = [
         ("blur_sigma", C.c_double),

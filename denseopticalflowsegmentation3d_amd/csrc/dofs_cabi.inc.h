@@ -2,10 +2,13 @@
 // that has defined `using DofsBackend = <backend>;` (dofs_hip.hip: the HIP backend).
 #pragma once
 
+#include <memory>
+
 #include "dofs_api.h"
 
 struct dofs_ctx : dofs::Context<DofsBackend> {
     explicit dofs_ctx(int device) : dofs::Context<DofsBackend>(device) {}
+    std::shared_ptr<void> flow_engine;  // the optical-flow stage (HIP build; created on first use)
 };
 
 extern "C" {

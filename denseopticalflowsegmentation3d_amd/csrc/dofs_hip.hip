@@ -1313,3 +1313,85 @@ struct HipBackend {
 
 using DofsBackend = dofs::HipBackend;
 #include "dofs_cabi.inc.h"
+
+// ---- optical flow (upstream stage; HIP build only) ---------------------------------------------
+#include "dofs_flow.h"
+
+namespace {
+dofs::flow::Engine* flow_engine(dofs_ctx* ctx) {
+    if (!ctx->flow_engine) ctx->flow_engine = std::make_shared<dofs::flow::Engine>();
+    return static_cast<dofs::flow::Engine*>(ctx->flow_engine.get());
+}
+}  // namespace
+
+extern "C" {
+
+void dofs_default_flow_params(dofs_flow_params* p) {
+    if (!p) return;
+    p->pyr_scale = 0.5;
+    p->levels = 3;
+    p->winsize = 15;
+    p->iterations = 3;
+    p->poly_n = 5;
+    p->poly_sigma = 1.2;
+    p->flags = 0;
+}
+
+int32_t dofs_farneback_batch_device(dofs_ctx* ctx, const uint8_t* d_prev, const uint8_t* d_next, int32_t B,
+                                    int32_t H, int32_t W, const dofs_flow_params* params, float* d_flow,
+                                    void* stream) {
+    if (!ctx || !d_prev || !d_next || !d_flow || B <= 0 || H <= 0 || W <= 0) return DOFS_ERR_INVALID_ARG;
+    dofs_flow_params p;
+    dofs_default_flow_params(&p);
+    if (params) p = *params;
+    dofs::flow::Engine* e = flow_engine(ctx);
+    const int rc = e->run(d_prev, d_next, B, H, W, p, d_flow, (hipStream_t)stream);
+    if (rc != DOFS_OK) ctx->err = e->err;
+    return rc;
+}
+
+int32_t dofs_farneback(dofs_ctx* ctx, const uint8_t* prev, const uint8_t* next, int32_t H, int32_t W,
+                       size_t row_stride_bytes, const dofs_flow_params* params, float* flow_uv) {
+    if (!ctx || !prev || !next || !flow_uv || H <= 0 || W <= 0) return DOFS_ERR_INVALID_ARG;
+    const size_t st = row_stride_bytes ? row_stride_bytes : (size_t)W;
+    const size_t n = (size_t)H * W;
+    uint8_t* d = nullptr;
+    float* df = nullptr;
+    hipStream_t s = nullptr;
+    int rc = DOFS_ERR_DEVICE;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess && hipMalloc(&d, 2 * n) == hipSuccess &&
+        hipMalloc(&df, sizeof(float) * 2 * n) == hipSuccess &&
+        hipMemcpy2DAsync(d, W, prev, st, W, H, hipMemcpyHostToDevice, s) == hipSuccess &&
+        hipMemcpy2DAsync(d + n, W, next, st, W, H, hipMemcpyHostToDevice, s) == hipSuccess) {
+        rc = dofs_farneback_batch_device(ctx, d, d + n, 1, H, W, params, df, s);
+        if (rc == DOFS_OK &&
+            (hipMemcpyAsync(flow_uv, df, sizeof(float) * 2 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+             hipStreamSynchronize(s) != hipSuccess))
+            rc = DOFS_ERR_DEVICE;
+    }
+    if (rc == DOFS_ERR_DEVICE && ctx->err.empty()) ctx->err = "HIP error in dofs_farneback";
+    if (s) (void)hipStreamSynchronize(s);
+    if (d) (void)hipFree(d);
+    if (df) (void)hipFree(df);
+    if (s) (void)hipStreamDestroy(s);
+    return rc;
+}
+
+void dofs_bgr_to_gray(const uint8_t* bgr, int32_t H, int32_t W, size_t row_stride_bytes, uint8_t* gray) {
+    const size_t st = row_stride_bytes ? row_stride_bytes : (size_t)W * 3;
+    for (int32_t y = 0; y < H; ++y)
+        for (int32_t x = 0; x < W; ++x) {
+            const uint8_t* q = bgr + y * st + 3 * x;
+            gray[(size_t)y * W + x] = (uint8_t)((q[0] * 1868 + q[1] * 9617 + q[2] * 4899 + (1 << 13)) >> 14);
+        }
+}
+
+int32_t dofs_bgr_to_gray_device(const uint8_t* d_bgr, int64_t n_pixels, uint8_t* d_gray, void* stream) {
+    if (!d_bgr || !d_gray || n_pixels < 0) return DOFS_ERR_INVALID_ARG;
+    if (n_pixels == 0) return DOFS_OK;
+    const unsigned gx = (unsigned)std::min<int64_t>((n_pixels + 255) / 256, 16384);
+    hipLaunchKernelGGL(dofs::flow::k_bgr_gray, dim3(gx), dim3(256), 0, (hipStream_t)stream, d_bgr, n_pixels, d_gray);
+    return hipGetLastError() == hipSuccess ? DOFS_OK : DOFS_ERR_DEVICE;
+}
+
+}  // extern "C"

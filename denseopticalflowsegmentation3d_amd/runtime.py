@@ -12,8 +12,8 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from .abi import (DofsBoxRecord, DofsEvent, DofsParams, DofsResult, DofsSnapshot, DofsSolution, default_params,
-                  solution_dict)
+from .abi import (DofsBoxRecord, DofsEvent, DofsFlowParams, DofsParams, DofsResult, DofsSnapshot, DofsSolution,
+                  default_flow_params, default_params, solution_dict)
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DOFS_LIB") or os.path.join(_PKG, "_build", "libdofs_hip.so")
@@ -30,6 +30,10 @@ def load(path: str | None = None) -> C.CDLL:
         return _LIBS[path]
     if not os.path.exists(path):
         raise RuntimeError(f"dofs HIP extension not built: {path} missing (run __graft_entry__.build())")
+    try:  # one HIP runtime per process: torch's libamdhip64.so.7 first (same soname as /opt/rocm's), so
+        import torch  # noqa: F401  a caller's torch device work keeps working after our context exists
+    except ImportError:
+        pass
     L = C.CDLL(path)
     L.dofs_abi_version.restype = C.c_int32
     L.dofs_default_params.argtypes = [C.POINTER(DofsParams)]
@@ -81,6 +85,18 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_lift_batch.restype = C.c_int32
     L.dofs_synth_flow_device.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_uint64, C.c_void_p]
     L.dofs_synth_flow_device.restype = C.c_int32
+    if hasattr(L, "dofs_farneback"):  # the optical-flow stage (HIP build; the test emulator has none)
+        u8 = C.POINTER(C.c_uint8)
+        L.dofs_default_flow_params.argtypes = [C.POINTER(DofsFlowParams)]
+        L.dofs_farneback.argtypes = [C.c_void_p, u8, u8, C.c_int32, C.c_int32, C.c_size_t, C.POINTER(DofsFlowParams),
+                                     _fp]
+        L.dofs_farneback.restype = C.c_int32
+        L.dofs_farneback_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
+                                                  C.POINTER(DofsFlowParams), C.c_void_p, C.c_void_p]
+        L.dofs_farneback_batch_device.restype = C.c_int32
+        L.dofs_bgr_to_gray.argtypes = [u8, C.c_int32, C.c_int32, C.c_size_t, u8]
+        L.dofs_bgr_to_gray_device.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
+        L.dofs_bgr_to_gray_device.restype = C.c_int32
     if L.dofs_abi_version() != 1:
         raise RuntimeError("dofs ABI version mismatch")
     _LIBS[path] = L
@@ -297,6 +313,46 @@ class Dofs:
                                       out.ctypes.data_as(C.POINTER(DofsSolution)))
         self._err(rc, "dofs_lift_batch")
         return out
+
+
+    # ---- optical flow (upstream of the path) ----
+    def farneback(self, prev, nxt, **params) -> np.ndarray:
+        """calcOpticalFlowFarneback(prev, next, flow, 0.5, 3, 15, 3, 5, 1.2, 0) on the GPU (host arrays)."""
+        a = np.ascontiguousarray(prev, np.uint8)
+        b = np.ascontiguousarray(nxt, np.uint8)
+        if a.shape != b.shape or a.ndim != 2:
+            raise ValueError("prev and next must be equal-size 2-D uint8 frames")
+        H, W = a.shape
+        out = np.zeros((H, W, 2), np.float32)
+        p = default_flow_params(**params)
+        rc = self.lib.dofs_farneback(self.ctx, _p(a, C.c_uint8), _p(b, C.c_uint8), H, W, 0, C.byref(p), _p(out))
+        self._err(rc, "dofs_farneback")
+        return out
+
+    def farneback_batch_device(self, d_prev: int, d_next: int, B: int, H: int, W: int, d_flow: int,
+                               stream: int | None = None, **params) -> None:
+        """Device batch: B x H x W uint8 frame pairs -> B x H x W x 2 float32 flow, asynchronous on stream."""
+        p = default_flow_params(**params)
+        rc = self.lib.dofs_farneback_batch_device(self.ctx, C.c_void_p(d_prev), C.c_void_p(d_next), B, H, W,
+                                                  C.byref(p), C.c_void_p(d_flow), C.c_void_p(stream or 0))
+        self._err(rc, "dofs_farneback_batch_device")
+
+
+def bgr_to_gray(bgr, lib: C.CDLL | None = None) -> np.ndarray:
+    """cvtColor(COLOR_BGR2GRAY) (host code of the library)."""
+    L = lib or load()
+    a = np.ascontiguousarray(bgr, np.uint8)
+    H, W = a.shape[:2]
+    out = np.empty((H, W), np.uint8)
+    L.dofs_bgr_to_gray(_p(a, C.c_uint8), H, W, 0, _p(out, C.c_uint8))
+    return out
+
+
+def bgr_to_gray_device(d_bgr: int, n_pixels: int, d_gray: int, stream: int | None = None,
+                       lib: C.CDLL | None = None) -> None:
+    L = lib or load()
+    if L.dofs_bgr_to_gray_device(C.c_void_p(d_bgr), n_pixels, C.c_void_p(d_gray), C.c_void_p(stream or 0)) != 0:
+        raise RuntimeError("dofs_bgr_to_gray_device failed")
 
 
 def synth_flow_device(d_out: int, B: int, H: int, W: int, seed0: int = 0, stream: int | None = None,

@@ -228,6 +228,34 @@ int32_t dofs_lift_batch(dofs_ctx* ctx, int32_t n, const float* dirs, const int32
 /* get_intersect (host code, exact float semantics of lifting_3d.cpp:63-89). */
 void dofs_intersect(const float a1[2], const float a2[2], const float b1[2], const float b2[2], float out[2]);
 
+/* ---- Upstream of the path: dense optical flow --------------------------------
+ * dofs_farneback ← cv::calcOpticalFlowFarneback(prev, next, flow, pyr_scale, levels, winsize,
+ *                   iterations, poly_n, poly_sigma, flags)   as called at cpp/src/segment.cpp:101,226
+ *                   (0.5, 3, 15, 3, 5, 1.2, 0); OpenCV 4.x optflowgf.cpp algorithm, flags 0 only
+ *                   (box-filter update, no initial flow). Frames are 8-bit single channel.
+ * dofs_bgr_to_gray ← cv::cvtColor(im, gray, COLOR_BGR2GRAY)   cpp/src/segment.cpp:97-98,222-223 */
+typedef struct dofs_flow_params {
+    double pyr_scale;   /* 0.5 */
+    int32_t levels;     /* 3   */
+    int32_t winsize;    /* 15  */
+    int32_t iterations; /* 3   */
+    int32_t poly_n;     /* 5   */
+    double poly_sigma;  /* 1.2 */
+    int32_t flags;      /* 0 (OPTFLOW_USE_INITIAL_FLOW / OPTFLOW_FARNEBACK_GAUSSIAN unsupported) */
+} dofs_flow_params;
+void dofs_default_flow_params(dofs_flow_params* p);
+/* Host frames (row stride in bytes, 0 = packed) -> host flow H x W x 2 float32. Synchronous. */
+int32_t dofs_farneback(dofs_ctx* ctx, const uint8_t* prev, const uint8_t* next, int32_t H, int32_t W,
+                       size_t row_stride_bytes, const dofs_flow_params* params, float* flow_uv);
+/* Device batch: d_prev, d_next = B x H x W uint8 (packed), d_flow = B x H x W x 2 float32 — the layout
+ * dofs_segment_batch_device consumes. Asynchronous on `stream` (NULL = the default stream). */
+int32_t dofs_farneback_batch_device(dofs_ctx* ctx, const uint8_t* d_prev, const uint8_t* d_next, int32_t B,
+                                    int32_t H, int32_t W, const dofs_flow_params* params, float* d_flow,
+                                    void* stream);
+/* BGR (3 bytes per pixel, packed rows) -> gray: host, and device (n_pixels, asynchronous on stream). */
+void dofs_bgr_to_gray(const uint8_t* bgr, int32_t H, int32_t W, size_t row_stride_bytes, uint8_t* gray);
+int32_t dofs_bgr_to_gray_device(const uint8_t* d_bgr, int64_t n_pixels, uint8_t* d_gray, void* stream);
+
 /* Synthetic flow fields of the benchmark spec (DESIGN.md §Synthetic input), generated on device:
  * frame b uses seed0 + b. d_out = B×H×W×2 float32. */
 int32_t dofs_synth_flow_device(float* d_out, int32_t B, int32_t H, int32_t W, uint64_t seed0, void* stream);

@@ -175,3 +175,86 @@ def segment(flow: np.ndarray, persp, inv, inv_upper, params: DofsParams | None =
     st = {k: getattr(res.stats, k) for k, _ in res.stats._fields_}
     return OracleResult(H, W, snaps[:res.n_snapshots].copy(), labels, leaf, blurred, st,
                         ev[:max(N - 1, 0)] if events else None)
+
+
+# ---- Farneback dense optical flow (oracle/farneback.cpp) ----------------------
+FARNEBACK_REF = dict(pyr_scale=0.5, levels=3, winsize=15, iterations=3, poly_n=5, poly_sigma=1.2, flags=0)
+
+
+def _fb_lib() -> C.CDLL:
+    L = lib()
+    if getattr(L, "_fb_ready", False):
+        return L
+    u8p = C.POINTER(C.c_uint8)
+    fp = C.POINTER(C.c_float)
+    L.oracle_bgr_to_gray.argtypes = [u8p, C.c_int32, C.c_int32, u8p]
+    L.oracle_fb_gauss_kernel.argtypes = [C.c_int32, C.c_double, fp]
+    L.oracle_fb_poly_consts.argtypes = [C.c_int32, C.c_double, fp, fp, fp, C.POINTER(C.c_double)]
+    L.oracle_fb_blur.argtypes = [fp, C.c_int32, C.c_int32, C.c_int32, C.c_double, fp]
+    L.oracle_fb_resize.argtypes = [fp, C.c_int32, C.c_int32, C.c_int32, fp, C.c_int32, C.c_int32]
+    L.oracle_fb_poly_exp.argtypes = [fp, C.c_int32, C.c_int32, C.c_int32, C.c_double, fp]
+    L.oracle_farneback.argtypes = [u8p, u8p, C.c_int32, C.c_int32, C.c_double, C.c_int32, C.c_int32, C.c_int32,
+                                   C.c_int32, C.c_double, C.c_int32, fp]
+    L.oracle_farneback.restype = C.c_int32
+    L._fb_ready = True
+    return L
+
+
+def bgr_to_gray(bgr: np.ndarray) -> np.ndarray:
+    bgr = np.ascontiguousarray(bgr, dtype=np.uint8)
+    H, W = bgr.shape[:2]
+    out = np.empty((H, W), np.uint8)
+    _fb_lib().oracle_bgr_to_gray(_ptr(bgr, C.c_uint8), H, W, _ptr(out, C.c_uint8))
+    return out
+
+
+def farneback(prev: np.ndarray, nxt: np.ndarray, **kw) -> np.ndarray:
+    """calcOpticalFlowFarneback(prev, next, flow, 0.5, 3, 15, 3, 5, 1.2, 0) restated (segment.cpp:101)."""
+    p = dict(FARNEBACK_REF, **kw)
+    a = np.ascontiguousarray(prev, dtype=np.uint8)
+    b = np.ascontiguousarray(nxt, dtype=np.uint8)
+    H, W = a.shape
+    out = np.zeros((H, W, 2), np.float32)
+    r = _fb_lib().oracle_farneback(_ptr(a, C.c_uint8), _ptr(b, C.c_uint8), H, W, p["pyr_scale"], p["levels"],
+                                   p["winsize"], p["iterations"], p["poly_n"], p["poly_sigma"], p["flags"],
+                                   _ptr(out, C.c_float))
+    if r < 0:
+        raise ValueError("unsupported Farneback flags")
+    return out
+
+
+def fb_stage(name: str, *args):
+    """One Farneback stage of the oracle (unit tests of the GPU stages)."""
+    L = _fb_lib()
+    if name == "gauss_kernel":
+        n, sigma = args
+        out = np.zeros(n, np.float32)
+        L.oracle_fb_gauss_kernel(n, sigma, _ptr(out, C.c_float))
+        return out
+    if name == "poly_consts":
+        n, sigma = args
+        g, xg, xxg = (np.zeros(2 * n + 1, np.float32) for _ in range(3))
+        ig = np.zeros(4, np.float64)
+        L.oracle_fb_poly_consts(n, sigma, _ptr(g, C.c_float), _ptr(xg, C.c_float), _ptr(xxg, C.c_float),
+                                _ptr(ig, C.c_double))
+        return g, xg, xxg, ig
+    if name == "blur":
+        img, ks, sigma = args
+        img = _f(img)
+        out = np.empty_like(img)
+        L.oracle_fb_blur(_ptr(img, C.c_float), img.shape[0], img.shape[1], ks, sigma, _ptr(out, C.c_float))
+        return out
+    if name == "resize":
+        img, dh, dw = args
+        img = _f(img)
+        cn = 1 if img.ndim == 2 else img.shape[2]
+        out = np.empty((dh, dw) + (() if img.ndim == 2 else (cn,)), np.float32)
+        L.oracle_fb_resize(_ptr(img, C.c_float), img.shape[0], img.shape[1], cn, _ptr(out, C.c_float), dh, dw)
+        return out
+    if name == "poly_exp":
+        img, n, sigma = args
+        img = _f(img)
+        out = np.empty(img.shape + (5,), np.float32)
+        L.oracle_fb_poly_exp(_ptr(img, C.c_float), img.shape[0], img.shape[1], n, sigma, _ptr(out, C.c_float))
+        return out
+    raise KeyError(name)

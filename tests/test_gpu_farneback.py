@@ -1,0 +1,81 @@
+"""GPU: the optical-flow stage (dofs_farneback*, csrc/dofs_flow.h) against the oracle restatement
+(oracle/farneback.cpp), bit for bit: every kernel repeats the oracle's float / double operations in
+the same order (no FMA), so the tolerance is zero. Parity with OpenCV itself is unpinned."""
+import numpy as np
+import pytest
+
+from oracle import binding as ob
+from test_farneback import _pair
+
+pytestmark = pytest.mark.gpu
+
+
+def _eq(a, b):
+    if not np.array_equal(a, b):
+        bad = np.argwhere(a != b)
+        raise AssertionError(f"{len(bad)} flow values differ, first at {bad[0].tolist()}: "
+                             f"{a[tuple(bad[0])]} vs {b[tuple(bad[0])]}")
+
+
+@pytest.mark.parametrize("H,W,dx,dy", [(128, 160, 2, 1), (97, 131, -1, 2), (40, 50, 1, 0), (360, 640, 3, -2)])
+def test_flow_matches_oracle(gpu, H, W, dx, dy):
+    a, b = _pair(H, W, dx, dy, seed=H)
+    _eq(gpu.farneback(a, b), ob.farneback(a, b))
+
+
+def test_reference_frames_match_oracle(gpu):
+    from denseopticalflowsegmentation3d_amd import video
+    a, b = video.load_gray_pair()
+    _eq(gpu.farneback(a, b), ob.farneback(a, b))
+
+
+def test_config3_upscaled_frames_match_oracle(gpu):
+    from denseopticalflowsegmentation3d_amd import video
+    a, b = video.config3_pair()
+    _eq(gpu.farneback(a, b), ob.farneback(a, b))
+
+
+@pytest.mark.parametrize("kw", [dict(levels=0), dict(winsize=5, iterations=1), dict(poly_n=7, poly_sigma=1.5),
+                                dict(pyr_scale=0.6, levels=4), dict(iterations=5, winsize=21)])
+def test_parameters_match_oracle(gpu, kw):
+    a, b = _pair(150, 190, 2, 2, seed=7)
+    _eq(gpu.farneback(a, b, **kw), ob.farneback(a, b, **kw))
+
+
+def test_device_batch_matches_oracle(gpu):
+    import torch
+    pairs = [_pair(120, 176, dx, dy, seed=10 + i) for i, (dx, dy) in enumerate([(1, 1), (-2, 0), (0, 3)])]
+    prev = torch.tensor(np.stack([p[0] for p in pairs]), device="cuda:0")
+    nxt = torch.tensor(np.stack([p[1] for p in pairs]), device="cuda:0")
+    flow = torch.empty((3, 120, 176, 2), dtype=torch.float32, device="cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    gpu.farneback_batch_device(prev.data_ptr(), nxt.data_ptr(), 3, 120, 176, flow.data_ptr(), stream=s)
+    got = flow.cpu().numpy()
+    for i, (a, b) in enumerate(pairs):
+        _eq(got[i], ob.farneback(a, b))
+
+
+def test_bgr_to_gray_device(gpu):
+    import torch
+    from denseopticalflowsegmentation3d_amd import runtime
+    rng = np.random.default_rng(8)
+    bgr = rng.integers(0, 256, (45, 67, 3), dtype=np.uint8)
+    d = torch.tensor(bgr, device="cuda:0")
+    g = torch.empty((45, 67), dtype=torch.uint8, device="cuda:0")
+    runtime.bgr_to_gray_device(d.data_ptr(), 45 * 67, g.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert np.array_equal(g.cpu().numpy(), ob.bgr_to_gray(bgr))
+
+
+def test_flow_feeds_segment(gpu, calib):
+    """Config 1 shape end to end on the GPU: real frame pair -> flow -> segment, against the oracle
+    chain (oracle flow -> oracle segment)."""
+    from denseopticalflowsegmentation3d_amd import video
+    from parity import params
+    a, b = video.load_gray_pair()
+    flow = gpu.farneback(a, b)
+    persp, inv, up = calib
+    prm = params()
+    g = gpu.segment(flow, persp, inv, up, params=prm)
+    o = ob.segment(ob.farneback(a, b), persp, inv, up, params=prm, mode=0)
+    assert np.array_equal(g.labels, o.labels)
+    assert np.array_equal(g.snapshots["slot"], o.snapshots["slot"])
