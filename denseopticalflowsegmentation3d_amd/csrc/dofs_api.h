@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 
+#include "dofs_overlay.h"
 #include "dofs_pipeline.h"
 
 namespace dofs {
@@ -177,6 +178,8 @@ struct Context {
     size_t d_in_bytes = 0;
     void* d_scratch = nullptr;
     size_t d_scratch_bytes = 0;
+    int* d_lmap[kSlots] = {nullptr, nullptr, nullptr};  // overlay edge maps per workspace (api_overlay)
+    size_t d_lmap_bytes[kSlots] = {0, 0, 0};
     int64_t nbatch = 0;  // batches issued; batch id b uses workspace b % nslots
     int nslots = kSlots;
     int64_t snap_cap = 4096;
@@ -218,6 +221,8 @@ struct Context {
         drain();
         if (d_in) be.free(d_in);
         if (d_scratch) be.free(d_scratch);
+        for (int k = 0; k < kSlots; ++k)
+            if (d_lmap[k]) be.free(d_lmap[k]);
     }
     Pipeline<Backend>& pipe(int slot) { return slot == 0 ? p0 : (slot == 1 ? p1 : p2); }
     int slot_of(int64_t id) const { return (int)(id % nslots); }
@@ -504,6 +509,97 @@ int api_lift_batch(Context<Backend>* cx, int n, const float* dirs, const int* bo
     }
     be.launch(1, n, k);
     be.d2h(out, s + o_out, b_out);
+    be.sync();
+    return cx->check();
+}
+
+// plot_best_segments_simple + draw_cube (draw.cpp:85-160) for the frames of batch `batch`:
+// d_frames / d_out = B x H x W x 3 BGR (packed; d_out may equal d_frames). Ordered after the batch
+// on the caller's stream; the edge map belongs to the batch's workspace, so overlays of one batch
+// must be issued on one stream (or before the workspace is reused, batch + slots).
+template <class Backend>
+int api_overlay(Context<Backend>* cx, int64_t batch, const unsigned char* d_frames, unsigned char* d_out) {
+    if (!cx->live(batch) || !d_frames || !d_out) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
+    const int slot = cx->slot_of(batch);
+    const typename Context<Backend>::Meta& m = cx->meta[slot];
+    const Ws& w = cx->pipe(slot).w;
+    const int64_t N = (int64_t)m.H * m.W;
+    const size_t lbytes = sizeof(int) * (size_t)m.B * (size_t)N;
+    Backend& be = cx->be;
+    if (lbytes > cx->d_lmap_bytes[slot]) {
+        if (cx->d_lmap[slot]) {
+            be.sync();  // an earlier overlay on this stream may still read it
+            be.free(cx->d_lmap[slot]);
+        }
+        cx->d_lmap[slot] = (int*)be.alloc(lbytes);
+        cx->d_lmap_bytes[slot] = cx->d_lmap[slot] ? lbytes : 0;
+        if (!cx->d_lmap[slot]) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    }
+    OverlayWs o;
+    o.frame = d_frames;
+    o.out = d_out;
+    o.lmap = cx->d_lmap[slot];
+    o.labels = w.labels;
+    o.snaps = w.snaps;
+    o.ctr = w.ctr;
+    o.snap_cap = w.snap_cap;
+    o.H = m.H;
+    o.W = m.W;
+    o.N = N;
+    o.min_score = m.prm.overlay_min_score;
+    cx->join(batch);
+    be.memset(o.lmap, 0xFF, lbytes);
+    const int steps = (m.H > m.W ? m.H : m.W) + 1;
+    be.launch(m.B, 12 * (int64_t)steps, KCubeLines{o, steps});
+    be.launch(m.B, N, KOverlay{o});
+    return cx->check();
+}
+
+// Host form for frame `frame` of the last batch (H2D of the frame, overlay, D2H).
+template <class Backend>
+int api_overlay_host(Context<Backend>* cx, int frame, const unsigned char* bgr, size_t stride, unsigned char* out) {
+    if (!cx->have_batch() || !bgr || !out) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
+    const int64_t id = cx->nbatch - 1;
+    const int slot = cx->slot_of(id);
+    const typename Context<Backend>::Meta& m = cx->meta[slot];
+    if (frame < 0 || frame >= m.B) return cx->fail(DOFS_ERR_INVALID_ARG, "no frame");
+    const size_t row = (size_t)m.W * 3, bytes = row * (size_t)m.H;
+    if (stride == 0) stride = row;
+    if (stride < row) return cx->fail(DOFS_ERR_INVALID_ARG, "row stride too small");
+    // a one-frame view of the batch: labels / snapshots / counters of `frame`
+    unsigned char* d = (unsigned char*)cx->scratch(2 * bytes + 256);
+    if (!d) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    Backend& be = cx->be;
+    if (stride == row)
+        be.h2d(d, bgr, bytes);
+    else
+        for (int y = 0; y < m.H; ++y) be.h2d(d + row * y, bgr + stride * y, row);
+    const Ws& w = cx->pipe(slot).w;
+    const int64_t N = (int64_t)m.H * m.W;
+    if (sizeof(int) * (size_t)N > cx->d_lmap_bytes[slot]) {
+        if (cx->d_lmap[slot]) be.free(cx->d_lmap[slot]);
+        cx->d_lmap[slot] = (int*)be.alloc(sizeof(int) * (size_t)m.B * N);
+        cx->d_lmap_bytes[slot] = cx->d_lmap[slot] ? sizeof(int) * (size_t)m.B * N : 0;
+        if (!cx->d_lmap[slot]) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    }
+    OverlayWs o;
+    o.frame = d;
+    o.out = d + bytes;
+    o.lmap = cx->d_lmap[slot];
+    o.labels = w.labels + (int64_t)frame * N;
+    o.snaps = w.snaps + (int64_t)frame * w.snap_cap;
+    o.ctr = w.ctr + (int64_t)frame * kCounters;
+    o.snap_cap = w.snap_cap;
+    o.H = m.H;
+    o.W = m.W;
+    o.N = N;
+    o.min_score = m.prm.overlay_min_score;
+    cx->join(id);
+    be.memset(o.lmap, 0xFF, sizeof(int) * (size_t)N);
+    const int steps = (m.H > m.W ? m.H : m.W) + 1;
+    be.launch(1, 12 * (int64_t)steps, KCubeLines{o, steps});
+    be.launch(1, N, KOverlay{o});
+    be.d2h(out, d + bytes, bytes);
     be.sync();
     return cx->check();
 }

@@ -9,6 +9,7 @@
 struct dofs_ctx : dofs::Context<DofsBackend> {
     explicit dofs_ctx(int device) : dofs::Context<DofsBackend>(device) {}
     std::shared_ptr<void> flow_engine;  // the optical-flow stage (HIP build; created on first use)
+    std::shared_ptr<void> video;        // the clip pipeline's buffers and streams (HIP build)
 };
 
 extern "C" {
@@ -159,6 +160,20 @@ int32_t dofs_synth_flow_device(float* d_out, int32_t B, int32_t H, int32_t W, ui
     if (!d_out || B <= 0 || H <= 0 || W <= 0) return DOFS_ERR_INVALID_ARG;
     dofs::KSynth k{(dofs::F2*)d_out, H, W, (unsigned long long)seed0};
     return DofsBackend::launch_static(stream, B, (int64_t)H * W, k);
+}
+
+int32_t dofs_overlay_batch_device(dofs_ctx* ctx, int64_t batch, const uint8_t* d_frames, uint8_t* d_out,
+                                  void* stream) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    ctx->be.set_stream(stream);
+    return dofs::api_overlay(ctx, batch, d_frames, d_out);
+}
+
+int32_t dofs_overlay(dofs_ctx* ctx, int32_t frame, const uint8_t* frame_bgr, size_t row_stride_bytes,
+                     uint8_t* out_bgr) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    ctx->be.use_own();
+    return dofs::api_overlay_host(ctx, frame, frame_bgr, row_stride_bytes, out_bgr);
 }
 
 }  // extern "C"

@@ -1322,6 +1322,124 @@ dofs::flow::Engine* flow_engine(dofs_ctx* ctx) {
     if (!ctx->flow_engine) ctx->flow_engine = std::make_shared<dofs::flow::Engine>();
     return static_cast<dofs::flow::Engine*>(ctx->flow_engine.get());
 }
+
+// main1's loop (segment.cpp:209-269) over a device-resident clip: gray, Farneback, segment and overlay
+// of consecutive frame pairs, in chunks of `batch` pairs. Chunk c runs its Farneback on flow stream
+// sf[c % 2] (own Farneback workspace and flow buffer), submits the chunk to the context's two-stage
+// segment pipeline from that stream, and its overlay + box-record copy run on stream so once the
+// chunk's segmentation is done — so chunk c+1's Farneback overlaps chunk c's graph stage, and the
+// overlay of chunk c overlaps chunk c+1's stages.
+struct VideoState {
+    unsigned char* gray = nullptr;
+    size_t gray_bytes = 0;
+    float* flow[2] = {nullptr, nullptr};
+    size_t flow_bytes = 0;
+    dofs::flow::Engine eng[2];
+    hipStream_t sf[2] = {nullptr, nullptr};
+    hipStream_t so = nullptr;
+    hipEvent_t ev_in = nullptr, ev_gray = nullptr, ev_end[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_ov[dofs::Context<DofsBackend>::kSlots] = {};
+    bool ok = true;
+    explicit VideoState(int device) {
+        (void)hipSetDevice(device);
+        for (auto* st : {&sf[0], &sf[1], &so}) ok = ok && hipStreamCreateWithFlags(st, hipStreamNonBlocking) == hipSuccess;
+        for (auto* e : {&ev_in, &ev_gray, &ev_end[0], &ev_end[1], &ev_end[2]})
+            ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+        for (auto& e : ev_ov) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    }
+    ~VideoState() {
+        for (auto st : {sf[0], sf[1], so})
+            if (st) (void)hipStreamSynchronize(st);
+        if (gray) (void)hipFree(gray);
+        for (auto f : flow)
+            if (f) (void)hipFree(f);
+        for (auto st : {sf[0], sf[1], so})
+            if (st) (void)hipStreamDestroy(st);
+        for (auto e : {ev_in, ev_gray, ev_end[0], ev_end[1], ev_end[2]})
+            if (e) (void)hipEventDestroy(e);
+        for (auto e : ev_ov)
+            if (e) (void)hipEventDestroy(e);
+    }
+    bool reserve(size_t gb, size_t fb) {
+        for (auto st : {sf[0], sf[1], so}) (void)hipStreamSynchronize(st);
+        if (gb > gray_bytes) {
+            if (gray) (void)hipFree(gray);
+            gray = nullptr;
+            gray_bytes = hipMalloc(&gray, gb) == hipSuccess ? gb : 0;
+            if (!gray_bytes) return false;
+        }
+        if (fb > flow_bytes) {
+            for (auto& f : flow) {
+                if (f) (void)hipFree(f);
+                f = nullptr;
+            }
+            flow_bytes = (hipMalloc(&flow[0], fb) == hipSuccess && hipMalloc(&flow[1], fb) == hipSuccess) ? fb : 0;
+            if (!flow_bytes) return false;
+        }
+        return true;
+    }
+};
+
+int video_clip(dofs_ctx* ctx, const unsigned char* d_bgr, int n, int H, int W, int batch, const float persp[9],
+               const float inv[9], const float inv_upper[27], const dofs_params* params,
+               const dofs_flow_params& fp, unsigned char* d_overlay, int* d_counts, dofs_box_record* d_records,
+               int per_frame, hipStream_t caller) {
+    if (!ctx->video) ctx->video = std::make_shared<VideoState>(ctx->be.device);
+    VideoState& v = *static_cast<VideoState*>(ctx->video.get());
+    if (!v.ok) return ctx->fail(DOFS_ERR_DEVICE, "video streams");
+    const int64_t N = (int64_t)H * W;
+    const int P = n - 1;  // frame pairs
+    if (!v.reserve((size_t)n * N, sizeof(float) * 2 * (size_t)batch * N))
+        return ctx->fail(DOFS_ERR_OOM, "video buffers");
+    auto ck = [&](hipError_t e) { return e == hipSuccess; };
+    bool ok = ck(hipEventRecord(v.ev_in, caller));
+    for (auto st : {v.sf[0], v.sf[1], v.so}) ok = ok && ck(hipStreamWaitEvent(st, v.ev_in, 0));
+    const int64_t px = (int64_t)n * N;
+    hipLaunchKernelGGL(dofs::flow::k_bgr_gray, dim3((unsigned)std::min<int64_t>((px + 255) / 256, 16384)), dim3(256),
+                       0, v.sf[0], d_bgr, px, v.gray);
+    ok = ok && ck(hipGetLastError()) && ck(hipEventRecord(v.ev_gray, v.sf[0])) &&
+         ck(hipStreamWaitEvent(v.sf[1], v.ev_gray, 0));
+    if (!ok) return ctx->fail(DOFS_ERR_DEVICE, "video setup");
+    const int nslots = ctx->nslots;
+    std::vector<bool> ov_rec(nslots, false);
+    for (int i = 0, c = 0; i < P; i += batch, ++c) {
+        const int bc = std::min(batch, P - i);
+        const int k = c & 1;
+        hipStream_t st = v.sf[k];
+        const int slot = ctx->slot_of(ctx->nbatch);
+        // the workspace this chunk takes was last read by an overlay / record copy on v.so
+        if (ov_rec[slot] && !ck(hipStreamWaitEvent(st, v.ev_ov[slot], 0))) return ctx->fail(DOFS_ERR_DEVICE, "wait");
+        int rc = v.eng[k].run(v.gray + (int64_t)i * N, v.gray + (int64_t)(i + 1) * N, bc, H, W, fp, v.flow[k], st);
+        if (rc != DOFS_OK) return ctx->fail(rc, v.eng[k].err);
+        ctx->be.set_stream(st);  // api_run leaves st ordered after the chunk's graph stage (flow consumed)
+        rc = dofs::api_run(ctx, (const dofs::F2*)v.flow[k], N, bc, H, W, persp, inv, inv_upper, params);
+        if (rc != DOFS_OK) return rc;
+        const int64_t id = ctx->nbatch - 1;
+        ctx->be.set_stream(v.so);
+        if (d_overlay) {
+            rc = dofs::api_overlay(ctx, id, d_bgr + (int64_t)(i + 1) * N * 3, d_overlay + (int64_t)i * N * 3);
+            if (rc != DOFS_OK) return rc;
+        } else {
+            ctx->join(id);
+        }
+        const dofs::Ws& w = ctx->pipe(slot).w;
+        if (d_counts)
+            ctx->be.copy2d(d_counts + i, sizeof(int), w.ctr + dofs::C_SNAP, sizeof(int) * dofs::kCounters, sizeof(int),
+                           bc);
+        const int kr = std::min(per_frame, w.snap_cap);
+        if (d_records && kr > 0)
+            ctx->be.copy2d(d_records + (int64_t)i * per_frame, sizeof(dofs_box_record) * per_frame, w.recs,
+                           sizeof(dofs_box_record) * w.snap_cap, sizeof(dofs_box_record) * kr, bc);
+        if (!ck(hipEventRecord(v.ev_ov[slot], v.so))) return ctx->fail(DOFS_ERR_DEVICE, "record");
+        ov_rec[slot] = true;
+    }
+    ctx->be.set_stream(caller);
+    hipStream_t all[3] = {v.sf[0], v.sf[1], v.so};
+    for (int t = 0; t < 3; ++t)
+        ok = ok && ck(hipEventRecord(v.ev_end[t], all[t])) && ck(hipStreamWaitEvent(caller, v.ev_end[t], 0));
+    if (!ok) return ctx->fail(DOFS_ERR_DEVICE, "video join");
+    return ctx->check();
+}
 }  // namespace
 
 extern "C" {
@@ -1375,6 +1493,21 @@ int32_t dofs_farneback(dofs_ctx* ctx, const uint8_t* prev, const uint8_t* next, 
     if (df) (void)hipFree(df);
     if (s) (void)hipStreamDestroy(s);
     return rc;
+}
+
+int32_t dofs_video_clip_device(dofs_ctx* ctx, const uint8_t* d_bgr, int32_t n_frames, int32_t H, int32_t W,
+                               int32_t batch, const float persp[9], const float inv[9], const float inv_upper[27],
+                               const dofs_params* params, const dofs_flow_params* flow_params, uint8_t* d_overlay,
+                               int32_t* d_counts, dofs_box_record* d_records, int32_t per_frame, void* stream) {
+    if (!ctx || !d_bgr || n_frames < 1 || H <= 0 || W <= 0 || batch <= 0 || per_frame < 0 || !persp || !inv ||
+        !inv_upper)
+        return DOFS_ERR_INVALID_ARG;
+    if (n_frames == 1) return DOFS_OK;  // no pair (main1 keeps the first frame as prev_frame)
+    dofs_flow_params fp;
+    dofs_default_flow_params(&fp);
+    if (flow_params) fp = *flow_params;
+    return video_clip(ctx, d_bgr, n_frames, H, W, batch, persp, inv, inv_upper, params, fp, d_overlay, d_counts,
+                      d_records, per_frame, (hipStream_t)stream);
 }
 
 void dofs_bgr_to_gray(const uint8_t* bgr, int32_t H, int32_t W, size_t row_stride_bytes, uint8_t* gray) {

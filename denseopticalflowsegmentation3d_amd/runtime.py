@@ -97,6 +97,14 @@ def load(path: str | None = None) -> C.CDLL:
         L.dofs_bgr_to_gray.argtypes = [u8, C.c_int32, C.c_int32, C.c_size_t, u8]
         L.dofs_bgr_to_gray_device.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
         L.dofs_bgr_to_gray_device.restype = C.c_int32
+        L.dofs_video_clip_device.argtypes = ([C.c_void_p, C.c_void_p] + [C.c_int32] * 4 + [_fp, _fp, _fp] +
+                                             [C.POINTER(DofsParams), C.POINTER(DofsFlowParams)] +
+                                             [C.c_void_p] * 3 + [C.c_int32, C.c_void_p])
+        L.dofs_video_clip_device.restype = C.c_int32
+    L.dofs_overlay_batch_device.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.dofs_overlay_batch_device.restype = C.c_int32
+    L.dofs_overlay.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(C.c_uint8)]
+    L.dofs_overlay.restype = C.c_int32
     if L.dofs_abi_version() != 1:
         raise RuntimeError("dofs ABI version mismatch")
     _LIBS[path] = L
@@ -314,6 +322,40 @@ class Dofs:
         self._err(rc, "dofs_lift_batch")
         return out
 
+    # ---- overlay (downstream of the path) ----
+    def overlay(self, frame_bgr, frame: int = 0) -> np.ndarray:
+        """plot_best_segments_simple(frame, bev, forest, overlay_min_score) for frame `frame` of the last
+        batch, on the GPU (host H x W x 3 BGR uint8 in, new array out; draw.cpp:101-160)."""
+        a = np.ascontiguousarray(frame_bgr, np.uint8)
+        if a.ndim != 3 or a.shape[2] != 3 or a.shape[:2] != tuple(self._last_hw):
+            raise ValueError(f"frame must be {self._last_hw[0]} x {self._last_hw[1]} x 3 uint8")
+        out = np.empty_like(a)
+        rc = self.lib.dofs_overlay(self.ctx, frame, _p(a, C.c_uint8), 0, _p(out, C.c_uint8))
+        self._err(rc, "dofs_overlay")
+        return out
+
+    def overlay_batch_device(self, batch: int, d_frames: int, d_out: int, stream: int | None = None) -> None:
+        """Overlay of every frame of batch id `batch` (device B x H x W x 3 BGR uint8 in / out, may alias),
+        asynchronous on `stream`, ordered after the batch."""
+        rc = self.lib.dofs_overlay_batch_device(self.ctx, batch, C.c_void_p(d_frames), C.c_void_p(d_out),
+                                                C.c_void_p(stream or 0))
+        self._err(rc, "dofs_overlay_batch_device")
+
+    # ---- main1's video loop (SURVEY.md §8(f) #3) ----
+    def video_clip_device(self, d_bgr: int, n_frames: int, H: int, W: int, persp, inv, inv_upper, batch: int = 8,
+                          d_overlay: int | None = None, d_counts: int | None = None, d_records: int | None = None,
+                          per_frame: int = 64, params: DofsParams | None = None, stream: int | None = None,
+                          **flow_params) -> None:
+        """gray -> Farneback -> segment -> overlay for every consecutive frame pair of a device clip
+        (n_frames x H x W x 3 BGR uint8); outputs for frame p + 1 at index p. Asynchronous on stream."""
+        p, i, u = self._mats(persp, inv, inv_upper)
+        fp = default_flow_params(**flow_params)
+        rc = self.lib.dofs_video_clip_device(self.ctx, C.c_void_p(d_bgr), n_frames, H, W, batch, _p(p), _p(i), _p(u),
+                                             C.byref(params or default_params()), C.byref(fp),
+                                             C.c_void_p(d_overlay or 0), C.c_void_p(d_counts or 0),
+                                             C.c_void_p(d_records or 0), per_frame, C.c_void_p(stream or 0))
+        self._err(rc, "dofs_video_clip_device")
+        self._last_hw = (H, W)
 
     # ---- optical flow (upstream of the path; SURVEY.md §8(f) #1) ----
     def farneback(self, prev, nxt, **params) -> np.ndarray:

@@ -47,3 +47,32 @@ def config3_pair() -> tuple[np.ndarray, np.ndarray]:
     """BASELINE config 3 input: the shipped pair upscaled x3 to 1920x1080."""
     a, b = load_gray_pair()
     return upscale(a, 3), upscale(b, 3)
+
+
+def synth_clip(n: int, H: int = 360, W: int = 640, seed: int = 0) -> np.ndarray:
+    """A BGR test clip (n x H x W x 3 uint8): the reference's frame 1052 (resized to H x W by
+    `upscale` / subsampling) as a static background, plus two textured boxes moving (+4, +1) and
+    (-3, +2) pixels per frame — the kind of scene main1 (segment.cpp:174-275) processes."""
+    bg, _ = load_gray_pair()
+    if (H, W) != bg.shape:
+        f = max(1, -(-H // bg.shape[0]))
+        big = upscale(bg, f) if f > 1 else bg
+        ys = (np.arange(H) * big.shape[0]) // H
+        xs = (np.arange(W) * big.shape[1]) // W
+        bg = big[ys][:, xs]
+    rng = np.random.default_rng(seed)
+    tex = [rng.integers(0, 256, size=(H // 5, W // 6), dtype=np.uint8) for _ in range(2)]
+    starts = [(W // 8, H // 3), (W // 2, H // 6)]
+    vel = [(4, 1), (-3, 2)]
+    out = np.empty((n, H, W, 3), np.uint8)
+    for k in range(n):
+        g = bg.astype(np.int32).copy()
+        for t, (x0, y0), (vx, vy) in zip(tex, starts, vel):
+            x, y = x0 + vx * k, y0 + vy * k
+            h, w = t.shape
+            ys, xs = slice(max(y, 0), min(y + h, H)), slice(max(x, 0), min(x + w, W))
+            g[ys, xs] = t[ys.start - y:ys.stop - y, xs.start - x:xs.stop - x]
+        out[k, :, :, 0] = np.clip(g + 7, 0, 255)
+        out[k, :, :, 1] = g
+        out[k, :, :, 2] = np.clip(g - 11, 0, 255)
+    return out

@@ -256,6 +256,41 @@ int32_t dofs_farneback_batch_device(dofs_ctx* ctx, const uint8_t* d_prev, const 
 void dofs_bgr_to_gray(const uint8_t* bgr, int32_t H, int32_t W, size_t row_stride_bytes, uint8_t* gray);
 int32_t dofs_bgr_to_gray_device(const uint8_t* d_bgr, int64_t n_pixels, uint8_t* d_gray, void* stream);
 
+/* ---- The video loop around the path --------------------------------------------
+ * dofs_video_clip_device ← int main1() (cpp/src/segment.cpp:174-275): for each consecutive frame pair
+ *   of a clip, cvtColor(BGR2GRAY) (:222-223), calcOpticalFlowFarneback(gray1, gray2, flow, 0.5, 3, 15,
+ *   3, 5, 1.2, 0) (:226), get_segmented_array(flow, ...) (:251) and plot_best_segments_simple(frame,
+ *   bev, forest, 0.7) (:258) — decode and display are the caller's. d_bgr = n_frames x H x W x 3 BGR
+ *   uint8 (device). Pair p = (frame p, frame p + 1) writes, for frame p + 1:
+ *     d_overlay + p*H*W*3     the overlay (H x W x 3; NULL = skip),
+ *     d_counts[p]             its snapshot count (NULL = skip),
+ *     d_records + p*per_frame its first per_frame 3D-box records (NULL = skip).
+ *   Pairs run in chunks of `batch` through dofs_farneback_batch_device and the two-stage segment
+ *   pipeline, the Farneback of one chunk overlapping the segmentation of the previous one. Asynchronous
+ *   on `stream`; uses dofs_segment_batch_device batches (results of the last chunks stay readable). */
+int32_t dofs_video_clip_device(dofs_ctx* ctx, const uint8_t* d_bgr, int32_t n_frames, int32_t H, int32_t W,
+                               int32_t batch, const float persp[9], const float inv[9], const float inv_upper[27],
+                               const dofs_params* params, const dofs_flow_params* flow_params, uint8_t* d_overlay,
+                               int32_t* d_counts, dofs_box_record* d_records, int32_t per_frame, void* stream);
+
+/* ---- Downstream of the path: the overlay -------------------------------------
+ * dofs_overlay_batch_device ← cv::Mat plot_best_segments_simple(cv::Mat frame, cv::Mat bev, Forest&,
+ *                              double min_score)   cpp/src/draw.cpp:101-160, with
+ *                              draw_cube(im, lower_face, upper_face, Vec3b(255,0,0), 1)  draw.cpp:85-99
+ *                              as called at cpp/src/segment.cpp:166 and :258 (min_score 0.7 =
+ *                              dofs_params.overlay_min_score of the batch).
+ *   Members of every snapshot with score > min_score painted in its class colour, its 3D box drawn
+ *   (cv::line, thickness 1, 8-connected) into frame and painted copy, then
+ *   addWeighted(frame, 0.6, seg, 0.4, 0). d_frames / d_out = B x H x W x 3 BGR uint8 (packed) of
+ *   batch id `batch` (one of the last dofs_batch_slots issued); d_out may equal d_frames (the
+ *   reference draws into `frame`). Asynchronous on `stream`, ordered after the batch.
+ * dofs_overlay: the same for frame `frame` of the last batch, host buffers (row stride in bytes,
+ *   0 = packed W*3; out is packed). Synchronous. */
+int32_t dofs_overlay_batch_device(dofs_ctx* ctx, int64_t batch, const uint8_t* d_frames, uint8_t* d_out,
+                                  void* stream);
+int32_t dofs_overlay(dofs_ctx* ctx, int32_t frame, const uint8_t* frame_bgr, size_t row_stride_bytes,
+                     uint8_t* out_bgr);
+
 /* Synthetic flow fields of the benchmark spec (DESIGN.md §Synthetic input), generated on device:
  * frame b uses seed0 + b. d_out = B×H×W×2 float32. */
 int32_t dofs_synth_flow_device(float* d_out, int32_t B, int32_t H, int32_t W, uint64_t seed0, void* stream);

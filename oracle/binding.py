@@ -258,3 +258,35 @@ def fb_stage(name: str, *args):
         L.oracle_fb_poly_exp(_ptr(img, C.c_float), img.shape[0], img.shape[1], n, sigma, _ptr(out, C.c_float))
         return out
     raise KeyError(name)
+
+
+# ---- overlay: plot_best_segments_simple + draw_cube (oracle/overlay.cpp) -------
+def _ov_lib() -> C.CDLL:
+    L = lib()
+    if getattr(L, "_ov_ready", False):
+        return L
+    u8p = C.POINTER(C.c_uint8)
+    L.oracle_line.argtypes = [C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float, C.c_float, u8p]
+    L.oracle_overlay.argtypes = [u8p, C.c_int32, C.c_int32, C.POINTER(DofsSnapshot), C.c_int32,
+                                 C.POINTER(C.c_int32), C.c_double, u8p]
+    L._ov_ready = True
+    return L
+
+
+def line_mask(H: int, W: int, a, b) -> np.ndarray:
+    """Pixels cv::line(img, a, b, color, 1) writes on an H x W image (uint8 mask)."""
+    out = np.zeros((H, W), np.uint8)
+    _ov_lib().oracle_line(H, W, float(a[0]), float(a[1]), float(b[0]), float(b[1]), _ptr(out, C.c_uint8))
+    return out
+
+
+def overlay(frame_bgr: np.ndarray, snapshots: np.ndarray, leaf_order: np.ndarray, min_score: float = 0.7):
+    """plot_best_segments_simple(frame, bev, forest, min_score) on one frame (draw.cpp:101-160)."""
+    fr = np.ascontiguousarray(frame_bgr, dtype=np.uint8)
+    H, W = fr.shape[:2]
+    sn = np.ascontiguousarray(snapshots, dtype=DofsSnapshot.np_dtype())
+    lo = np.ascontiguousarray(leaf_order, dtype=np.int32)
+    out = np.empty_like(fr)
+    _ov_lib().oracle_overlay(_ptr(fr, C.c_uint8), H, W, sn.ctypes.data_as(C.POINTER(DofsSnapshot)), len(sn),
+                             _ptr(lo, C.c_int32), min_score, _ptr(out, C.c_uint8))
+    return out

@@ -170,3 +170,14 @@ struct HostBackend {
 
 using DofsBackend = dofs::HostBackend;
 #include "../../denseopticalflowsegmentation3d_amd/csrc/dofs_cabi.inc.h"
+
+// Test-only: the pixels the device line walk (dofs_overlay.h, closed form) covers, for comparison
+// with the oracle's iterative LineIterator restatement.
+extern "C" void emu_line_mask(int32_t H, int32_t W, float ax, float ay, float bx, float by, uint8_t* mask) {
+    const dofs::LineWalk L = dofs::line_walk(W, H, ax, ay, bx, by);
+    for (int64_t t = 0; t < L.count; ++t) {
+        int x, y;
+        L.at(t, x, y);
+        if ((unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H) mask[(int64_t)y * W + x] = 1;
+    }
+}
