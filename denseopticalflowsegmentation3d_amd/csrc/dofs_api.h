@@ -205,6 +205,8 @@ struct Context {
         p0.skip_mask = p1.skip_mask = p2.skip_mask = sm ? atoi(sm) : 0;
         const char* lp = getenv("DOFS_LONG_PATH");
         if (lp && atoi(lp) > 0) p0.long_path = p1.long_path = p2.long_path = atoi(lp);
+        const char* kd = getenv("DOFS_KRT_DNC");
+        p0.krt_dnc = p1.krt_dnc = p2.krt_dnc = kd && kd[0] == '1';
         const char* sp = getenv("DOFS_SPLIT");
         p0.preorder_in_b = p1.preorder_in_b = p2.preorder_in_b = sp && sp[0] == '1';
         const char* pr = getenv("DOFS_PRIO");  // experiment: 1 = graph stage urgent, replay stage least

@@ -919,6 +919,78 @@ __global__ __launch_bounds__(kAggT) void k_dnc_compress(Ws w, int64_t S, int ep)
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// K3 block-start labels (KSeqInit, seq_*): one 1024-thread workgroup per frame sweeps the frame's
+// rank blocks in order. Per block: (1) endpoint labels from the pixel union-find (roots kept in LDS),
+// (2) the block's unions (lock-free; each hooked root recorded once), (3) per resulting root, in an
+// LDS hash: the max rank in the block and the sizes of the roots hooked into it, then one write of
+// its new label, size and the KRT node size. The frames' sweeps are latency-bound and use one CU
+// each; the rest of the chip runs the other stream's replay stage meanwhile.
+// ---------------------------------------------------------------------------------------------
+constexpr int kSeqT = 1024, kSeqHT = 8192, kSeqB = kDeepTop;
+static_assert(2 * kSeqB <= kSeqHT, "hash load factor");
+__global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w) {
+    __shared__ int hk[kSeqHT], hmx[kSeqHT], hsz[kSeqHT];
+    __shared__ int rU[kSeqB], rV[kSeqB];
+    const Dims& d = w.d;
+    const int f = blockIdx.x, tid = threadIdx.x;
+    int* par = w.comp + f * d.N;
+    int* usz = w.uf + f * d.N;
+    int* lab = w.cnt + f * d.N;
+    const int* EU = w.EU + f * d.M;
+    const int* EV = w.EV + f * d.M;
+    int* lu = w.lu + f * d.M;
+    int* lv = w.lv + f * d.M;
+    for (int x = tid; x < kSeqHT; x += kSeqT) {
+        hk[x] = -1;
+        hmx[x] = -1;
+        hsz[x] = 0;
+    }
+    __syncthreads();
+    for (int64_t s = 0; s < d.M; s += kSeqB) {
+        const int cnt = (int)((d.M - s) < kSeqB ? (d.M - s) : kSeqB);
+        for (int t = tid; t < cnt; t += kSeqT) {  // (1) labels at the block start
+            const int u = EU[s + t], v = EV[s + t];
+            const int ru = uf_find(par, u), rv = uf_find(par, v);
+            rU[t] = ru;
+            rV[t] = rv;
+            lu[s + t] = seq_label(lab, ru, u, d.N);
+            lv[s + t] = seq_label(lab, rv, v, d.N);
+        }
+        __syncthreads();
+        for (int t = tid; t < cnt; t += kSeqT) rV[t] = uf_union_hooked(par, rU[t], rV[t]);  // (2)
+        __syncthreads();
+        for (int t = tid; t < cnt; t += kSeqT) {  // (3) aggregate per resulting root
+            const int R = uf_find(par, rU[t]);
+            int slot = (int)(uf_prio(R) & (kSeqHT - 1));
+            for (;;) {
+                int old = -1;
+                __hip_atomic_compare_exchange_strong(hk + slot, &old, R, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (old == -1 || old == R) break;
+                slot = (slot + 1) & (kSeqHT - 1);
+            }
+            atomicMax(hmx + slot, t);
+            const int h = rV[t];
+            if (h >= 0) atomicAdd(hsz + slot, dofs_ld(usz + h));
+        }
+        __syncthreads();
+        for (int x = tid; x < kSeqHT; x += kSeqT) {
+            const int R = hk[x];
+            if (R < 0) continue;
+            const int sz = dofs_ld(usz + R) + hsz[x];
+            const int j = (int)(s + hmx[x]);
+            dofs_st(usz + R, sz);
+            dofs_st(lab + R, j);
+            seq_set_size(w, f, j, sz);
+            hk[x] = -1;
+            hmx[x] = -1;
+            hsz[x] = 0;
+        }
+        __syncthreads();
+    }
+}
+
 struct HipBackend {
     int device = 0;
     hipStream_t own = nullptr;
@@ -1163,6 +1235,12 @@ struct HipBackend {
     }
 
     static constexpr int64_t deep_block() { return kDeepTop; }
+    void krt_seq(const Ws& w) {
+        timed("k_krt_seq", [&] {
+            hipLaunchKernelGGL(k_krt_seq, dim3((unsigned)w.d.B), dim3(kSeqT), 0, stream, w);
+        });
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_krt_seq launch");
+    }
     void dnc_deep(const Ws& w) {
         const unsigned nb = (unsigned)((w.d.M + kDeepTop - 1) / kDeepTop);
         timed("k_dnc_deep", [&] {

@@ -511,6 +511,54 @@ struct KEdgeInit {
     }
 };
 
+// ---------------------------------------------------------------------------------------------
+// K3 block-start labels by one sequential sweep over rank blocks: a pixel
+// union-find holds the forest of all merges before the current block; a block's endpoint labels
+// are read from it (the component's max merge rank, or the pixel itself while it is alone), then
+// the block's merges are united into it and each resulting component records its new max rank and
+// size. Replaces the top-down global depths: one union per merge instead of one per depth.
+// Arrays (per frame, stride N): kpar = parent, ksz = size at roots, klab = max merge rank at roots
+// (-1: a single pixel).
+// ---------------------------------------------------------------------------------------------
+struct KSeqInit {
+    int* kpar;
+    int* ksz;
+    int* klab;
+    int64_t N;
+    DOFS_HD void operator()(int f, int64_t x) const {
+        const int64_t o = f * N + x;
+        kpar[o] = (int)x;
+        ksz[o] = 1;
+        klab[o] = -1;
+    }
+};
+// label of pixel x whose component root is r
+DOFS_HD inline int seq_label(const int* klab, int r, int x, int64_t N) {
+    const int j = dofs_ld((int*)klab + r);
+    return j < 0 ? x : (int)(N + j);
+}
+// union returning the root it hooked (-1: already one component)
+DOFS_HD inline int uf_union_hooked(int* P, int a, int b) {
+    for (;;) {
+        a = uf_find(P, a);
+        b = uf_find(P, b);
+        if (a == b) return -1;
+        if (!uf_above(a, b)) {
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        if (dofs_cas(P + a, a, b) == a) return a;
+    }
+}
+// size of KRT node N + j (label size for the deep kernel: SZ; and the high half of its label word
+// for the global-kernel form of the deep depths)
+DOFS_HD inline void seq_set_size(const Ws& w, int f, int j, int sz) {
+    const int64_t o = f * w.d.NL + w.d.N + j;
+    w.SZ[o] = sz;
+    ((int*)(w.P + o))[1] = sz;
+}
+
 // pointer-jumping word: (ancestor, offset sum) packed
 DOFS_HD inline unsigned long long jump_pack(int anc, int sum) {
     return (unsigned long long)(unsigned)anc | ((unsigned long long)(unsigned)sum << 32);

@@ -55,6 +55,7 @@ struct Pipeline {
     int* pre = nullptr;
     int64_t snap_cap = 4096;
     bool preorder_in_b = false;
+    bool krt_dnc = false;  // DOFS_KRT_DNC=1: block-start labels by the top-down global depths
     int skip_mask = 0;
     int long_path = kLongPath;  // measurement only (DOFS_SKIPMASK): 1 short replay, 2 long replay, 4 lift  // pipeline split: K4 at the end of phase A (default) or start of B
 
@@ -255,11 +256,16 @@ struct Pipeline {
         be.launch(B, M, KEdgeInit{w});
         be.launch(B, NL, KLabelInit{w});
         const int64_t deep = Backend::deep_block();  // levels with block size <= deep run per block
-        for (int64_t S = (int64_t)1 << ceil_log2(M); S > deep; S >>= 1) {
-            const int ep = dnc_epoch(M, S);
-            be.launch(B, M, KDncUnion{w, S, ep});
-            be.dnc_compress(w, S, ep);  // KDncCompress (HIP: workgroup-aggregated atomics)
-            be.launch(B, M, KDncLRootRelabel{w, S, ep});
+        if (krt_dnc) {  // measurement: the top-down global depths (DOFS_KRT_DNC=1)
+            for (int64_t S = (int64_t)1 << ceil_log2(M); S > deep; S >>= 1) {
+                const int ep = dnc_epoch(M, S);
+                be.launch(B, M, KDncUnion{w, S, ep});
+                be.dnc_compress(w, S, ep);  // KDncCompress (HIP: workgroup-aggregated atomics)
+                be.launch(B, M, KDncLRootRelabel{w, S, ep});
+            }
+        } else {  // labels at every deep block's start by one sweep over the blocks in rank order
+            be.launch(B, N, KSeqInit{w.comp, w.uf, w.cnt, N});
+            be.krt_seq(w);
         }
         be.dnc_deep(w);
         be.launch(B, M, KDncParent{w});

@@ -11,6 +11,7 @@
 #include <numeric>
 #include <string>
 #include <type_traits>
+#include <unordered_map>
 #include <vector>
 
 #define DOFS_HD
@@ -98,6 +99,43 @@ struct HostBackend {
             launch(w.d.B, M, KDncUnion{w, S, ep});
             launch(w.d.B, M, KDncCompress{w, S, ep});
             launch(w.d.B, M, KDncLRootRelabel{w, S, ep});
+        }
+    }
+    // block-start labels: the HIP kernel's three phases per block, sequentially
+    void krt_seq(const Ws& w) {
+        const Dims& d = w.d;
+        const int64_t blk = deep_block();
+        std::vector<int> ru((size_t)blk), hooked((size_t)blk);
+        for (int f = 0; f < d.B; ++f) {
+            int* par = w.comp + f * d.N;
+            int* usz = w.uf + f * d.N;
+            int* lab = w.cnt + f * d.N;
+            const int* EU = w.EU + f * d.M;
+            const int* EV = w.EV + f * d.M;
+            for (int64_t s = 0; s < d.M; s += blk) {
+                const int cnt = (int)std::min<int64_t>(blk, d.M - s);
+                for (int t = 0; t < cnt; ++t) {
+                    const int u = EU[s + t], v = EV[s + t];
+                    const int a = uf_find(par, u), b = uf_find(par, v);
+                    w.lu[f * d.M + s + t] = seq_label(lab, a, u, d.N);
+                    w.lv[f * d.M + s + t] = seq_label(lab, b, v, d.N);
+                    ru[t] = a;
+                    hooked[t] = b;
+                }
+                for (int t = 0; t < cnt; ++t) hooked[t] = uf_union_hooked(par, ru[t], hooked[t]);
+                std::unordered_map<int, std::pair<int, int>> agg;  // root -> (max t, hooked sizes)
+                for (int t = 0; t < cnt; ++t) {
+                    auto it = agg.emplace(uf_find(par, ru[t]), std::make_pair(-1, 0)).first;
+                    it->second.first = std::max(it->second.first, t);
+                    if (hooked[t] >= 0) it->second.second += usz[hooked[t]];
+                }
+                for (auto& a : agg) {
+                    const int R = a.first, sz = usz[R] + a.second.second, j = (int)(s + a.second.first);
+                    usz[R] = sz;
+                    lab[R] = j;
+                    seq_set_size(w, f, j, sz);
+                }
+            }
         }
     }
     void boruvka_min(const Ws& w, int r, int pass) {
