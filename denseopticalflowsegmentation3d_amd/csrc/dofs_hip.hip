@@ -927,20 +927,140 @@ __global__ __launch_bounds__(kAggT) void k_dnc_compress(Ws w, int64_t S, int ep)
 // its new label, size and the KRT node size. The frames' sweeps are latency-bound and use one CU
 // each; the rest of the chip runs the other stream's replay stage meanwhile.
 // ---------------------------------------------------------------------------------------------
-constexpr int kSeqT = 1024, kSeqHT = 8192, kSeqB = kDeepTop;
-static_assert(2 * kSeqB <= kSeqHT, "hash load factor");
-__global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w) {
-    __shared__ int hk[kSeqHT], hmx[kSeqHT], hsz[kSeqHT];
-    __shared__ int rU[kSeqB], rV[kSeqB];
+constexpr int kSeqT = 1024, kSeqHT = 8192, kSeqB = kDeepTop, kSeqK = kSeqB / kSeqT;
+static_assert(2 * kSeqB <= kSeqHT && kSeqK * kSeqT == kSeqB, "sweep shape");
+
+// One workgroup owns a frame's union-find: workgroup-scope accesses (plain loads and stores that
+// may stay in the CU's L1 / the XCD's L2; the kernel boundary publishes them to the next kernels)
+__device__ __forceinline__ int wg_ld(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void wg_st(int* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int wg_cas(int* p, int expect, int v) {
+    __hip_atomic_compare_exchange_strong(p, &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+    return expect;
+}
+// union-find finds of K independent chains at once (path halving): each round issues every pending
+// chain's load before waiting, so a thread's K finds cost about one find's latency
+template <int K>
+__device__ __forceinline__ void seq_find(int* par, int (&x)[K], const bool (&act)[K]) {
+    bool pend[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) pend[k] = act[k];
+    for (;;) {
+        int p[K], g[K];
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k) p[k] = pend[k] ? wg_ld(par + x[k]) : 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (pend[k] && p[k] == x[k]) pend[k] = false;
+            any |= pend[k];
+        }
+        if (!any) return;
+#pragma unroll
+        for (int k = 0; k < K; ++k) g[k] = pend[k] ? wg_ld(par + p[k]) : 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (!pend[k]) continue;
+            if (g[k] == p[k]) {
+                x[k] = p[k];
+                pend[k] = false;
+            } else {
+                wg_st(par + x[k], g[k]);
+                x[k] = g[k];
+            }
+        }
+    }
+}
+
+// Union-find node of the sweep: parent, and at roots the component's max merge rank (-1: a single
+// pixel) and size — one 16-byte record, so the find that reaches a root also reads its label and
+// size (one memory request per hop). Kept in the StepIn region of the workspace, which KPathInit
+// fills only after the KRT.
+struct alignas(16) SeqRec {
+    int par, pad, lab, sz;
+};
+struct KSeqInitRec {
+    SeqRec* rec;
+    int64_t NL2;  // records per frame stride (StepIn region: 2 records per StepIn)
+    DOFS_HD void operator()(int f, int64_t x) const {
+        SeqRec r;
+        r.par = (int)x;
+        r.pad = 0;
+        r.lab = -1;
+        r.sz = 1;
+        rec[f * NL2 + x] = r;
+    }
+};
+__device__ __forceinline__ SeqRec rec_ld(const SeqRec* p) { return *p; }
+__device__ __forceinline__ void rec_set_par(SeqRec* p, int v) { wg_st(&p->par, v); }
+
+// finds of K chains at once with path halving: each round issues every pending chain's load first
+template <int K>
+__device__ __forceinline__ void rec_find(SeqRec* rec, int (&x)[K], bool (&pend)[K], SeqRec (&root)[K]) {
+    for (;;) {
+        SeqRec p[K], g[K];
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (pend[k]) p[k] = rec_ld(rec + x[k]);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (pend[k] && p[k].par == x[k]) {
+                root[k] = p[k];
+                pend[k] = false;
+            }
+            any |= pend[k];
+        }
+        if (!any) return;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (pend[k]) g[k] = rec_ld(rec + p[k].par);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (!pend[k]) continue;
+            if (g[k].par == p[k].par) {
+                x[k] = p[k].par;
+                root[k] = g[k];
+                pend[k] = false;
+            } else {
+                rec_set_par(rec + x[k], g[k].par);
+                x[k] = g[k].par;
+            }
+        }
+    }
+}
+
+// Per block of kSeqB merges (four barrier-separated phases):
+//   A  endpoint roots at the block start -> labels (lu, lv)
+//   B  the block's unions: one CAS per merge (parents always point to lower hash priority, so a
+//      root may be hooked onto any node of lower priority without forming a cycle)
+//   C  each merge's resulting root R, aggregated per R in LDS: max rank in the block, sizes of the
+//      roots hooked into it, R's old size; the endpoints are compressed onto R
+//   D  per R: its new label and size (one 8-byte store) and the KRT node size SZ
+__global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w, unsigned long long* stamps) {
+    // diagnostic (DOFS_SEQ_STAMP=1): shader cycles per phase, summed over the blocks, workgroup 0
+    unsigned long long t0 = stamps ? __builtin_amdgcn_s_memtime() : 0, acc[4] = {0, 0, 0, 0};
+    auto stamp = [&](int ph) {
+        if (!stamps || blockIdx.x != 0 || threadIdx.x != 0) return;
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        acc[ph] += t1 - t0;
+        t0 = t1;
+    };
+    constexpr int K = kSeqK, K2 = 2 * kSeqK, KS = kSeqHT / kSeqT;
+    __shared__ int hk[kSeqHT], hmx[kSeqHT], hsz[kSeqHT], hold[kSeqHT];
     const Dims& d = w.d;
     const int f = blockIdx.x, tid = threadIdx.x;
-    int* par = w.comp + f * d.N;
-    int* usz = w.uf + f * d.N;
-    int* lab = w.cnt + f * d.N;
+    SeqRec* rec = reinterpret_cast<SeqRec*>(w.In + f * d.NL);
     const int* EU = w.EU + f * d.M;
     const int* EV = w.EV + f * d.M;
     int* lu = w.lu + f * d.M;
     int* lv = w.lv + f * d.M;
+    int* SZ = w.SZ + f * d.NL + d.N;
     for (int x = tid; x < kSeqHT; x += kSeqT) {
         hk[x] = -1;
         hmx[x] = -1;
@@ -949,46 +1069,126 @@ __global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w) {
     __syncthreads();
     for (int64_t s = 0; s < d.M; s += kSeqB) {
         const int cnt = (int)((d.M - s) < kSeqB ? (d.M - s) : kSeqB);
-        for (int t = tid; t < cnt; t += kSeqT) {  // (1) labels at the block start
-            const int u = EU[s + t], v = EV[s + t];
-            const int ru = uf_find(par, u), rv = uf_find(par, v);
-            rU[t] = ru;
-            rV[t] = rv;
-            lu[s + t] = seq_label(lab, ru, u, d.N);
-            lv[s + t] = seq_label(lab, rv, v, d.N);
+        // ---- A
+        int e[K2], c[K2];
+        bool act2[K2], pend[K2];
+        SeqRec rt[K2];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int t = tid + k * kSeqT;
+            act2[2 * k] = act2[2 * k + 1] = t < cnt;
+            e[2 * k] = t < cnt ? EU[s + t] : 0;
+            e[2 * k + 1] = t < cnt ? EV[s + t] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < K2; ++k) {
+            c[k] = e[k];
+            pend[k] = act2[k];
+        }
+        rec_find<K2>(rec, c, pend, rt);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (!act2[2 * k]) continue;
+            const int t = tid + k * kSeqT;
+            lu[s + t] = rt[2 * k].lab < 0 ? e[2 * k] : (int)(d.N + rt[2 * k].lab);
+            lv[s + t] = rt[2 * k + 1].lab < 0 ? e[2 * k + 1] : (int)(d.N + rt[2 * k + 1].lab);
         }
         __syncthreads();
-        for (int t = tid; t < cnt; t += kSeqT) rV[t] = uf_union_hooked(par, rU[t], rV[t]);  // (2)
-        __syncthreads();
-        for (int t = tid; t < cnt; t += kSeqT) {  // (3) aggregate per resulting root
-            const int R = uf_find(par, rU[t]);
-            int slot = (int)(uf_prio(R) & (kSeqHT - 1));
-            for (;;) {
-                int old = -1;
-                __hip_atomic_compare_exchange_strong(hk + slot, &old, R, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (old == -1 || old == R) break;
-                slot = (slot + 1) & (kSeqHT - 1);
+        stamp(0);
+        // ---- B
+        int hooked_sz[K];
+        {
+            int x[K2];
+            bool pu[K2], todo[K];
+#pragma unroll
+            for (int k = 0; k < K2; ++k) {
+                x[k] = c[k];
+                pu[k] = false;
             }
-            atomicMax(hmx + slot, t);
-            const int h = rV[t];
-            if (h >= 0) atomicAdd(hsz + slot, dofs_ld(usz + h));
+            SeqRec r2[K2];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                todo[k] = act2[2 * k];
+                hooked_sz[k] = 0;
+                r2[2 * k] = rt[2 * k];
+                r2[2 * k + 1] = rt[2 * k + 1];
+            }
+            for (;;) {
+                bool any = false;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    if (!todo[k]) continue;
+                    int a = x[2 * k], b = x[2 * k + 1], sa = r2[2 * k].sz;
+                    if (!uf_above(a, b)) {
+                        a = x[2 * k + 1];
+                        b = x[2 * k];
+                        sa = r2[2 * k + 1].sz;
+                    }
+                    if (wg_cas(&rec[a].par, a, b) == a) {
+                        hooked_sz[k] = sa;
+                        todo[k] = false;
+                    } else {  // a was hooked meanwhile: find both roots again
+                        pu[2 * k] = pu[2 * k + 1] = true;
+                        any = true;
+                    }
+                }
+                if (!any) break;
+                rec_find<K2>(rec, x, pu, r2);
+            }
         }
         __syncthreads();
-        for (int x = tid; x < kSeqHT; x += kSeqT) {
+        stamp(1);
+        // ---- C
+        {
+            int R[K];
+            bool pr[K];
+            SeqRec rr[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                R[k] = c[2 * k];
+                pr[k] = act2[2 * k];
+            }
+            rec_find<K>(rec, R, pr, rr);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (!act2[2 * k]) continue;
+                int slot = (int)(uf_prio(R[k]) & (kSeqHT - 1));
+                for (;;) {
+                    int o = -1;
+                    __hip_atomic_compare_exchange_strong(hk + slot, &o, R[k], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (o == -1 || o == R[k]) break;
+                    slot = (slot + 1) & (kSeqHT - 1);
+                }
+                atomicMax(hmx + slot, tid + k * kSeqT);
+                atomicAdd(hsz + slot, hooked_sz[k]);
+                hold[slot] = rr[k].sz;  // R's size at the block start (same value from every inserter)
+                if (e[2 * k] != R[k]) rec_set_par(rec + e[2 * k], R[k]);
+                if (e[2 * k + 1] != R[k]) rec_set_par(rec + e[2 * k + 1], R[k]);
+            }
+        }
+        __syncthreads();
+        stamp(2);
+        // ---- D
+#pragma unroll
+        for (int q = 0; q < KS; ++q) {
+            const int x = tid + q * kSeqT;
             const int R = hk[x];
             if (R < 0) continue;
-            const int sz = dofs_ld(usz + R) + hsz[x];
+            const int sz = hold[x] + hsz[x];
             const int j = (int)(s + hmx[x]);
-            dofs_st(usz + R, sz);
-            dofs_st(lab + R, j);
-            seq_set_size(w, f, j, sz);
+            int2* lz = reinterpret_cast<int2*>(&rec[R].lab);
+            *lz = make_int2(j, sz);
+            SZ[j] = sz;
             hk[x] = -1;
             hmx[x] = -1;
             hsz[x] = 0;
         }
         __syncthreads();
+        stamp(3);
     }
+    if (stamps && blockIdx.x == 0 && threadIdx.x == 0)
+        for (int k = 0; k < 4; ++k) stamps[k] += acc[k];
 }
 
 struct HipBackend {
@@ -1020,6 +1220,14 @@ struct HipBackend {
         stream = own;
     }
     ~HipBackend() {
+        if (stamps_) {
+            unsigned long long h[8];
+            (void)hipDeviceSynchronize();
+            (void)hipMemcpy(h, stamps_, sizeof(h), hipMemcpyDeviceToHost);
+            fprintf(stderr, "k_krt_seq cycles per phase (workgroup 0, all launches): %llu %llu %llu %llu\n", h[0], h[1],
+                    h[2], h[3]);
+            (void)hipFree(stamps_);
+        }
         for (auto e : pool) (void)hipEventDestroy(e);
         for (auto e : events) (void)hipEventDestroy(e);
         for (auto& t : tmps)
@@ -1235,9 +1443,22 @@ struct HipBackend {
     }
 
     static constexpr int64_t deep_block() { return kDeepTop; }
+    unsigned long long* stamps_ = nullptr;
+    unsigned long long* seq_stamps() {
+        static const bool on = [] {
+            const char* e = getenv("DOFS_SEQ_STAMP");
+            return e && e[0] == '1';
+        }();
+        if (on && !stamps_) {
+            note(hipMalloc(&stamps_, 64), "hipMalloc");
+            note(hipMemset(stamps_, 0, 64), "hipMemset");
+        }
+        return stamps_;
+    }
     void krt_seq(const Ws& w) {
+        launch(w.d.B, w.d.N, KSeqInitRec{reinterpret_cast<SeqRec*>(w.In), 2 * w.d.NL});
         timed("k_krt_seq", [&] {
-            hipLaunchKernelGGL(k_krt_seq, dim3((unsigned)w.d.B), dim3(kSeqT), 0, stream, w);
+            hipLaunchKernelGGL(k_krt_seq, dim3((unsigned)w.d.B), dim3(kSeqT), 0, stream, w, seq_stamps());
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_krt_seq launch");
     }

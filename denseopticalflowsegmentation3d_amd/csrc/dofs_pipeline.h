@@ -264,7 +264,6 @@ struct Pipeline {
                 be.launch(B, M, KDncLRootRelabel{w, S, ep});
             }
         } else {  // labels at every deep block's start by one sweep over the blocks in rank order
-            be.launch(B, N, KSeqInit{w.comp, w.uf, w.cnt, N});
             be.krt_seq(w);
         }
         be.dnc_deep(w);

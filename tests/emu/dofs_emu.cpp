@@ -106,6 +106,7 @@ struct HostBackend {
         const Dims& d = w.d;
         const int64_t blk = deep_block();
         std::vector<int> ru((size_t)blk), hooked((size_t)blk);
+        launch(d.B, d.N, KSeqInit{w.comp, w.uf, w.cnt, d.N});
         for (int f = 0; f < d.B; ++f) {
             int* par = w.comp + f * d.N;
             int* usz = w.uf + f * d.N;
