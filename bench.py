@@ -32,10 +32,24 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 GATHER_PER_FRAME = 64  # box records per frame in the gathered block
 DEEP_BLOCK = int(os.environ.get("DOFS_DEEP_S", "4096"))  # KRT depths with block size <= this run in LDS (k_dnc_deep), the rest globally
 
-# Algorithmic (compulsory) bytes per active lane of the probed kernels:
-# KDncCompress, per L edge of a depth: own label (4 B read), its parent (4 B read), its size
-# (4 B read), component size CS += (4 B read + 4 B write), max L rank MX (4 B read + 4 B write).
-KERNEL_BYTES = {"KDncCompress": 28, "k_dnc_compress": 28}
+# Algorithmic (compulsory) bytes of the probed kernels:
+#   k_boruvka_min (per pixel of a frame still active in that Borůvka pass): its component label (4 B)
+#     and its blurred flow vector (8 B), each read once; neighbours' words are other pixels' own
+#     reads; the per-component minima are LDS-aggregated per tile (not counted).
+#   k_dnc_compress (DOFS_KRT_DNC=1 only), per L edge of a depth: own label 4 B, parent 4 B, size 4 B,
+#     component size RMW 8 B, max rank RMW 8 B.
+KERNEL_BYTES = {"k_boruvka_min": 12, "KDncCompress": 28, "k_dnc_compress": 28}
+ROOF_KERNEL = "k_boruvka_min"
+ROUND_FLAG = 16  # counters: C_ACT + r = Borůvka round r found a cross-component edge
+
+
+def boruvka_min_units(counters, N):
+    """Pixels processed per batch by k_boruvka_min: round r >= 1 runs pass 0 for frames whose round
+    r - 1 found an edge and pass 1 for frames whose round r found one (dofs_pipeline.h boruvka())."""
+    R = min(ceil_log2(N) + 2, 40 - 1)
+    act = counters[:, ROUND_FLAG:ROUND_FLAG + R] != 0
+    frames_launches = int(act[:, 0:R - 1].sum() + act[:, 1:R].sum())
+    return frames_launches * N, 2 * (R - 1)
 
 
 def ceil_log2(n):
@@ -69,8 +83,9 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--cpu-frames", type=int, default=1, help="frames of the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-stages", action="store_true", help="skip the per-stage event timing pass")
-    ap.add_argument("--probe", default="k_dnc_compress", help="kernel timed with device events for the roofline")
-    ap.add_argument("--pmc", default=None, help="PMC summary JSON (tools/pmc_summary.py) for roofline.traffic")
+    ap.add_argument("--probe", default=ROOF_KERNEL, help="kernel timed with device events for the roofline")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01", "pmc_summary.json"),
+                    help="PMC summary JSON (tools/pmc_summary.py) for roofline.traffic")
     return ap.parse_args()
 
 
@@ -166,10 +181,14 @@ def main():
         probe = {"kernel": a.probe, "ms_per_batch": round(probe_ms / a.steps, 3),
                  "launches_per_batch": probe_n / a.steps}
     elif probe_n:
-        per_launch = [n * B * KERNEL_BYTES[a.probe] for n in dnc_L_edges(N - 1)] if a.probe in KERNEL_BYTES else []
-        launches_per_batch = len(per_launch)
+        if a.probe == "k_boruvka_min":
+            units, launches_per_batch = boruvka_min_units(ctx.batch_counters(B), N)
+            alg_batch = units * KERNEL_BYTES[a.probe]
+        else:
+            per_launch = [n * B * KERNEL_BYTES[a.probe] for n in dnc_L_edges(N - 1)]
+            launches_per_batch, alg_batch = len(per_launch), sum(per_launch)
         assert launches_per_batch and probe_n == launches_per_batch * a.steps, (probe_n, launches_per_batch)
-        alg = sum(per_launch) * a.steps
+        alg = alg_batch * a.steps
         achieved = alg / (probe_ms / 1e3) / 1e9
         traffic = None
         if a.pmc and os.path.exists(a.pmc):
@@ -179,7 +198,7 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                 "kernel": a.probe, "launches": probe_n, "avg_launch_us": round(probe_ms / probe_n * 1e3, 2),
-                "alg_bytes_per_launch": round(alg / probe_n), "alg_bytes_per_lane": KERNEL_BYTES[a.probe],
+                "alg_bytes_per_launch": round(alg / probe_n), "alg_bytes_per_unit": KERNEL_BYTES[a.probe],
                 "path_input_roofline_frac": None}
 
     # per-stage device-event timing of extra profiled batches (not part of the timed region)

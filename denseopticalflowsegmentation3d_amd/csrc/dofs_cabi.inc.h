@@ -110,6 +110,18 @@ int32_t dofs_batch_records_copy_id(dofs_ctx* ctx, int64_t batch, void* d_dst, in
     return dofs::api_records_copy(ctx, batch, d_dst, per_frame, stream);
 }
 
+int32_t dofs_batch_counters(dofs_ctx* ctx, int32_t* out, int64_t capacity) {
+    if (!ctx || !out || !ctx->have_batch()) return DOFS_ERR_INVALID_ARG;
+    const int slot = ctx->last_slot();
+    const int64_t n = (int64_t)ctx->meta[slot].B * dofs::kCounters;
+    if (capacity < n) return DOFS_ERR_CAPACITY;
+    ctx->be.use_own();
+    ctx->join(ctx->nbatch - 1);
+    ctx->be.d2h(out, ctx->pipe(slot).w.ctr, sizeof(int32_t) * (size_t)n);
+    ctx->be.sync();
+    return ctx->check();
+}
+
 int64_t dofs_batch_count(dofs_ctx* ctx) { return ctx ? ctx->nbatch : -1; }
 
 int32_t dofs_batch_slots(dofs_ctx* ctx) { return ctx ? ctx->nslots : -1; }

@@ -1472,7 +1472,7 @@ struct HipBackend {
     void boruvka_min(const Ws& w, int r, int pass) {
         const int64_t tiles = (int64_t)((w.d.W + kTileX - 1) / kTileX) * ((w.d.H + kTileY - 1) / kTileY);
         const int64_t gx = std::min<int64_t>(tiles, std::max<int64_t>(1, grid_cap() / w.d.B));
-        timed(pass ? "k_boruvka_min_i" : "k_boruvka_min_w", [&] {
+        timed("k_boruvka_min", [&] {
             hipLaunchKernelGGL(k_boruvka_min, dim3((unsigned)gx, (unsigned)w.d.B), dim3(256), 0, stream, w, r, pass);
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_boruvka_min launch");

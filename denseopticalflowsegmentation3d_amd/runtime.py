@@ -67,6 +67,8 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_batch_records_copy.restype = C.c_int32
     L.dofs_batch_records_copy_id.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p]
     L.dofs_batch_records_copy_id.restype = C.c_int32
+    L.dofs_batch_counters.argtypes = [C.c_void_p, _ip, C.c_int64]
+    L.dofs_batch_counters.restype = C.c_int32
     L.dofs_batch_count.argtypes = [C.c_void_p]
     L.dofs_batch_count.restype = C.c_int64
     L.dofs_batch_slots.argtypes = [C.c_void_p]
@@ -271,6 +273,12 @@ class Dofs:
             rc = self.lib.dofs_batch_records_copy_id(self.ctx, batch, C.c_void_p(d_dst), per_frame,
                                                      C.c_void_p(stream or 0))
         self._err(rc, "dofs_batch_records_copy")
+
+    def batch_counters(self, B: int) -> np.ndarray:
+        """The last batch's per-frame counter blocks (B x 64 int32; Borůvka round flags at 16 + r)."""
+        out = np.zeros((B, 64), np.int32)
+        self._err(self.lib.dofs_batch_counters(self.ctx, _p(out, C.c_int32), out.size), "dofs_batch_counters")
+        return out
 
     def batch_count(self) -> int:
         return int(self.lib.dofs_batch_count(self.ctx))

@@ -206,6 +206,11 @@ int64_t dofs_batch_count(dofs_ctx* ctx);
  * results after submitting batch k + slots - 1 keeps every stage of the pipeline busy). */
 int32_t dofs_batch_slots(dofs_ctx* ctx);
 
+/* The last batch's per-frame counter blocks (B x 64 int32: candidates, snapshots, MST edges, ... and
+ * at 16 + r the flag "Borůvka round r found a cross-component edge"), copied to host; waits for the
+ * batch. Diagnostics and the bench's roofline model. capacity = ints available at out. */
+int32_t dofs_batch_counters(dofs_ctx* ctx, int32_t* out, int64_t capacity);
+
 /* Stage timing with device events (0 = off). Stages: 0 blur, 1 MST (Borůvka), 2 MST sort, 3 KRT,
  * 4 preorder, 5 replay, 6 lift + slots, 7 labels. dofs_profile_read returns the accumulated
  * milliseconds per stage and the number of profiled batches, then resets. */
