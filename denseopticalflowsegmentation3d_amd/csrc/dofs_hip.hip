@@ -766,10 +766,12 @@ __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
 // pass 0: minimum weight bits; pass 1: minimum emission index among the edges of that weight.
 // ---------------------------------------------------------------------------------------------
 constexpr int kTileX = 32, kTileY = 8, kMinHT = 512;
-__global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass) {
+// Tiles whose pixels have no cross-component edge left are done for good (components only merge):
+// pass 0 marks them in `tdone` (per frame and tile) and later passes skip them.
+__global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass, unsigned char* tdone) {
     __shared__ int hk[kMinHT];
     __shared__ unsigned long long hv[kMinHT];
-    __shared__ int any;
+    __shared__ int any, tany;
     const Dims& d = w.d;
     const int f = blockIdx.y;
     if (pass == 0 ? (r > 0 && !w.C(f)[C_ACT + r - 1]) : !w.C(f)[C_ACT + r]) return;
@@ -784,7 +786,8 @@ __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass) {
         hk[x] = -1;
         hv[x] = ~0ull;
     }
-    if (tid == 0) any = 0;
+    if (tid == 0) any = tany = 0;
+    unsigned char* td = tdone + (int64_t)f * tiles;
     __syncthreads();
     auto put = [&](int key, unsigned long long v) {
         int slot = (int)(uf_prio(key) & (kMinHT - 1));
@@ -798,6 +801,7 @@ __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass) {
         atomicMin(hv + slot, v);
     };
     for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
+        if (td[t]) continue;  // block-uniform
         const int x = (t % tiles_x) * kTileX + (tid % kTileX), y = (t / tiles_x) * kTileY + tid / kTileX;
         int cp = -1;
         unsigned long long own_best = ~0ull;  // this pixel's candidates for its own component,
@@ -823,7 +827,7 @@ __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass) {
                     if (wb == bw[cq]) put(cq, idx);
                 }
             }
-            if (mine && pass == 0) any = 1;
+            if (mine && pass == 0) any = tany = 1;
         }
         {  // the lanes of a wave mostly share the component (a tile row of a contiguous region): one
            // put for the first such lane's component, reduced across the lanes that share it
@@ -843,6 +847,10 @@ __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass) {
             }
         }
         __syncthreads();
+        if (pass == 0 && tid == 0) {
+            if (!tany) td[t] = 1;
+            tany = 0;
+        }
         for (int x = tid; x < kMinHT; x += 256) {
             const int key = hk[x];
             if (key < 0) continue;
@@ -1035,6 +1043,10 @@ __device__ __forceinline__ void rec_find(SeqRec* rec, int (&x)[K], bool (&pend)[
     }
 }
 
+#ifndef DOFS_SEQ_COMPRESS
+#define DOFS_SEQ_COMPRESS 0  // measured: the two endpoint stores cost more than the hops they save
+#endif
+__device__ __forceinline__ constexpr bool seq_compress() { return DOFS_SEQ_COMPRESS != 0; }
 // Per block of kSeqB merges (four barrier-separated phases):
 //   A  endpoint roots at the block start -> labels (lu, lv)
 //   B  the block's unions: one CAS per merge (parents always point to lower hash priority, so a
@@ -1163,8 +1175,10 @@ __global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w, unsigned long long* sta
                 atomicMax(hmx + slot, tid + k * kSeqT);
                 atomicAdd(hsz + slot, hooked_sz[k]);
                 hold[slot] = rr[k].sz;  // R's size at the block start (same value from every inserter)
-                if (e[2 * k] != R[k]) rec_set_par(rec + e[2 * k], R[k]);
-                if (e[2 * k + 1] != R[k]) rec_set_par(rec + e[2 * k + 1], R[k]);
+                if (seq_compress()) {
+                    if (e[2 * k] != R[k]) rec_set_par(rec + e[2 * k], R[k]);
+                    if (e[2 * k + 1] != R[k]) rec_set_par(rec + e[2 * k + 1], R[k]);
+                }
             }
         }
         __syncthreads();
@@ -1189,6 +1203,71 @@ __global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w, unsigned long long* sta
     }
     if (stamps && blockIdx.x == 0 && threadIdx.x == 0)
         for (int k = 0; k < 4; ++k) stamps[k] += acc[k];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Borůvka per-pixel passes, four pixels per lane (one 16-byte label load): KBoruvkaHook and
+// KBoruvkaRelabelFind of dofs_kernels.h. A frame's unaligned head and tail (H*W % 4 != 0) run
+// one pixel per lane.
+// ---------------------------------------------------------------------------------------------
+struct Span4 {  // [0, head) scalar, [head, head + 4 n4) as int4, [tail, N) scalar
+    int64_t head, n4, tail;
+};
+__device__ __forceinline__ Span4 span4(const int* frame, int64_t N) {
+    Span4 sp;
+    const int64_t mis = (int64_t)(((uintptr_t)frame >> 2) & 3);
+    sp.head = mis ? 4 - mis : 0;
+    if (sp.head > N) sp.head = N;
+    sp.n4 = (N - sp.head) / 4;
+    sp.tail = sp.head + 4 * sp.n4;
+    return sp;
+}
+__global__ __launch_bounds__(256) void k_boruvka_hook4(Ws w, int r) {
+    const int f = blockIdx.y;
+    if (!w.C(f)[C_ACT + r]) return;
+    const int64_t N = w.d.N;
+    const int* comp = w.comp + f * N;
+    const Span4 sp = span4(comp, N);
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = i0; i < sp.n4; i += step) {
+        const int64_t c = sp.head + 4 * i;
+        const int4 v = *reinterpret_cast<const int4*>(comp + c);
+        if (v.x == (int)c) boruvka_hook_root(w, f, c);
+        if (v.y == (int)(c + 1)) boruvka_hook_root(w, f, c + 1);
+        if (v.z == (int)(c + 2)) boruvka_hook_root(w, f, c + 2);
+        if (v.w == (int)(c + 3)) boruvka_hook_root(w, f, c + 3);
+    }
+    if (i0 < sp.head + (N - sp.tail)) {
+        const int64_t c = i0 < sp.head ? i0 : sp.tail + (i0 - sp.head);
+        if (comp[c] == (int)c) boruvka_hook_root(w, f, c);
+    }
+}
+__global__ __launch_bounds__(256) void k_boruvka_relabel4(Ws w, int r) {
+    const int f = blockIdx.y;
+    if (!w.C(f)[C_ACT + r]) return;
+    const int64_t N = w.d.N;
+    int* comp = w.comp + f * N;
+    int* uf = w.uf + f * N;
+    const Span4 sp = span4(comp, N);
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = i0; i < sp.n4; i += step) {
+        int4* p4 = reinterpret_cast<int4*>(comp + sp.head + 4 * i);
+        const int4 v = *p4;
+        int4 o;
+        o.x = uf_find(uf, v.x);
+        o.y = v.y == v.x ? o.x : uf_find(uf, v.y);
+        o.z = v.z == v.y ? o.y : uf_find(uf, v.z);
+        o.w = v.w == v.z ? o.z : uf_find(uf, v.w);
+        if (o.x != v.x || o.y != v.y || o.z != v.z || o.w != v.w) *p4 = o;
+    }
+    if (i0 < sp.head + (N - sp.tail)) {
+        const int64_t p = i0 < sp.head ? i0 : sp.tail + (i0 - sp.head);
+        const int c = comp[p];
+        const int root = uf_find(uf, c);
+        if (root != c) comp[p] = root;
+    }
 }
 
 struct HipBackend {
@@ -1469,11 +1548,26 @@ struct HipBackend {
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_dnc_deep launch");
     }
+    void boruvka_hook(const Ws& w, int r) { pixel4(w, r, k_boruvka_hook4, "KBoruvkaHook"); }
+    void boruvka_relabel(const Ws& w, int r) { pixel4(w, r, k_boruvka_relabel4, "KBoruvkaRelabelFind"); }
+    void pixel4(const Ws& w, int r, void (*k)(Ws, int), const char* name) {
+        const int64_t n4 = (w.d.N + 3) / 4;
+        int64_t gx = (n4 + 255) / 256;
+        const int64_t cap = std::max<int64_t>(1, grid_cap() / w.d.B);
+        if (gx > cap) gx = cap;
+        if (gx < 1) gx = 1;
+        timed(name, [&] { hipLaunchKernelGGL(k, dim3((unsigned)gx, (unsigned)w.d.B), dim3(256), 0, stream, w, r); });
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, name);
+    }
     void boruvka_min(const Ws& w, int r, int pass) {
         const int64_t tiles = (int64_t)((w.d.W + kTileX - 1) / kTileX) * ((w.d.H + kTileY - 1) / kTileY);
         const int64_t gx = std::min<int64_t>(tiles, std::max<int64_t>(1, grid_cap() / w.d.B));
+        unsigned char* tdone = w.hlB;  // free during the MST (KDncParent fills it after the KRT)
+        static_assert(sizeof(*w.hlB) == 1, "tile flags are bytes");
+        if (r == 1 && pass == 0) memset(tdone, 0, (size_t)tiles * w.d.B);  // tiles <= M per frame
         timed("k_boruvka_min", [&] {
-            hipLaunchKernelGGL(k_boruvka_min, dim3((unsigned)gx, (unsigned)w.d.B), dim3(256), 0, stream, w, r, pass);
+            hipLaunchKernelGGL(k_boruvka_min, dim3((unsigned)gx, (unsigned)w.d.B), dim3(256), 0, stream, w, r, pass,
+                               tdone);
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_boruvka_min launch");
     }

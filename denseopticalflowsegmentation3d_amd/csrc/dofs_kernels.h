@@ -61,7 +61,7 @@ struct Ws {
     unsigned long long* bw;
     unsigned* bi;
     int* uf;
-    int* mstbits;
+    int* mstbits;  // per pixel: byte k != 0 <=> its emitted edge k is an MST edge (plain byte stores)
     int* cnt;
     int* off;
     // MST edges (stride M)
@@ -351,7 +351,7 @@ struct KBoruvkaFirst {
     }
 };
 
-struct KBoruvkaReset {  // round r: clear per-component minima
+struct KBoruvkaReset {  // clear the per-component minima (measurement / fallback path; Hook clears them)
     Ws w;
     int r;
     DOFS_HD void operator()(int f, int64_t c) const {
@@ -413,21 +413,28 @@ struct KBoruvkaMinI {
     }
 };
 
-struct KBoruvkaHook {  // every component root hooks along its minimum edge
+// root c hooks along its minimum edge and clears its minima: the next round's minima of a root start
+// from "none" (every root of round r + 1 is a root of round r, and only roots are keys of the minima)
+DOFS_HD inline void boruvka_hook_root(const Ws& w, int f, int64_t c) {
+    const Dims& d = w.d;
+    const int* comp = w.comp + f * d.N;
+    const int64_t o = f * d.N + c;
+    const unsigned idx = w.bi[o];
+    w.bw[o] = ~0ull;
+    w.bi[o] = kNoEdge;
+    if (idx == kNoEdge) return;
+    const int64_t p = idx >> 2;
+    const int k = idx & 3;
+    const int64_t q = edge_end(d, p, k);
+    reinterpret_cast<unsigned char*>(w.mstbits + f * d.N + p)[k] = 1;  // no atomic: one byte per edge
+    uf_union(w.uf + f * d.N, comp[p], comp[q]);
+}
+struct KBoruvkaHook {  // every component root (HIP: k_boruvka_hook4, four pixels per lane)
     Ws w;
     int r;
     DOFS_HD void operator()(int f, int64_t c) const {
         if (!w.C(f)[C_ACT + r]) return;
-        const Dims& d = w.d;
-        const int* comp = w.comp + f * d.N;
-        if (comp[c] != (int)c) return;
-        const unsigned idx = w.bi[f * d.N + c];
-        if (idx == kNoEdge) return;
-        const int64_t p = idx >> 2;
-        const int k = idx & 3;
-        const int64_t q = edge_end(d, p, k);
-        dofs_aor(w.mstbits + f * d.N + p, 1 << k);
-        uf_union(w.uf + f * d.N, comp[p], comp[q]);
+        if (w.comp[f * w.d.N + c] == (int)c) boruvka_hook_root(w, f, c);
     }
 };
 
@@ -449,6 +456,18 @@ struct KBoruvkaCompress {  // uf[c] = root
     }
 };
 
+struct KBoruvkaRelabelFind {  // comp[p] = the root of its component (finds with path halving)
+    Ws w;
+    int r;
+    DOFS_HD void operator()(int f, int64_t p) const {
+        if (!w.C(f)[C_ACT + r]) return;
+        int* comp = w.comp + f * w.d.N;
+        const int c = comp[p];
+        const int root = uf_find(w.uf + f * w.d.N, c);
+        if (root != c) comp[p] = root;
+    }
+};
+
 struct KBoruvkaRelabel {
     Ws w;
     int r;
@@ -462,16 +481,22 @@ struct KBoruvkaRelabel {
 // ---------------------------------------------------------------------------------------------
 // MST edge list in emission order, then (after the radix sort) in Kruskal order.
 // ---------------------------------------------------------------------------------------------
+// the four edge bytes of a pixel's MST word as bits 0..3
+DOFS_HD inline unsigned mst_bits(int word) {
+    const unsigned v = (unsigned)word;
+    return (v & 1u) | ((v >> 7) & 2u) | ((v >> 14) & 4u) | ((v >> 21) & 8u);
+}
+
 struct KMaskOut {  // a band's minimum spanning forest as per-pixel emitted-edge bits
     Ws w;
     unsigned char* mask;
-    DOFS_HD void operator()(int, int64_t p) const { mask[p] = (unsigned char)w.mstbits[p]; }
+    DOFS_HD void operator()(int, int64_t p) const { mask[p] = (unsigned char)mst_bits(w.mstbits[p]); }
 };
 
 struct KMstCount {
     Ws w;
     DOFS_HD void operator()(int f, int64_t p) const {
-        w.cnt[f * w.d.N + p] = __builtin_popcount((unsigned)w.mstbits[f * w.d.N + p]);
+        w.cnt[f * w.d.N + p] = __builtin_popcount(mst_bits(w.mstbits[f * w.d.N + p]));
     }
 };
 
@@ -479,7 +504,7 @@ struct KMstEmit {
     Ws w;
     DOFS_HD void operator()(int f, int64_t p) const {
         const Dims& d = w.d;
-        const int bits = w.mstbits[f * d.N + p];
+        const int bits = (int)mst_bits(w.mstbits[f * d.N + p]);
         if (!bits) return;
         int64_t j = w.off[f * d.N + p];
         const F2* b = w.blur + f * d.N;

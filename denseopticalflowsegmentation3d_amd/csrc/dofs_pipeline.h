@@ -188,13 +188,11 @@ struct Pipeline {
             if (r == 0) {
                 be.launch(B, N, KBoruvkaFirst{w});
             } else {
-                be.launch(B, N, KBoruvkaReset{w, r});
                 be.boruvka_min(w, r, 0);  // KBoruvkaMinW (HIP: workgroup-aggregated per tile)
                 be.boruvka_min(w, r, 1);  // KBoruvkaMinI
             }
-            be.launch(B, N, KBoruvkaHook{w, r});
-            be.launch(B, N, KBoruvkaCompress{w, r});
-            be.launch(B, N, KBoruvkaRelabel{w, r});
+            be.boruvka_hook(w, r);  // KBoruvkaHook (also clears the roots' minima for round r + 1)
+            be.boruvka_relabel(w, r);  // KBoruvkaRelabelFind
         }
     }
 

@@ -139,6 +139,8 @@ struct HostBackend {
             }
         }
     }
+    void boruvka_hook(const Ws& w, int r) { launch(w.d.B, w.d.N, KBoruvkaHook{w, r}); }
+    void boruvka_relabel(const Ws& w, int r) { launch(w.d.B, w.d.N, KBoruvkaRelabelFind{w, r}); }
     void boruvka_min(const Ws& w, int r, int pass) {
         if (pass == 0)
             launch(w.d.B, w.d.N, KBoruvkaMinW{w, r});
