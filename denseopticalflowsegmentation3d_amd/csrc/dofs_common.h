@@ -59,6 +59,7 @@ enum Counter {
     C_MST = 5,
     C_SHORT = 6,
     C_LONG = 7,
+    C_SQ = 8,  // C_SQ + (r & 1): short paths parked in replay round r (ping-pong lists)
     C_ACT = 16  // C_ACT + r: Borůvka round r found a cross-component edge
 };
 

@@ -190,6 +190,22 @@ __global__ __launch_bounds__(kBlock) void k_generic_take(F f, int64_t n) {
         f(fr, i, i < n, t);
     }
 }
+// list launch: elements [0, min(n, frame counter cidx)) — the bound is read on the device, so a
+// shrinking list costs only the blocks it needs (the others exit at once)
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_counted_take(F f, int64_t n, int cidx) {
+    __shared__ int wsum[kBlock / 64];
+    __shared__ int base;
+    BlockTaker t{wsum, &base};
+    const int fr = blockIdx.y;
+    const int64_t c = f.w.C(fr)[cidx];
+    const int64_t m = c < n ? c : n;
+    const int64_t step = (int64_t)gridDim.x * kBlock;
+    for (int64_t i0 = (int64_t)blockIdx.x * kBlock; i0 < m; i0 += step) {
+        const int64_t i = i0 + threadIdx.x;
+        f(fr, i, i < m, t);
+    }
+}
 template <class F, class = void>
 struct takes : std::false_type {};
 template <class F>
@@ -744,7 +760,84 @@ __device__ void top_level(const Ws& w, TopShared& sh, int f, int64_t s0, int cnt
     __syncthreads();
 }
 
-constexpr size_t kDeepSmem = sizeof(DeepShared) > sizeof(TopShared) ? sizeof(DeepShared) : sizeof(TopShared);
+// Epilogue of a block (KDncParent's work, plus block-local pointer jumping): the block's final labels
+// are its merges' KRT children. Each merge splits them into heavy (larger subtree; ties -> A) and
+// light, records the light side (hlB) and the path-top flags (lite), and seeds the heavy-first
+// preorder's pointer-jumping words: a child's word = (parent, 1) if heavy, (parent, 2 size(heavy))
+// if light. A child that is a merge of this block instead gets (the topmost ancestor inside the
+// block, the sum of the offsets up to it), found by pointer jumping in LDS — so every global jump
+// leaves a block, and the global pointer jumping needs ~log3(2 x blocks) launches, not log3(M).
+struct ParentShared {
+    int lp[kDeepTop];    // local parent (index in the block) of a block merge, -1: parent outside
+    int loff[kDeepTop];  // offset to it
+};
+__device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, int cnt) {
+    const Dims& d = w.d;
+    const int64_t lb = f * d.NL, eb = f * d.M;
+    const int tid = threadIdx.x;
+    const int64_t x0 = d.N + s0;  // node id of the block's first merge
+    for (int t = tid; t < cnt; t += kDeepT) sh.lp[t] = -1;
+    __syncthreads();
+    for (int t = tid; t < cnt; t += kDeepT) {
+        const int a = w.lu[eb + s0 + t], b = w.lv[eb + s0 + t];
+        const int sa = w.SZ[lb + a], sb = w.SZ[lb + b];
+        const bool lightB = sa >= sb;
+        const int h = lightB ? a : b, l = lightB ? b : a;
+        const int offl = 2 * (lightB ? sa : sb);
+        const int x = (int)(x0 + t);
+        w.hlB[eb + s0 + t] = lightB ? 1 : 0;
+        w.lite[lb + h] = 0;
+        w.lite[lb + l] = 1;
+        if (h >= x0 && h < x0 + cnt) {
+            sh.lp[h - x0] = t;
+            sh.loff[h - x0] = 1;
+        } else {
+            w.J[lb + h] = jump_pack(x, 1);
+        }
+        if (l >= x0 && l < x0 + cnt) {
+            sh.lp[l - x0] = t;
+            sh.loff[l - x0] = offl;
+        } else {
+            w.J[lb + l] = jump_pack(x, offl);
+        }
+    }
+    __syncthreads();
+    // pointer jumping to the block-top ancestor (a node whose parent is outside the block keeps
+    // lp = -1 and its word is written by the block of its parent)
+    for (int it = 0; (1 << it) < cnt; ++it) {
+        int na[kDeepTop / kDeepT], ns[kDeepTop / kDeepT];
+#pragma unroll
+        for (int k = 0; k < kDeepTop / kDeepT; ++k) {
+            const int t = tid + k * kDeepT;
+            na[k] = -1;
+            if (t >= cnt) continue;
+            const int p = sh.lp[t];
+            na[k] = p;
+            ns[k] = sh.loff[t];
+            if (p >= 0 && sh.lp[p] >= 0) {
+                na[k] = sh.lp[p];
+                ns[k] += sh.loff[p];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kDeepTop / kDeepT; ++k) {
+            const int t = tid + k * kDeepT;
+            if (t >= cnt) continue;
+            sh.lp[t] = na[k];
+            sh.loff[t] = ns[k];
+        }
+        __syncthreads();
+    }
+    for (int t = tid; t < cnt; t += kDeepT) {
+        const int p = sh.lp[t];
+        if (p >= 0) w.J[lb + x0 + t] = jump_pack((int)(x0 + p), sh.loff[t]);
+    }
+}
+static_assert(kDeepTop % kDeepT == 0, "parent epilogue shape");
+
+constexpr size_t kDeepSmem0 = sizeof(DeepShared) > sizeof(TopShared) ? sizeof(DeepShared) : sizeof(TopShared);
+constexpr size_t kDeepSmem = kDeepSmem0 > sizeof(ParentShared) ? kDeepSmem0 : sizeof(ParentShared);
 __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
     __shared__ __attribute__((aligned(16))) char smem[kDeepSmem];
     const Dims& d = w.d;
@@ -756,6 +849,8 @@ __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
     deep_block(w, *reinterpret_cast<DeepShared*>(smem), f, s0, cnt < kDeepS ? cnt : kDeepS);
     __syncthreads();
     if (cnt > kDeepS) deep_block(w, *reinterpret_cast<DeepShared*>(smem), f, s0 + kDeepS, cnt - kDeepS);
+    __syncthreads();
+    deep_parent(w, *reinterpret_cast<ParentShared*>(smem), f, s0, cnt);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1521,7 +1616,22 @@ struct HipBackend {
             timed(functor_name<F>(), fn);
     }
 
+    template <class F>
+    void launch_counted(int nf, int64_t n, const F& f, int cidx) {
+        if (n <= 0 || nf <= 0) return;
+        int64_t gx = (n + kBlock - 1) / kBlock;
+        const int64_t cap = grid_cap() > 0 ? std::max<int64_t>(1, grid_cap() / nf) : 8192;
+        if (gx > cap) gx = cap;
+        timed(functor_name<F>(), [&] {
+            hipLaunchKernelGGL(k_counted_take<F>, dim3((unsigned)gx, (unsigned)nf), dim3(kBlock), 0, stream, f, n, cidx);
+        });
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_counted_take launch");
+    }
     static constexpr int64_t deep_block() { return kDeepTop; }
+    void dnc_parent(const Ws&) {}  // done by k_dnc_deep's epilogue
+    // longest pointer chain the preorder's global jumping starts from: every word leaves its block
+    // or goes to the block's top, so at most two words per block on any path
+    static int64_t jump_chain_bound(int64_t M) { return 2 * ((M + kDeepTop - 1) / kDeepTop) + 1; }
     unsigned long long* stamps_ = nullptr;
     unsigned long long* seq_stamps() {
         static const bool on = [] {

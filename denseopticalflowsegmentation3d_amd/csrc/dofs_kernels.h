@@ -991,18 +991,34 @@ DOFS_HD inline void path_start(const Ws& w, int f, int64_t qb, float* mx, float*
 
 // Replay kernels run in phases: round r's short-path pass is phase 2r, its long-path pass 2r+1
 // (a path top's ready[] = the phase it completed in). A pass sees completions of earlier phases.
+// Advances heavy paths bottom-up until they complete or block on a light child whose path has not
+// completed yet. A parked path is appended to `out` (the next round's list; one block-aggregated
+// counter atomic per block), so later rounds only visit the paths still pending. out == nullptr:
+// the list is rescanned every round (the emulator's long paths).
 struct KReplay {
     Ws w;
     int phase;
     const int* list;
-    int count;
-    DOFS_HD void operator()(int f, int64_t jj) const {
+    int count;  // counter index of list's length (the launch is bounded by it)
+    int* out;
+    int outc;   // counter index of out's length
+    static constexpr bool kBlockTake = true;
+    template <class T>
+    DOFS_HD void operator()(int f, int64_t jj, bool valid, T& t) const {
+        int j = 0;
+        const bool park = valid && advance(f, jj, &j);
+        if (out) {
+            const int s = t.take(w.C(f) + outc, park);
+            if (park) out[f * w.d.N + s] = j;
+        }
+    }
+    DOFS_HD bool advance(int f, int64_t jj, int* jo) const {  // true: parked
         const Dims& d = w.d;
-        if (jj >= w.C(f)[count]) return;
         const int j = list[f * d.N + jj];
+        *jo = j;
         int* curp = w.cur + f * d.N + j;
         int q = *curp;
-        if (q < 0) return;
+        if (q < 0) return false;
         const int64_t lb = f * d.NL;
         RunState s;
         path_start(w, f, q + 1, &s.mx, &s.my, &s.rank, &s.root, &s.bb);
@@ -1015,7 +1031,7 @@ struct KReplay {
                 const int lq = in.lb;
                 if (w.ready[lb + lq] >= phase) {
                     *curp = q;
-                    return;
+                    return true;
                 }
                 wbx = w.Rmx[lb + lq] * (float)in.la;
                 wby = w.Rmy[lb + lq] * (float)in.la;
@@ -1035,11 +1051,17 @@ struct KReplay {
             if (in.meta & kStepTop) {
                 w.ready[lb + q] = phase;
                 *curp = -1;
-                return;
+                return false;
             }
             --q;
         }
     }
+};
+
+struct KCtrZero {  // counter `idx` of every frame = 0
+    Ws w;
+    int idx;
+    DOFS_HD void operator()(int f, int64_t) const { w.C(f)[idx] = 0; }
 };
 
 // State of merge node x after its merge: replay outputs (by preorder position) + size/bbox (KRT).

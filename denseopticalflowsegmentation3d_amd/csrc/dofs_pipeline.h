@@ -265,7 +265,7 @@ struct Pipeline {
             be.krt_seq(w);
         }
         be.dnc_deep(w);
-        be.launch(B, M, KDncParent{w});
+        be.dnc_parent(w);  // KDncParent (HIP: k_dnc_deep's epilogue)
 
         if (!preorder_in_b) preorder();
     }
@@ -280,7 +280,8 @@ struct Pipeline {
         // node's jump distance (the second hop may read an ancestor word not yet advanced in this
         // launch), so 3^launches >= M reaches every root
         int launches = 0;
-        for (int64_t span = 1; span < d.M; span *= 3) ++launches;
+        const int64_t chain = std::min<int64_t>(d.M, Backend::jump_chain_bound(d.M));
+        for (int64_t span = 1; span < chain; span *= 3) ++launches;
         for (int t = 0; t < launches; ++t) be.launch(B, d.M, KJump{w.J, NL, 2, N});
         be.launch(B, N, KJumpLeaf{w.J, NL});
         pre = w.pre;
@@ -301,8 +302,19 @@ struct Pipeline {
         be.mark(5);
         // K5 bottom-up replay of Forest::merge along heavy paths
         const int RR = ceil_log2(N) + 2;
+        // short paths: round r advances the paths parked in round r - 1 (lists ping-pong between two
+        // pixel-sized buffers whose owners, the MST passes, are done)
+        int* park[2] = {w.off, w.comp};
+        const int* in = w.list_short;
+        int inc = C_SHORT;
         for (int r = 0; r < RR; ++r) {
-            if (!(skip_mask & 1)) be.launch(B, N, KReplay{w, 2 * r, w.list_short, C_SHORT});
+            if (!(skip_mask & 1)) {
+                const int oc = C_SQ + (r & 1);
+                be.launch(B, 1, KCtrZero{w, oc});
+                be.launch_counted(B, N, KReplay{w, 2 * r, in, inc, park[r & 1], oc}, inc);
+                in = park[r & 1];
+                inc = oc;
+            }
             if (!(skip_mask & 2)) be.replay_long(w, r);  // HIP: three-wave kernel; emulator: KReplay
         }
 

@@ -90,6 +90,8 @@ struct HostBackend {
     // the HIP build runs the levels with block size <= 512 per block in LDS (k_dnc_deep); the
     // emulator runs them with the global kernels (same parents and sizes)
     static constexpr int64_t deep_block() { return 4096; }
+    void dnc_parent(const Ws& w) { launch(w.d.B, w.d.M, KDncParent{w}); }
+    static int64_t jump_chain_bound(int64_t M) { return M; }
     void dnc_deep(const Ws& w) {
         const int64_t M = w.d.M;
         int64_t top = 1;
@@ -148,7 +150,17 @@ struct HostBackend {
             launch(w.d.B, w.d.N, KBoruvkaMinI{w, r});
     }
     void dnc_compress(const Ws& w, int64_t S, int ep) { launch(w.d.B, w.d.M, KDncCompress{w, S, ep}); }
-    void replay_long(const Ws& w, int r) { launch(w.d.B, w.d.N, KReplay{w, 2 * r + 1, w.list_long, C_LONG}); }
+    void replay_long(const Ws& w, int r) {
+        launch_counted(w.d.B, w.d.N, KReplay{w, 2 * r + 1, w.list_long, C_LONG, nullptr, 0}, C_LONG);
+    }
+    template <class F>
+    void launch_counted(int nf, int64_t n, const F& f, int cidx) {  // elements [0, min(n, counter))
+        HostTaker t;
+        for (int fr = 0; fr < nf; ++fr) {
+            const int64_t m = std::min<int64_t>(n, f.w.C(fr)[cidx]);
+            for (int64_t i = 0; i < m; ++i) f(fr, i, true, t);
+        }
+    }
     void profile(bool) {}
     void probe(const char*) {}
     int64_t probe_read(double* ms) {
