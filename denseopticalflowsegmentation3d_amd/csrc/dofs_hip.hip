@@ -1365,6 +1365,77 @@ __global__ __launch_bounds__(256) void k_boruvka_relabel4(Ws w, int r) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// K1 blur, LDS-tiled (KBlurRow / KBlurCol of dofs_kernels.h, same float operations in the same
+// order): a row segment of 256 outputs (+ reflect-101 halo) or a 64 x 64 column tile (+ halo rows)
+// is staged once in LDS with coalesced loads, then every output reads its taps from LDS.
+// ---------------------------------------------------------------------------------------------
+constexpr int kBlurSeg = 256, kBlurR = kMaxTaps / 2;  // radius <= 31 (bn <= 63)
+__global__ __launch_bounds__(kBlurSeg) void k_blur_row(Ws w) {
+    __shared__ F2 buf[kBlurSeg + 2 * kBlurR];
+    const int W = w.d.W, H = w.d.H;
+    const int segs = (W + kBlurSeg - 1) / kBlurSeg;
+    const int f = blockIdx.y;
+    const int r = w.bn / 2;
+    for (int64_t bi = blockIdx.x; bi < (int64_t)segs * H; bi += gridDim.x) {
+        const int y = (int)(bi / segs), x0 = (int)(bi % segs) * kBlurSeg;
+        const F2* row = w.flow + f * w.flow_fstride + (int64_t)y * W;
+        for (int k = threadIdx.x; k < kBlurSeg + 2 * r; k += kBlurSeg) buf[k] = row[reflect101(x0 - r + k, W)];
+        __syncthreads();
+        const int x = x0 + threadIdx.x;
+        if (x < W) {
+            const F2* b = buf + threadIdx.x;
+            float sx = w.bk[0] * b[0].x, sy = w.bk[0] * b[0].y;
+            for (int t = 1; t < w.bn; ++t) {
+                sx += w.bk[t] * b[t].x;
+                sy += w.bk[t] * b[t].y;
+            }
+            F2 o;
+            o.x = sx;
+            o.y = sy;
+            w.tmp[f * w.d.N + (int64_t)y * W + x] = o;
+        }
+        __syncthreads();
+    }
+}
+constexpr int kColW = 64, kColH = 64, kColT = 256;
+__global__ __launch_bounds__(kColT) void k_blur_col(Ws w) {
+    __shared__ F2 buf[(kColH + 2 * kBlurR) * kColW];
+    const int W = w.d.W, H = w.d.H;
+    const int tx = (W + kColW - 1) / kColW, ty = (H + kColH - 1) / kColH;
+    const int f = blockIdx.y;
+    const int r = w.bn / 2;
+    const F2* src = w.tmp + f * w.d.N;
+    const int cx = threadIdx.x % kColW, cg = threadIdx.x / kColW;  // column, row group
+    for (int64_t bi = blockIdx.x; bi < (int64_t)tx * ty; bi += gridDim.x) {
+        const int x0 = (int)(bi % tx) * kColW, y0 = (int)(bi / tx) * kColH;
+        const int x = x0 + cx;
+        const int rows = kColH + 2 * r;
+        if (x < W)
+            for (int k = cg; k < rows; k += kColT / kColW)
+                buf[k * kColW + cx] = src[(int64_t)reflect101(y0 - r + k, H) * W + x];
+        __syncthreads();
+        if (x < W) {
+            for (int yy = cg; yy < kColH; yy += kColT / kColW) {
+                const int y = y0 + yy;
+                if (y >= H) break;
+                const F2* c = buf + (yy + r) * kColW + cx;
+                float sx = w.bk[r] * c[0].x + 0.0f, sy = w.bk[r] * c[0].y + 0.0f;
+                for (int j = 1; j <= r; ++j) {
+                    const F2 a = c[j * kColW], b = c[-j * kColW];
+                    sx += w.bk[r + j] * (a.x + b.x);
+                    sy += w.bk[r + j] * (a.y + b.y);
+                }
+                F2 o;
+                o.x = sx;
+                o.y = sy;
+                w.blur[f * w.d.N + (int64_t)y * W + x] = o;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 struct HipBackend {
     int device = 0;
     hipStream_t own = nullptr;
@@ -1629,6 +1700,21 @@ struct HipBackend {
     }
     static constexpr int64_t deep_block() { return kDeepTop; }
     void dnc_parent(const Ws&) {}  // done by k_dnc_deep's epilogue
+    void blur(const Ws& w) {  // KBlurRow + KBlurCol, LDS-tiled
+        const int64_t segs = (int64_t)((w.d.W + kBlurSeg - 1) / kBlurSeg) * w.d.H;
+        const int64_t tiles = (int64_t)((w.d.W + kColW - 1) / kColW) * ((w.d.H + kColH - 1) / kColH);
+        const int64_t cap = std::max<int64_t>(1, grid_cap() / w.d.B);
+        timed("k_blur_row", [&] {
+            hipLaunchKernelGGL(k_blur_row, dim3((unsigned)std::min(segs, cap), (unsigned)w.d.B), dim3(kBlurSeg), 0,
+                               stream, w);
+        });
+        timed("k_blur_col", [&] {
+            hipLaunchKernelGGL(k_blur_col, dim3((unsigned)std::min(tiles, cap), (unsigned)w.d.B), dim3(kColT), 0,
+                               stream, w);
+        });
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "blur launch");
+    }
+    static constexpr bool kKrtLabelWords = false;  // the LDS KRT and the sweep keep their own words
     // longest pointer chain the preorder's global jumping starts from: every word leaves its block
     // or goes to the block's top, so at most two words per block on any path
     static int64_t jump_chain_bound(int64_t M) { return 2 * ((M + kDeepTop - 1) / kDeepTop) + 1; }

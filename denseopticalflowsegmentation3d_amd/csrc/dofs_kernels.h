@@ -591,18 +591,29 @@ DOFS_HD inline unsigned long long jump_pack(int anc, int sum) {
 DOFS_HD inline int jump_anc(unsigned long long v) { return (int)(unsigned)(v & 0xffffffffu); }
 DOFS_HD inline int jump_sum(unsigned long long v) { return (int)(unsigned)(v >> 32); }
 
-struct KLabelInit {  // untagged label words (epoch 0), zero counters, pixel sizes, root size
-    Ws w;
+struct KLabelInit {  // pixel sizes, the root's size / jump word / path-top flag; full: also the
+    Ws w;           // global-kernel KRT's words (untagged label words, zero counters) over NL
+    bool full;      // (launched over NL when full, over N otherwise)
     DOFS_HD void operator()(int f, int64_t x) const {
         const Dims& d = w.d;
         const int64_t o = f * d.NL + x;
+        if (!full) {
+            w.SZ[o] = 1;
+            if (x == 0) {  // KRT root = last merge: the whole frame (preorder 0, a path top)
+                const int64_t r = f * d.NL + d.NL - 1;
+                w.SZ[r] = (int)d.N;
+                w.J[r] = jump_pack(-1, 0);
+                w.lite[r] = 1;
+            }
+            return;
+        }
         w.MX[o] = 0;
         w.CS[o] = 0;
         int sz = 0;
         if (x < d.N) {
             sz = 1;
             w.SZ[o] = 1;
-        } else if (x == d.NL - 1) {  // KRT root = last merge: the whole frame (preorder 0, a path top)
+        } else if (x == d.NL - 1) {
             sz = (int)d.N;
             w.SZ[o] = sz;
             w.J[o] = jump_pack(-1, 0);

@@ -230,11 +230,10 @@ struct Pipeline {
         be.memset(w.ctr, 0, sizeof(int) * (size_t)B * kCounters);
 
         be.mark(0);
-        // K1 blur (segment.cpp:52)
-        be.launch(B, N, KBlurRow{w});
-        be.launch(B, N, KBlurCol{w});
+        // K1 blur (segment.cpp:52): KBlurRow + KBlurCol (HIP: LDS-tiled)
+        be.blur(w);
         if (M <= 0) {  // single pixel: no edge, no merge
-            be.launch(B, N, KLabelInit{w});
+            be.launch(B, N, KLabelInit{w, true});
             be.launch(B, 1, KSingle{w});
             pre = nullptr;
             be.mark(8);
@@ -252,7 +251,8 @@ struct Pipeline {
         be.mark(3);
         // K3 Kruskal reconstruction tree
         be.launch(B, M, KEdgeInit{w});
-        be.launch(B, NL, KLabelInit{w});
+        const bool words = krt_dnc || Backend::kKrtLabelWords;  // the global-kernel KRT reads them
+        be.launch(B, words ? NL : N, KLabelInit{w, words});
         const int64_t deep = Backend::deep_block();  // levels with block size <= deep run per block
         if (krt_dnc) {  // measurement: the top-down global depths (DOFS_KRT_DNC=1)
             for (int64_t S = (int64_t)1 << ceil_log2(M); S > deep; S >>= 1) {

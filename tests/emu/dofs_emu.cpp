@@ -91,6 +91,11 @@ struct HostBackend {
     // emulator runs them with the global kernels (same parents and sizes)
     static constexpr int64_t deep_block() { return 4096; }
     void dnc_parent(const Ws& w) { launch(w.d.B, w.d.M, KDncParent{w}); }
+    void blur(const Ws& w) {
+        launch(w.d.B, w.d.N, KBlurRow{w});
+        launch(w.d.B, w.d.N, KBlurCol{w});
+    }
+    static constexpr bool kKrtLabelWords = true;  // the deep depths run as global kernels here
     static int64_t jump_chain_bound(int64_t M) { return M; }
     void dnc_deep(const Ws& w) {
         const int64_t M = w.d.M;
