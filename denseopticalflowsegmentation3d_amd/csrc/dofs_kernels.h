@@ -321,7 +321,11 @@ struct KBoruvkaInit {
 };
 
 // Round 0: every pixel is its own component, so its minimum edge is the min over its <= 8 incident
-// edges (4 it emits, 4 its right/lower neighbours emit towards it) — no atomics.
+// edges (4 it emits, 4 its right/lower neighbours emit towards it) — no atomics. The minimum edges
+// form a forest whose only cycles are the mutual pairs (a unique minimum per component under the
+// strict order): each pixel points at the far end of its minimum edge (uf) and marks the edge;
+// KBoruvkaPairs then roots each pair at its smaller pixel, and the relabel's finds (path halving)
+// give every pixel its component — no unions, no CAS. The minima words start round 1 as "none".
 struct KBoruvkaFirst {
     Ws w;
     DOFS_HD void operator()(int f, int64_t p) const {
@@ -330,6 +334,7 @@ struct KBoruvkaFirst {
         const F2* b = w.blur + f * d.N;
         unsigned long long best = ~0ull;
         unsigned bidx = kNoEdge;
+        int64_t far = p;
         auto take = [&](int64_t s, int k, int64_t e) {
             if (!edge_allowed(w, f, s, k)) return;
             const unsigned long long wb = dbits(edge_weight(b, s, e));
@@ -337,6 +342,7 @@ struct KBoruvkaFirst {
             if (wb < best || (wb == best && idx < bidx)) {
                 best = wb;
                 bidx = idx;
+                far = s == p ? e : s;
             }
         };
         for (int k = 0; k < 4; ++k)
@@ -345,9 +351,22 @@ struct KBoruvkaFirst {
         if (y + 1 < d.H) take(p + d.W, 1, p);                                     // below: its up edge
         if (d.nbr8 && x + 1 < d.W && y + 1 < d.H) take(p + d.W + 1, 2, p);       // down-right: up-left
         if (d.nbr8 && x + 1 < d.W && y >= 1) take(p - d.W + 1, 3, p);            // up-right: down-left
-        w.bw[f * d.N + p] = best;
-        w.bi[f * d.N + p] = bidx;
-        if (bidx != kNoEdge && p == 0) w.C(f)[C_ACT + 0] = 1;
+        const int64_t o = f * d.N + p;
+        w.bw[o] = ~0ull;
+        w.bi[o] = kNoEdge;
+        w.uf[o] = (int)far;
+        if (bidx != kNoEdge) {
+            reinterpret_cast<unsigned char*>(w.mstbits + f * d.N + (bidx >> 2))[bidx & 3] = 1;
+            if (p == 0) w.C(f)[C_ACT + 0] = 1;
+        }
+    }
+};
+struct KBoruvkaPairs {  // a mutual pair of minimum edges: the smaller pixel becomes the root
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t p) const {
+        int* uf = w.uf + f * w.d.N;
+        const int q = uf[p];
+        if (q > (int)p && uf[q] == (int)p) uf[p] = (int)p;
     }
 };
 

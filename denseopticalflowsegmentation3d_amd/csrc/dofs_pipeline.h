@@ -185,13 +185,14 @@ struct Pipeline {
         be.launch(B, N, KBoruvkaInit{w});
         const int R = std::min(ceil_log2(N) + 2, kRoundsMax - 1);
         for (int r = 0; r < R; ++r) {
-            if (r == 0) {
+            if (r == 0) {  // every pixel hooks along its minimum edge (a forest of pointers)
                 be.launch(B, N, KBoruvkaFirst{w});
+                be.launch(B, N, KBoruvkaPairs{w});
             } else {
                 be.boruvka_min(w, r, 0);  // KBoruvkaMinW (HIP: workgroup-aggregated per tile)
                 be.boruvka_min(w, r, 1);  // KBoruvkaMinI
+                be.boruvka_hook(w, r);    // KBoruvkaHook (also clears the roots' minima for round r + 1)
             }
-            be.boruvka_hook(w, r);  // KBoruvkaHook (also clears the roots' minima for round r + 1)
             be.boruvka_relabel(w, r);  // KBoruvkaRelabelFind
         }
     }
