@@ -838,12 +838,9 @@ static_assert(kDeepTop % kDeepT == 0, "parent epilogue shape");
 
 constexpr size_t kDeepSmem0 = sizeof(DeepShared) > sizeof(TopShared) ? sizeof(DeepShared) : sizeof(TopShared);
 constexpr size_t kDeepSmem = kDeepSmem0 > sizeof(ParentShared) ? kDeepSmem0 : sizeof(ParentShared);
-__global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
-    __shared__ __attribute__((aligned(16))) char smem[kDeepSmem];
+// all depths of one kDeepTop-merge block of frame f in LDS, then its parents (block-uniform call)
+__device__ void deep_item(const Ws& w, char* smem, int f, int64_t s0) {
     const Dims& d = w.d;
-    const int f = blockIdx.y;
-    const int64_t s0 = (int64_t)blockIdx.x * kDeepTop;
-    if (s0 >= d.M) return;
     const int cnt = (int)((d.M - s0) < kDeepTop ? (d.M - s0) : kDeepTop);
     if (cnt > kDeepS) top_level(w, *reinterpret_cast<TopShared*>(smem), f, s0, cnt);
     deep_block(w, *reinterpret_cast<DeepShared*>(smem), f, s0, cnt < kDeepS ? cnt : kDeepS);
@@ -851,6 +848,12 @@ __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
     if (cnt > kDeepS) deep_block(w, *reinterpret_cast<DeepShared*>(smem), f, s0 + kDeepS, cnt - kDeepS);
     __syncthreads();
     deep_parent(w, *reinterpret_cast<ParentShared*>(smem), f, s0, cnt);
+}
+__global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
+    __shared__ __attribute__((aligned(16))) char smem[kDeepSmem];
+    const int64_t s0 = (int64_t)blockIdx.x * kDeepTop;
+    if (s0 >= w.d.M) return;
+    deep_item(w, smem, blockIdx.y, s0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1102,19 +1105,27 @@ struct KSeqInitRec {
 __device__ __forceinline__ SeqRec rec_ld(const SeqRec* p) { return *p; }
 __device__ __forceinline__ void rec_set_par(SeqRec* p, int v) { wg_st(&p->par, v); }
 
-// finds of K chains at once with path halving: each round issues every pending chain's load first
+// finds of K chains at once with path halving: each round issues every pending chain's load first;
+// on return x[k] is the root and lab[k] / sz[k] its label and size (only the fields a caller needs
+// stay live, to keep the sweep within 128 VGPRs)
 template <int K>
-__device__ __forceinline__ void rec_find(SeqRec* rec, int (&x)[K], bool (&pend)[K], SeqRec (&root)[K]) {
+__device__ __forceinline__ void rec_find(SeqRec* rec, int (&x)[K], bool (&pend)[K], int (&lab)[K], int (&sz)[K]) {
     for (;;) {
-        SeqRec p[K], g[K];
+        int pp[K], pl[K], ps[K];
         bool any = false;
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            if (pend[k]) p[k] = rec_ld(rec + x[k]);
+            if (pend[k]) {
+                const SeqRec r = rec_ld(rec + x[k]);
+                pp[k] = r.par;
+                pl[k] = r.lab;
+                ps[k] = r.sz;
+            }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            if (pend[k] && p[k].par == x[k]) {
-                root[k] = p[k];
+            if (pend[k] && pp[k] == x[k]) {
+                lab[k] = pl[k];
+                sz[k] = ps[k];
                 pend[k] = false;
             }
             any |= pend[k];
@@ -1122,19 +1133,18 @@ __device__ __forceinline__ void rec_find(SeqRec* rec, int (&x)[K], bool (&pend)[
         if (!any) return;
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            if (pend[k]) g[k] = rec_ld(rec + p[k].par);
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if (!pend[k]) continue;
-            if (g[k].par == p[k].par) {
-                x[k] = p[k].par;
-                root[k] = g[k];
-                pend[k] = false;
-            } else {
-                rec_set_par(rec + x[k], g[k].par);
-                x[k] = g[k].par;
+            if (pend[k]) {
+                const SeqRec g = rec_ld(rec + pp[k]);
+                if (g.par == pp[k]) {
+                    x[k] = pp[k];
+                    lab[k] = g.lab;
+                    sz[k] = g.sz;
+                    pend[k] = false;
+                } else {
+                    rec_set_par(rec + x[k], g.par);
+                    x[k] = g.par;
+                }
             }
-        }
     }
 }
 
@@ -1149,19 +1159,21 @@ __device__ __forceinline__ constexpr bool seq_compress() { return DOFS_SEQ_COMPR
 //   C  each merge's resulting root R, aggregated per R in LDS: max rank in the block, sizes of the
 //      roots hooked into it, R's old size; the endpoints are compressed onto R
 //   D  per R: its new label and size (one 8-byte store) and the KRT node size SZ
-__global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w, unsigned long long* stamps) {
-    // diagnostic (DOFS_SEQ_STAMP=1): shader cycles per phase, summed over the blocks, workgroup 0
-    unsigned long long t0 = stamps ? __builtin_amdgcn_s_memtime() : 0, acc[4] = {0, 0, 0, 0};
-    auto stamp = [&](int ph) {
-        if (!stamps || blockIdx.x != 0 || threadIdx.x != 0) return;
-        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-        acc[ph] += t1 - t0;
-        t0 = t1;
-    };
+struct SweepShared {
+    int hk[kSeqHT], hmx[kSeqHT], hsz[kSeqHT], hold[kSeqHT];
+};
+// The sweep of frame f by one workgroup. progress (optional, stride kCounters per frame): after
+// phase A of block b, the frame's word is set to b + 1 — the block's labels and every label size it refers to are then
+// published (stored write-through, drained, one agent-scope flag store) for k_krt_fused's LDS-KRT
+// workers.
+__device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
     constexpr int K = kSeqK, K2 = 2 * kSeqK, KS = kSeqHT / kSeqT;
-    __shared__ int hk[kSeqHT], hmx[kSeqHT], hsz[kSeqHT], hold[kSeqHT];
+    int* hk = sh.hk;
+    int* hmx = sh.hmx;
+    int* hsz = sh.hsz;
+    int* hold = sh.hold;
     const Dims& d = w.d;
-    const int f = blockIdx.x, tid = threadIdx.x;
+    const int tid = threadIdx.x;
     SeqRec* rec = reinterpret_cast<SeqRec*>(w.In + f * d.NL);
     const int* EU = w.EU + f * d.M;
     const int* EV = w.EV + f * d.M;
@@ -1179,7 +1191,7 @@ __global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w, unsigned long long* sta
         // ---- A
         int e[K2], c[K2];
         bool act2[K2], pend[K2];
-        SeqRec rt[K2];
+        int rtl[K2], rts[K2];  // roots' labels and sizes
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int t = tid + k * kSeqT;
@@ -1192,16 +1204,26 @@ __global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w, unsigned long long* sta
             c[k] = e[k];
             pend[k] = act2[k];
         }
-        rec_find<K2>(rec, c, pend, rt);
+        rec_find<K2>(rec, c, pend, rtl, rts);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             if (!act2[2 * k]) continue;
             const int t = tid + k * kSeqT;
-            lu[s + t] = rt[2 * k].lab < 0 ? e[2 * k] : (int)(d.N + rt[2 * k].lab);
-            lv[s + t] = rt[2 * k + 1].lab < 0 ? e[2 * k + 1] : (int)(d.N + rt[2 * k + 1].lab);
+            const int la = rtl[2 * k] < 0 ? e[2 * k] : (int)(d.N + rtl[2 * k]);
+            const int lb = rtl[2 * k + 1] < 0 ? e[2 * k + 1] : (int)(d.N + rtl[2 * k + 1]);
+            if (progress) {  // write-through (sc1): read by other workgroups after the flag
+                __hip_atomic_store(lu + s + t, la, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(lv + s + t, lb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                lu[s + t] = la;
+                lv[s + t] = lb;
+            }
         }
+        if (progress) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
         __syncthreads();
-        stamp(0);
+        if (progress && tid == 0)
+            __hip_atomic_store(progress + (int64_t)f * kCounters, (int)(s / kSeqB) + 1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         // ---- B
         int hooked_sz[K];
         {
@@ -1212,24 +1234,24 @@ __global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w, unsigned long long* sta
                 x[k] = c[k];
                 pu[k] = false;
             }
-            SeqRec r2[K2];
+            int r2l[K2], r2s[K2];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 todo[k] = act2[2 * k];
                 hooked_sz[k] = 0;
-                r2[2 * k] = rt[2 * k];
-                r2[2 * k + 1] = rt[2 * k + 1];
+                r2s[2 * k] = rts[2 * k];
+                r2s[2 * k + 1] = rts[2 * k + 1];
             }
             for (;;) {
                 bool any = false;
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     if (!todo[k]) continue;
-                    int a = x[2 * k], b = x[2 * k + 1], sa = r2[2 * k].sz;
+                    int a = x[2 * k], b = x[2 * k + 1], sa = r2s[2 * k];
                     if (!uf_above(a, b)) {
                         a = x[2 * k + 1];
                         b = x[2 * k];
-                        sa = r2[2 * k + 1].sz;
+                        sa = r2s[2 * k + 1];
                     }
                     if (wg_cas(&rec[a].par, a, b) == a) {
                         hooked_sz[k] = sa;
@@ -1240,22 +1262,21 @@ __global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w, unsigned long long* sta
                     }
                 }
                 if (!any) break;
-                rec_find<K2>(rec, x, pu, r2);
+                rec_find<K2>(rec, x, pu, r2l, r2s);
             }
         }
         __syncthreads();
-        stamp(1);
         // ---- C
         {
             int R[K];
             bool pr[K];
-            SeqRec rr[K];
+            int rrl[K], rrs[K];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 R[k] = c[2 * k];
                 pr[k] = act2[2 * k];
             }
-            rec_find<K>(rec, R, pr, rr);
+            rec_find<K>(rec, R, pr, rrl, rrs);
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 if (!act2[2 * k]) continue;
@@ -1269,7 +1290,7 @@ __global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w, unsigned long long* sta
                 }
                 atomicMax(hmx + slot, tid + k * kSeqT);
                 atomicAdd(hsz + slot, hooked_sz[k]);
-                hold[slot] = rr[k].sz;  // R's size at the block start (same value from every inserter)
+                hold[slot] = rrs[k];  // R's size at the block start (same value from every inserter)
                 if (seq_compress()) {
                     if (e[2 * k] != R[k]) rec_set_par(rec + e[2 * k], R[k]);
                     if (e[2 * k + 1] != R[k]) rec_set_par(rec + e[2 * k + 1], R[k]);
@@ -1277,7 +1298,6 @@ __global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w, unsigned long long* sta
             }
         }
         __syncthreads();
-        stamp(2);
         // ---- D
 #pragma unroll
         for (int q = 0; q < KS; ++q) {
@@ -1288,16 +1308,21 @@ __global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w, unsigned long long* sta
             const int j = (int)(s + hmx[x]);
             int2* lz = reinterpret_cast<int2*>(&rec[R].lab);
             *lz = make_int2(j, sz);
-            SZ[j] = sz;
+            if (progress)
+                __hip_atomic_store(SZ + j, sz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                SZ[j] = sz;
             hk[x] = -1;
             hmx[x] = -1;
             hsz[x] = 0;
         }
         __syncthreads();
-        stamp(3);
     }
-    if (stamps && blockIdx.x == 0 && threadIdx.x == 0)
-        for (int k = 0; k < 4; ++k) stamps[k] += acc[k];
+}
+
+__global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w) {
+    __shared__ SweepShared sh;
+    krt_sweep(w, blockIdx.x, sh, nullptr);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1436,6 +1461,54 @@ __global__ __launch_bounds__(kColT) void k_blur_col(Ws w) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// K3 fused (default; DOFS_FUSED=0: k_krt_seq then k_dnc_deep): one persistent launch in which the
+// latency-bound sweeps and the LDS KRT blocks share the chip. Every workgroup first claims a frame's
+// sweep while any is unclaimed (a claimed sweep runs to its end without waiting on anything), then
+// takes LDS-KRT blocks in block-major order; a block waits (agent-scope poll of its frame's
+// progress word, then one acquire) until the sweep has published the block's labels. No workgroup
+// ever waits on a workgroup that is not running, whatever the dispatch order.
+//   ctl = C(0) words: [C_FUSE] sweep claims, [C_FUSE + 1] block claims; progress = C(f)[C_PROG]
+// ---------------------------------------------------------------------------------------------
+static_assert(kSeqT == kDeepT, "one workgroup shape for both roles");
+constexpr size_t kFusedSmem = sizeof(SweepShared) > kDeepSmem ? sizeof(SweepShared) : kDeepSmem;
+__global__ __launch_bounds__(kDeepT) void k_krt_fused(Ws w, int* progress) {
+    __shared__ __attribute__((aligned(16))) char smem[kFusedSmem];
+    __shared__ int item;
+    const Dims& d = w.d;
+    const int B = d.B;
+    int* ctl = w.ctr + C_FUSE;
+    const int tid = threadIdx.x;
+    for (;;) {  // sweeps
+        if (tid == 0) item = atomicAdd(ctl, 1);
+        __syncthreads();
+        const int f = item;
+        __syncthreads();
+        if (f >= B) break;
+        krt_sweep(w, f, *reinterpret_cast<SweepShared*>(smem), progress);
+        __syncthreads();
+    }
+    const int64_t nblk = (d.M + kDeepTop - 1) / kDeepTop;
+    for (;;) {  // LDS KRT blocks, block-major over the frames
+        if (tid == 0) item = atomicAdd(ctl + 1, 1);
+        __syncthreads();
+        const int it = item;
+        __syncthreads();
+        if (it >= nblk * B) break;
+        const int f = it % B;
+        const int64_t k = it / B;
+        if (tid == 0) {
+            while (__hip_atomic_load(progress + f * kCounters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k + 1)
+                __builtin_amdgcn_s_sleep(8);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        deep_item(w, smem, f, k * kDeepTop);
+        __syncthreads();
+    }
+}
+
 struct HipBackend {
     int device = 0;
     hipStream_t own = nullptr;
@@ -1465,14 +1538,6 @@ struct HipBackend {
         stream = own;
     }
     ~HipBackend() {
-        if (stamps_) {
-            unsigned long long h[8];
-            (void)hipDeviceSynchronize();
-            (void)hipMemcpy(h, stamps_, sizeof(h), hipMemcpyDeviceToHost);
-            fprintf(stderr, "k_krt_seq cycles per phase (workgroup 0, all launches): %llu %llu %llu %llu\n", h[0], h[1],
-                    h[2], h[3]);
-            (void)hipFree(stamps_);
-        }
         for (auto e : pool) (void)hipEventDestroy(e);
         for (auto e : events) (void)hipEventDestroy(e);
         for (auto& t : tmps)
@@ -1718,26 +1783,38 @@ struct HipBackend {
     // longest pointer chain the preorder's global jumping starts from: every word leaves its block
     // or goes to the block's top, so at most two words per block on any path
     static int64_t jump_chain_bound(int64_t M) { return 2 * ((M + kDeepTop - 1) / kDeepTop) + 1; }
-    unsigned long long* stamps_ = nullptr;
-    unsigned long long* seq_stamps() {
+    static bool fused() {
         static const bool on = [] {
-            const char* e = getenv("DOFS_SEQ_STAMP");
-            return e && e[0] == '1';
+            const char* e = getenv("DOFS_FUSED");
+            return !(e && e[0] == '0');
         }();
-        if (on && !stamps_) {
-            note(hipMalloc(&stamps_, 64), "hipMalloc");
-            note(hipMemset(stamps_, 0, 64), "hipMemset");
-        }
-        return stamps_;
+        return on;
     }
     void krt_seq(const Ws& w) {
+        if (fused()) {  // sweep + LDS KRT in one persistent launch (k_krt_fused); dnc_deep is a no-op
+            launch(w.d.B, w.d.N, KSeqInitRec{reinterpret_cast<SeqRec*>(w.In), 2 * w.d.NL});
+            int dev_cus = 256;
+            (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, device);
+            timed("k_krt_fused", [&] {
+                hipLaunchKernelGGL(k_krt_fused, dim3((unsigned)dev_cus), dim3(kDeepT), 0, stream, w,
+                                   w.ctr + C_PROG);
+            });
+            if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_krt_fused launch");
+            fused_done = true;
+            return;
+        }
         launch(w.d.B, w.d.N, KSeqInitRec{reinterpret_cast<SeqRec*>(w.In), 2 * w.d.NL});
         timed("k_krt_seq", [&] {
-            hipLaunchKernelGGL(k_krt_seq, dim3((unsigned)w.d.B), dim3(kSeqT), 0, stream, w, seq_stamps());
+            hipLaunchKernelGGL(k_krt_seq, dim3((unsigned)w.d.B), dim3(kSeqT), 0, stream, w);
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_krt_seq launch");
     }
+    bool fused_done = false;  // the last krt_seq already ran the LDS KRT
     void dnc_deep(const Ws& w) {
+        if (fused_done) {
+            fused_done = false;
+            return;
+        }
         const unsigned nb = (unsigned)((w.d.M + kDeepTop - 1) / kDeepTop);
         timed("k_dnc_deep", [&] {
             hipLaunchKernelGGL(k_dnc_deep, dim3(nb, (unsigned)w.d.B), dim3(kDeepT), 0, stream, w);
