@@ -863,7 +863,7 @@ __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
 // issues one global atomic per distinct component — instead of one per candidate edge endpoint.
 // pass 0: minimum weight bits; pass 1: minimum emission index among the edges of that weight.
 // ---------------------------------------------------------------------------------------------
-constexpr int kTileX = 32, kTileY = 8, kMinHT = 512;
+constexpr int kTileX = 32, kTileY = 8, kMinHT = 512;  // 512 > 256 pixels + 82 halo keys per tile (no overflow)
 // Tiles whose pixels have no cross-component edge left are done for good (components only merge):
 // pass 0 marks them in `tdone` (per frame and tile) and later passes skip them.
 __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass, unsigned char* tdone) {
