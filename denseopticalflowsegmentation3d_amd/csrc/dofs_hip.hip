@@ -1793,11 +1793,18 @@ struct HipBackend {
     void krt_seq(const Ws& w) {
         if (fused()) {  // sweep + LDS KRT in one persistent launch (k_krt_fused); dnc_deep is a no-op
             launch(w.d.B, w.d.N, KSeqInitRec{reinterpret_cast<SeqRec*>(w.In), 2 * w.d.NL});
+            // persistent workgroups: the frames' sweeps plus `extra` LDS-KRT workers, one per CU
+            // by default (DOFS_FUSED_EXTRA; measured at B = 96: 0 / 32 / 64 / 96 / 160 extra ->
+            // 647 / 729 / 783 / 818 / 823 Mpix/s — the other stream's replay loses little)
+            static const int extra = [] {
+                const char* e = getenv("DOFS_FUSED_EXTRA");
+                return e ? atoi(e) : 1 << 20;
+            }();
             int dev_cus = 256;
             (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, device);
+            const int nwg = std::max(1, std::min(dev_cus, w.d.B + extra));
             timed("k_krt_fused", [&] {
-                hipLaunchKernelGGL(k_krt_fused, dim3((unsigned)dev_cus), dim3(kDeepT), 0, stream, w,
-                                   w.ctr + C_PROG);
+                hipLaunchKernelGGL(k_krt_fused, dim3((unsigned)nwg), dim3(kDeepT), 0, stream, w, w.ctr + C_PROG);
             });
             if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_krt_fused launch");
             fused_done = true;
