@@ -390,22 +390,16 @@ int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity
     if (capacity < d.M) return cx->fail(DOFS_ERR_CAPACITY, "event capacity");
     if (d.M <= 0) return DOFS_OK;
     Backend& be = cx->be;
-    std::vector<int> eu((size_t)d.M), evv((size_t)d.M), pre((size_t)d.M), rrank((size_t)d.NL), rroot((size_t)d.NL),
-        sz((size_t)d.M);
-    std::vector<float> rmx((size_t)d.NL), rmy((size_t)d.NL);
-    std::vector<B4> bb((size_t)d.NL);
+    std::vector<int> eu((size_t)d.M), evv((size_t)d.M), pre((size_t)d.M), sz((size_t)d.M);
+    std::vector<RepVal> rv((size_t)d.NL);
     std::vector<unsigned long long> key((size_t)d.M);
     const int64_t fo = (int64_t)frame * d.NL;
     be.d2h(eu.data(), w.EU + (int64_t)frame * d.M, 4 * (size_t)d.M);
     be.d2h(evv.data(), w.EV + (int64_t)frame * d.M, 4 * (size_t)d.M);
     be.d2h(key.data(), w.key_out + (int64_t)frame * d.M, 8 * (size_t)d.M);
     be.d2h(pre.data(), cx->pipe(slot).pre + fo + d.N, 4 * (size_t)d.M);
-    be.d2h(rmx.data(), w.Rmx + fo, 4 * (size_t)d.NL);
-    be.d2h(rmy.data(), w.Rmy + fo, 4 * (size_t)d.NL);
-    be.d2h(rrank.data(), w.Rrank + fo, 4 * (size_t)d.NL);
-    be.d2h(rroot.data(), w.Rroot + fo, 4 * (size_t)d.NL);
+    be.d2h(rv.data(), w.Rv + fo, sizeof(RepVal) * (size_t)d.NL);
     be.d2h(sz.data(), w.SZ + fo + d.N, 4 * (size_t)d.M);
-    be.d2h(bb.data(), w.Rbb + fo, sizeof(B4) * (size_t)d.NL);
     be.sync();
     for (int64_t i = 0; i < d.M; ++i) {
         dofs_event& e = ev[i];
@@ -413,15 +407,16 @@ int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity
         e.start = eu[i];
         e.end = evv[i];
         memcpy(&e.weight, &key[i], sizeof(double));
-        e.root = rroot[q];
+        const RepVal& r = rv[q];
+        e.root = r.root;
         e.size = sz[i];
-        e.rank = rrank[q];
-        e.bbox[0] = bb[q].x0;
-        e.bbox[1] = bb[q].y0;
-        e.bbox[2] = bb[q].x1;
-        e.bbox[3] = bb[q].y1;
-        e.mean[0] = rmx[q];
-        e.mean[1] = rmy[q];
+        e.rank = r.rank;
+        e.bbox[0] = r.bb.x0;
+        e.bbox[1] = r.bb.y0;
+        e.bbox[2] = r.bb.x1;
+        e.bbox[3] = r.bb.y1;
+        e.mean[0] = r.mx;
+        e.mean[1] = r.my;
     }
     return cx->check();
 }

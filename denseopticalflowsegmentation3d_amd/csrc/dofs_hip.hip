@@ -239,6 +239,7 @@ constexpr int kLongOk = 8;
 struct LongShared {
     ChainRec chain[2][2][64];  // [wave][buffer][step]
     SideRec side[2][64];       // [buffer][step]
+    float om[2][2][64];        // [buffer][wave][step]: the chains' outputs, stored by wave 2
     int go;                    // blocked step: 1 = its light child completed (continue), 0 = park
 };
 constexpr unsigned long long kSpinTicks = 5000000ull;  // 50 ms of s_memrealtime (100 MHz)
@@ -260,12 +261,13 @@ __device__ inline int long_resolve(const Ws& w, int64_t lb, int p, int top, int 
         const int phase = 2 * round + 1;
         if (w.ready[lb + lq] >= (p == accept ? phase + 1 : phase)) return meta;
         if (wv < 2) {
-            wb = (wv ? w.Rmy[lb + lq] : w.Rmx[lb + lq]) * (float)in.la;
+            wb = (wv ? w.Rv[lb + lq].my : w.Rv[lb + lq].mx) * (float)in.la;
         } else {
             wb = 0.f;
-            lrank = w.Rrank[lb + lq];
-            lroot = w.Rroot[lb + lq];
-            *lbb = w.Rbb[lb + lq];
+            const RepVal lv = w.Rv[lb + lq];
+            lrank = lv.rank;
+            lroot = lv.root;
+            *lbb = lv.bb;
         }
     } else {
         wb = wv ? in.wby : in.wbx;
@@ -354,6 +356,7 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can
         // stores inside the loop, so the compiler can issue the record loads ahead of the chain)
         float om = 0.f;
         int orank = 0, oroot = 0;
+        B4 obb;
         if (wv < 2) {
             const ChainRec* c = sh.chain[wv][cb];
 #pragma unroll 8
@@ -382,7 +385,7 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can
                 if (lane >= o) x = bb_join(x, y);
             }
             x = bb_join(x, bb);
-            if (lane < n) w.Rbb[lb + q - lane] = x;
+            obb = x;
             {
                 const int src = n > 0 ? n - 1 : 0;
                 const int lo = __shfl((int)((unsigned short)x.x0 | ((unsigned)(unsigned short)x.y0 << 16)), src, 64);
@@ -395,14 +398,19 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can
                 }
             }
         }
-        if (lane < n) {
-            const int p = q - lane;
-            if (wv == 0) w.Rmx[lb + p] = om;
-            if (wv == 1) w.Rmy[lb + p] = om;
-            if (wv == 2) {
-                w.Rrank[lb + p] = orank;
-                w.Rroot[lb + p] = oroot;
-            }
+        // the chunk's records: the chains hand their outputs to wave 2 through LDS (double-buffered
+        // by chunk parity), which stores each step's 32-byte record, 64 steps contiguous
+        if (wv < 2) sh.om[cb][wv][lane] = om;
+        __syncthreads();
+        if (wv == 2 && lane < n) {
+            RepVal o;
+            o.mx = sh.om[cb][0][lane];
+            o.my = sh.om[cb][1][lane];
+            o.rank = orank;
+            o.root = oroot;
+            o.bb = obb;
+            o.pad0 = o.pad1 = 0;
+            w.Rv[lb + q - lane] = o;
         }
         if (finished) {
             // publish the path top: every wave's output stores, then one agent-scope release, then

@@ -87,11 +87,7 @@ struct Ws {
     int* isleaf;
     int* lscan;
     StepIn* In;
-    float* Rmx;
-    float* Rmy;
-    int* Rrank;
-    int* Rroot;
-    B4* Rbb;
+    RepVal* Rv;  // replay outputs by preorder position
     int* ready;
     // per pixel (stride N)
     int* leaf_order;
@@ -1012,11 +1008,12 @@ DOFS_HD inline void path_start(const Ws& w, int f, int64_t qb, float* mx, float*
         bb->y0 = bb->y1 = (int16_t)(x / d.W);
         return;
     }
-    *mx = w.Rmx[lb + qb];
-    *my = w.Rmy[lb + qb];
-    *rank = w.Rrank[lb + qb];
-    *root = w.Rroot[lb + qb];
-    *bb = w.Rbb[lb + qb];
+    const RepVal v = w.Rv[lb + qb];
+    *mx = v.mx;
+    *my = v.my;
+    *rank = v.rank;
+    *root = v.root;
+    *bb = v.bb;
 }
 
 // Replay kernels run in phases: round r's short-path pass is phase 2r, its long-path pass 2r+1
@@ -1063,21 +1060,25 @@ struct KReplay {
                     *curp = q;
                     return true;
                 }
-                wbx = w.Rmx[lb + lq] * (float)in.la;
-                wby = w.Rmy[lb + lq] * (float)in.la;
-                lrank = w.Rrank[lb + lq];
-                lroot = w.Rroot[lb + lq];
-                lbb = w.Rbb[lb + lq];
+                const RepVal lv = w.Rv[lb + lq];
+                wbx = lv.mx * (float)in.la;
+                wby = lv.my * (float)in.la;
+                lrank = lv.rank;
+                lroot = lv.root;
+                lbb = lv.bb;
             } else {
                 lbb.x0 = lbb.x1 = (int16_t)(in.la & 0xffff);
                 lbb.y0 = lbb.y1 = (int16_t)(in.la >> 16);
             }
             step_merge(s, in.fs, wbx, wby, in.r, in.meta, lrank, lroot, lbb);
-            w.Rmx[lb + q] = s.mx;
-            w.Rmy[lb + q] = s.my;
-            w.Rrank[lb + q] = s.rank;
-            w.Rroot[lb + q] = s.root;
-            w.Rbb[lb + q] = s.bb;
+            RepVal o;
+            o.mx = s.mx;
+            o.my = s.my;
+            o.rank = s.rank;
+            o.root = s.root;
+            o.bb = s.bb;
+            o.pad0 = o.pad1 = 0;
+            w.Rv[lb + q] = o;
             if (in.meta & kStepTop) {
                 w.ready[lb + q] = phase;
                 *curp = -1;
@@ -1100,12 +1101,13 @@ DOFS_HD inline NodeVal node_val(const Ws& w, const int* pre, int f, int64_t x) {
     const int64_t lb = f * d.NL;
     const int q = pre[lb + x];
     NodeVal v;
-    v.mx = w.Rmx[lb + q];
-    v.my = w.Rmy[lb + q];
-    v.rank = w.Rrank[lb + q];
-    v.root = w.Rroot[lb + q];
+    const RepVal r = w.Rv[lb + q];
+    v.mx = r.mx;
+    v.my = r.my;
+    v.rank = r.rank;
+    v.root = r.root;
     v.size = w.SZ[lb + x];
-    const B4 b = w.Rbb[lb + q];
+    const B4 b = r.bb;
     v.x0 = b.x0;
     v.y0 = b.y0;
     v.x1 = b.x1;
@@ -1194,7 +1196,7 @@ struct KSlotEvent {  // first event reaching the slot's maximum wins (strict '<'
         const double s = w.cscore[f * d.M + j];
         if (!(s > w.score_threshold)) return;
         const int i = w.cand[f * d.M + j];
-        const int root = w.Rroot[f * d.NL + pre[f * d.NL + d.N + i]];
+        const int root = w.Rv[f * d.NL + pre[f * d.NL + d.N + i]].root;
         if (dbits(s) == w.sbest[f * d.N + root]) dofs_amin(w.sevent + f * d.N + root, i);
     }
 };

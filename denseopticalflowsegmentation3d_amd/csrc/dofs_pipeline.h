@@ -135,11 +135,7 @@ struct Pipeline {
         w.isleaf = (int*)take(4 * B * NL);
         w.lscan = (int*)take(4 * B * NL);
         w.In = (StepIn*)take(sizeof(StepIn) * B * NL);
-        w.Rmx = (float*)take(4 * B * NL);
-        w.Rmy = (float*)take(4 * B * NL);
-        w.Rrank = (int*)take(4 * B * NL);
-        w.Rroot = (int*)take(4 * B * NL);
-        w.Rbb = (B4*)take(sizeof(B4) * B * NL);
+        w.Rv = (RepVal*)take(sizeof(RepVal) * B * NL);
         w.ready = (int*)take(4 * B * NL);
         w.leaf_order = (int*)take(4 * B * N);
         w.cur = (int*)take(4 * B * N);
