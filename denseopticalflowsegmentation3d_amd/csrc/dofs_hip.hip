@@ -470,6 +470,183 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can
     }
 }
 
+// One-wave form (default; DOFS_LONG_WAVES=3 selects the three-wave kernel below): a single wave64 per
+// long path carries both mean chains (independent, so they interleave), the rank/root recurrence
+// and the bbox. Each step's chain latency grows (~54 vs 41 ns, tools/replay_micro.hip) but the
+// path holds a third of the wave slots, which the graph stage of the next batches running beside it
+// uses: +1.5 % end to end at B = 96 once the graph stage got shorter than the replay stage's slack.
+struct OneRec {  // step record (32 B)
+    float fs, wbx, wby;
+    int meta;  // StepIn meta | kLongOk
+    double r;
+    int lrank, lroot;
+};
+__device__ inline int one_resolve(const Ws& w, int64_t lb, int p, int top, int round, OneRec* o, B4* lbb,
+                                  int accept = -1) {
+    lbb->x0 = lbb->y0 = 0x7fff;
+    lbb->x1 = lbb->y1 = -1;
+    if (p < top) return 0;
+    const StepIn in = w.In[lb + p];
+    int meta = in.meta;
+    o->lrank = 0;
+    o->lroot = in.lb;
+    if (in.meta & kStepDyn) {
+        const int lq = in.lb;
+        const int phase = 2 * round + 1;
+        if (w.ready[lb + lq] >= (p == accept ? phase + 1 : phase)) return meta;
+        const RepVal lv = w.Rv[lb + lq];
+        o->wbx = lv.mx * (float)in.la;
+        o->wby = lv.my * (float)in.la;
+        o->lrank = lv.rank;
+        o->lroot = lv.root;
+        *lbb = lv.bb;
+    } else {
+        o->wbx = in.wbx;
+        o->wby = in.wby;
+        lbb->x0 = lbb->x1 = (int16_t)(in.la & 0xffff);
+        lbb->y0 = lbb->y1 = (int16_t)(in.la >> 16);
+    }
+    meta |= kLongOk;
+    o->fs = in.fs;
+    o->r = in.r;
+    o->meta = meta;
+    return meta;
+}
+
+__device__ void replay_long_path1(const Ws& w, int f, int jj, int round, bool can_wait, OneRec (*buf)[64]) {
+    const Dims& d = w.d;
+    const int j = w.list_long[f * d.N + jj];
+    int* curp = w.cur + f * d.N + j;
+    const int lane = threadIdx.x & 63;
+    int q = *curp;
+    const int top = w.ptop[f * d.N + j];
+    __builtin_amdgcn_wave_barrier();
+    if (q < 0) return;
+    const int64_t lb = f * d.NL;
+    float mx, my;
+    int rank, root;
+    B4 bb;
+    path_start(w, f, q + 1, &mx, &my, &rank, &root, &bb);
+    int cb = 0;
+    OneRec rec;
+    B4 lbb;
+    int meta = one_resolve(w, lb, q - lane, top, round, &rec, &lbb);
+    buf[cb][lane] = rec;
+    for (;;) {
+        OneRec nrec;
+        B4 nlbb;
+        const int nmeta = one_resolve(w, lb, q - 64 - lane, top, round, &nrec, &nlbb);
+        const unsigned long long blocked = __ballot(!(meta & kLongOk));
+        const unsigned long long tops = __ballot((meta & kLongOk) && (meta & kStepTop));
+        const int fb = blocked ? __ffsll((long long)blocked) - 1 : 64;
+        const int ft = tops ? __ffsll((long long)tops) - 1 : 64;
+        const int finished = ft < fb;
+        const int n = finished ? ft + 1 : fb;
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this chunk's LDS records have landed
+        __builtin_amdgcn_wave_barrier();
+        float omx = 0.f, omy = 0.f;
+        int orank = 0, oroot = 0;
+        const OneRec* c = buf[cb];
+#pragma unroll 4
+        for (int k = 0; k < n; ++k) {
+            const OneRec st = c[k];
+            mx = (float)((double)(mx * st.fs + st.wbx) * st.r);
+            my = (float)((double)(my * st.fs + st.wby) * st.r);
+            const int nroot = (st.meta & kStepB) ? (rank > st.lrank ? root : st.lroot)
+                                                 : (st.lrank > rank ? st.lroot : root);
+            rank = (rank == st.lrank) ? rank + 1 : (rank > st.lrank ? rank : st.lrank);
+            root = nroot;
+            omx = lane == k ? mx : omx;
+            omy = lane == k ? my : omy;
+            orank = lane == k ? rank : orank;
+            oroot = lane == k ? root : oroot;
+        }
+        B4 obb;
+        {  // bbox: inclusive prefix join over the chunk (lane = step), then the carried box
+            B4 x = lbb;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const B4 y = bb_shfl_up(x, o);
+                if (lane >= o) x = bb_join(x, y);
+            }
+            x = bb_join(x, bb);
+            obb = x;
+            const int src = n > 0 ? n - 1 : 0;
+            const int lo = __shfl((int)((unsigned short)x.x0 | ((unsigned)(unsigned short)x.y0 << 16)), src, 64);
+            const int hi = __shfl((int)((unsigned short)x.x1 | ((unsigned)(unsigned short)x.y1 << 16)), src, 64);
+            if (n > 0) {
+                bb.x0 = (int16_t)(lo & 0xffff);
+                bb.y0 = (int16_t)(lo >> 16);
+                bb.x1 = (int16_t)(hi & 0xffff);
+                bb.y1 = (int16_t)(hi >> 16);
+            }
+        }
+        if (lane < n) {
+            RepVal o;
+            o.mx = omx;
+            o.my = omy;
+            o.rank = orank;
+            o.root = oroot;
+            o.bb = obb;
+            o.pad0 = o.pad1 = 0;
+            w.Rv[lb + q - lane] = o;
+        }
+        if (finished) {  // publish the top: output stores, agent-scope release, then the flag
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) {
+                *curp = -1;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                __hip_atomic_store(w.ready + lb + top, 2 * round + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            return;
+        }
+        if (n < 64) {  // blocked at pb: wait (bounded) for a long light child of this round, or park
+            const int pb = q - n;
+            int go = 0;
+            if (lane == 0) {
+                const int lq = w.In[lb + pb].lb;
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                int rd;
+                for (;;) {
+                    rd = __hip_atomic_load(w.ready + lb + lq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (!can_wait || rd <= 2 * round + 1 || rd == kIntMax || rd == kParkBase - round) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) break;
+                    __builtin_amdgcn_s_sleep(8);
+                }
+                go = rd <= 2 * round + 1;
+                if (go) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                } else {
+                    *curp = pb;
+                    __hip_atomic_store(w.ready + lb + top, kParkBase - round, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            go = __shfl(go, 0, 64);
+            if (!go) return;
+            q = pb;
+            __builtin_amdgcn_wave_barrier();
+            meta = one_resolve(w, lb, q - lane, top, round, &rec, &lbb, pb);
+            buf[cb][lane] = rec;
+            continue;
+        }
+        q -= 64;
+        cb ^= 1;
+        meta = nmeta;
+        lbb = nlbb;
+        buf[cb][lane] = nrec;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_replay_long1(Ws w, int round, int wait) {
+    __shared__ OneRec buf[2][64];
+    const int f = blockIdx.y;
+    const int n = w.C(f)[C_LONG];
+    const bool can_wait = wait && n <= (int)gridDim.x;
+    for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path1(w, f, jj, round, can_wait, buf);
+}
+
 __global__ __launch_bounds__(192) void k_replay_long(Ws w, int round, int wait) {
     __shared__ LongShared sh;
     const int f = blockIdx.y;
@@ -1884,9 +2061,17 @@ struct HipBackend {
         return n;
     }
     void replay_long(const Ws& w, int round) {
+        static const bool one = [] {  // DOFS_LONG_WAVES=3: the three-wave form (measured ~1.5 % slower)
+            const char* e = getenv("DOFS_LONG_WAVES");
+            return !(e && e[0] == '3');
+        }();
         timed("k_replay_long", [&] {
-            hipLaunchKernelGGL(k_replay_long, dim3((unsigned)long_grid(), (unsigned)w.d.B), dim3(192), 0, stream, w,
-                               round, long_wait() ? 1 : 0);
+            if (one)
+                hipLaunchKernelGGL(k_replay_long1, dim3((unsigned)long_grid(), (unsigned)w.d.B), dim3(64), 0, stream,
+                                   w, round, long_wait() ? 1 : 0);
+            else
+                hipLaunchKernelGGL(k_replay_long, dim3((unsigned)long_grid(), (unsigned)w.d.B), dim3(192), 0, stream,
+                                   w, round, long_wait() ? 1 : 0);
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_replay_long launch");
     }
