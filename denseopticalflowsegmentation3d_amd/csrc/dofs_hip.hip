@@ -2106,7 +2106,19 @@ struct HipBackend {
         int64_t n;
         __device__ void operator()(int f, int64_t i) const { out[f * n + i] -= start[f]; }
     };
-    void scan_excl(const int* in, int* out, int64_t n, int nf) {
+    void scan_excl(const int* in, int* out, int64_t n, int nf) { scan_excl_it(in, out, n, nf); }
+    // leaf ranks in preorder: exclusive scan of (ord[q] < N) read through a transform iterator
+    // (no flag array written by KOrd)
+    struct IsLeaf {
+        int N;
+        __host__ __device__ int operator()(int x) const { return x < N ? 1 : 0; }
+    };
+    void scan_excl_leaf(const int* ord, int* out, int64_t n, int nf, int64_t N) {
+        hipcub::TransformInputIterator<int, IsLeaf, const int*> it(ord, IsLeaf{(int)N});
+        scan_excl_it(it, out, n, nf);
+    }
+    template <class It>
+    void scan_excl_it(It in, int* out, int64_t n, int nf) {
         const int64_t tot = n * nf;
         size_t bytes = 0;
         note(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, (int)tot, stream), "scan size");

@@ -84,7 +84,6 @@ struct Ws {
     unsigned char* lite;    // node is a light child (or the root): the top of a heavy path
     int* pre;               // heavy-first preorder position
     int* ord;
-    int* isleaf;
     int* lscan;
     StepIn* In;
     RepVal* Rv;  // replay outputs by preorder position
@@ -535,8 +534,9 @@ struct KMstEmit {
     }
 };
 
-struct KEdgeInit {
+struct KEdgeInit {  // endpoints by rank; labels = the endpoints (global-kernel KRT only: `labels`)
     Ws w;
+    bool labels;
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
         const int64_t o = f * d.M + i;
@@ -545,6 +545,7 @@ struct KEdgeInit {
         const int64_t q = edge_end(d, p, idx & 3);
         w.EU[o] = (int)p;
         w.EV[o] = (int)q;
+        if (!labels) return;  // the sweep writes every merge's block-start labels
         w.lu[o] = (int)p;
         w.lv[o] = (int)q;
         w.own[o] = 0;
@@ -888,8 +889,7 @@ struct KOrd {
         const Dims& d = w.d;
         const int q = jump_sum(w.J[f * d.NL + x]);
         w.pre[f * d.NL + x] = q;
-        w.ord[f * d.NL + q] = (int)x;
-        w.isleaf[f * d.NL + q] = x < d.N ? 1 : 0;
+        w.ord[f * d.NL + q] = (int)x;  // leaf ranks: scan of (ord < N)
     }
 };
 

@@ -132,7 +132,6 @@ struct Pipeline {
         w.lite = (unsigned char*)take(B * NL);
         w.pre = (int*)take(4 * B * NL);
         w.ord = (int*)take(4 * B * NL);
-        w.isleaf = (int*)take(4 * B * NL);
         w.lscan = (int*)take(4 * B * NL);
         w.In = (StepIn*)take(sizeof(StepIn) * B * NL);
         w.Rv = (RepVal*)take(sizeof(RepVal) * B * NL);
@@ -247,7 +246,7 @@ struct Pipeline {
 
         be.mark(3);
         // K3 Kruskal reconstruction tree
-        be.launch(B, M, KEdgeInit{w});
+        be.launch(B, M, KEdgeInit{w, krt_dnc});
         const bool words = krt_dnc || Backend::kKrtLabelWords;  // the global-kernel KRT reads them
         be.launch(B, words ? NL : N, KLabelInit{w, words});
         const int64_t deep = Backend::deep_block();  // levels with block size <= deep run per block
@@ -283,7 +282,7 @@ struct Pipeline {
         be.launch(B, N, KJumpLeaf{w.J, NL});
         pre = w.pre;
         be.launch(B, NL, KOrd{w});
-        be.scan_excl(w.isleaf, w.lscan, NL, B);
+        be.scan_excl_leaf(w.ord, w.lscan, NL, B, N);
         be.launch(B, N, KLeafOrder{w, pre});
         be.launch(B, d.M, KPathInit{w, pre});
     }

@@ -200,6 +200,15 @@ struct HostBackend {
     void launch(int nf, int64_t n, const F& f) {
         launch_static(nullptr, nf, n, f);
     }
+    void scan_excl_leaf(const int* ord, int* out, int64_t n, int nf, int64_t N) {
+        for (int f = 0; f < nf; ++f) {
+            int s = 0;
+            for (int64_t i = 0; i < n; ++i) {
+                out[f * n + i] = s;
+                s += ord[f * n + i] < N ? 1 : 0;
+            }
+        }
+    }
     void scan_excl(const int* in, int* out, int64_t n, int nf) {
         for (int f = 0; f < nf; ++f) {
             int s = 0;
