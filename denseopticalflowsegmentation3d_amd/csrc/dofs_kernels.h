@@ -950,9 +950,8 @@ struct KPathInit {  // one lane per merge node x = N + k; path ids and lists thr
             }
             w.ready[lb + q] = islong ? kPendLong : kIntMax;
         }
-        const int j = t.take(w.C(f) + C_PATHS, top);
-        const int jl = t.take(w.C(f) + C_LONG, islong);
-        const int js = t.take(w.C(f) + C_SHORT, top && !islong);
+        int j, jl, js;
+        t.take3(w.C(f) + C_PATHS, top, w.C(f) + C_LONG, islong, w.C(f) + C_SHORT, top && !islong, &j, &jl, &js);
         if (top) {
             w.cur[f * d.N + j] = qb - 1;
             w.ptop[f * d.N + j] = q;
@@ -1173,8 +1172,8 @@ struct KLift {
             qual = scored && !(convexity < w.min_convexity[cls]) && score > w.score_threshold;
             w.cscore[f * d.M + j] = qual ? score : -1.0;
         }
-        t.take(w.C(f) + C_SCORED, scored);
-        t.take(w.C(f) + C_QUAL, qual);
+        int unused[3];
+        t.take3(w.C(f) + C_SCORED, scored, w.C(f) + C_QUAL, qual, nullptr, false, unused, unused + 1, unused + 2);
         dofs_agg_max_u64(w.sbest + f * d.N, root, dbits(score), qual);
     }
 };

@@ -179,6 +179,11 @@ struct HostBackend {
     }
     struct HostTaker {  // list append: a plain counter
         int take(int* ctr, bool want) { return want ? (*ctr)++ : -1; }
+        void take3(int* c0, bool w0, int* c1, bool w1, int* c2, bool w2, int* r0, int* r1, int* r2) {
+            *r0 = c0 ? take(c0, w0) : -1;
+            *r1 = c1 ? take(c1, w1) : -1;
+            *r2 = c2 ? take(c2, w2) : -1;
+        }
     };
     template <class F, class = void>
     struct takes : std::false_type {};
