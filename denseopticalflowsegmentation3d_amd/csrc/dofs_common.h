@@ -70,9 +70,9 @@ enum Counter {
     C_MST = 5,
     C_SHORT = 6,
     C_LONG = 7,
-    C_SQ = 8,  // C_SQ + (r & 1): short paths parked in replay round r (ping-pong lists)
-    C_PROG = 10,  // KRT sweep progress (blocks whose labels are published; k_krt_fused)
-    C_FUSE = 11,  // frame 0 only: [C_FUSE] sweep claims, [C_FUSE + 1] LDS-KRT block claims
+    C_SQ = 8,     // C_SQ + (r + 1) % 3: short paths parked in replay round r (three rotating counters)
+    C_PROG = 11,  // KRT sweep progress (blocks whose labels are published; k_krt_fused)
+    C_FUSE = 12,  // frame 0 only: [C_FUSE] sweep claims, [C_FUSE + 1] LDS-KRT block claims
     C_ACT = 16  // C_ACT + r: Borůvka round r found a cross-component edge
 };
 

@@ -222,11 +222,12 @@ __global__ __launch_bounds__(kBlock) void k_generic_take(F f, int64_t n) {
 // list launch: elements [0, min(n, frame counter cidx)) — the bound is read on the device, so a
 // shrinking list costs only the blocks it needs (the others exit at once)
 template <class F>
-__global__ __launch_bounds__(kBlock) void k_counted_take(F f, int64_t n, int cidx) {
+__global__ __launch_bounds__(kBlock) void k_counted_take(F f, int64_t n, int cidx, int zidx) {
     __shared__ int wsum[3 * kBlock / 64];
     __shared__ int base[3];
     BlockTaker t{wsum, base};
     const int fr = blockIdx.y;
+    if (zidx >= 0 && blockIdx.x == 0 && threadIdx.x == 0) f.w.C(fr)[zidx] = 0;  // a counter no block uses here
     const int64_t c = f.w.C(fr)[cidx];
     const int64_t m = c < n ? c : n;
     const int64_t step = (int64_t)gridDim.x * kBlock;
@@ -1967,13 +1968,14 @@ struct HipBackend {
     }
 
     template <class F>
-    void launch_counted(int nf, int64_t n, const F& f, int cidx) {
+    void launch_counted(int nf, int64_t n, const F& f, int cidx, int zidx = -1) {
         if (n <= 0 || nf <= 0) return;
         int64_t gx = (n + kBlock - 1) / kBlock;
         const int64_t cap = grid_cap() > 0 ? std::max<int64_t>(1, grid_cap() / nf) : 8192;
         if (gx > cap) gx = cap;
         timed(functor_name<F>(), [&] {
-            hipLaunchKernelGGL(k_counted_take<F>, dim3((unsigned)gx, (unsigned)nf), dim3(kBlock), 0, stream, f, n, cidx);
+            hipLaunchKernelGGL(k_counted_take<F>, dim3((unsigned)gx, (unsigned)nf), dim3(kBlock), 0, stream, f, n, cidx,
+                               zidx);
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_counted_take launch");
     }

@@ -1088,12 +1088,6 @@ struct KReplay {
     }
 };
 
-struct KCtrZero {  // counter `idx` of every frame = 0
-    Ws w;
-    int idx;
-    DOFS_HD void operator()(int f, int64_t) const { w.C(f)[idx] = 0; }
-};
-
 // State of merge node x after its merge: replay outputs (by preorder position) + size/bbox (KRT).
 DOFS_HD inline NodeVal node_val(const Ws& w, const int* pre, int f, int64_t x) {
     const Dims& d = w.d;

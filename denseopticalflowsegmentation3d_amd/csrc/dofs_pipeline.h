@@ -305,9 +305,10 @@ struct Pipeline {
         int inc = C_SHORT;
         for (int r = 0; r < RR; ++r) {
             if (!(skip_mask & 1)) {
-                const int oc = C_SQ + (r & 1);
-                be.launch(B, 1, KCtrZero{w, oc});
-                be.launch_counted(B, N, KReplay{w, 2 * r, in, inc, park[r & 1], oc}, inc);
+                // round r appends to counter (r + 1) % 3 (zero: the batch's counter reset, or round
+                // r - 1) and zeroes (r + 2) % 3 for round r + 1 (last read by round r - 1)
+                const int oc = C_SQ + (r + 1) % 3;
+                be.launch_counted(B, N, KReplay{w, 2 * r, in, inc, park[r & 1], oc}, inc, C_SQ + (r + 2) % 3);
                 in = park[r & 1];
                 inc = oc;
             }

@@ -159,9 +159,10 @@ struct HostBackend {
         launch_counted(w.d.B, w.d.N, KReplay{w, 2 * r + 1, w.list_long, C_LONG, nullptr, 0}, C_LONG);
     }
     template <class F>
-    void launch_counted(int nf, int64_t n, const F& f, int cidx) {  // elements [0, min(n, counter))
+    void launch_counted(int nf, int64_t n, const F& f, int cidx, int zidx = -1) {  // [0, min(n, counter))
         HostTaker t;
         for (int fr = 0; fr < nf; ++fr) {
+            if (zidx >= 0) f.w.C(fr)[zidx] = 0;
             const int64_t m = std::min<int64_t>(n, f.w.C(fr)[cidx]);
             for (int64_t i = 0; i < m; ++i) f(fr, i, true, t);
         }
