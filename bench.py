@@ -33,44 +33,26 @@ GATHER_PER_FRAME = 64  # box records per frame in the gathered block
 DEEP_BLOCK = int(os.environ.get("DOFS_DEEP_S", "4096"))  # KRT depths with block size <= this run in LDS (k_dnc_deep), the rest globally
 
 # Algorithmic (compulsory) bytes of the probed kernels:
-#   k_boruvka_min (per pixel of a frame still active in that Borůvka pass): its component label (4 B)
-#     and its blurred flow vector (8 B), each read once; neighbours' words are other pixels' own
-#     reads; the per-component minima are LDS-aggregated per tile (not counted).
+#   k_boruvka_min, per pixel of a frame still active in that Borůvka pass:
+#     pass 0: its component label (4 B) and blurred flow (8 B) read once, its kept incident-minimum
+#             candidate (weight 8 B + index 4 B) written once = 24 B (neighbours' words are other
+#             pixels' own reads; the per-component minima are LDS-aggregated per tile);
+#     pass 1: its label (4 B) and kept candidate (12 B) read once = 16 B.
 #   k_dnc_compress (DOFS_KRT_DNC=1 only), per L edge of a depth: own label 4 B, parent 4 B, size 4 B,
 #     component size RMW 8 B, max rank RMW 8 B.
-KERNEL_BYTES = {"k_boruvka_min": 12, "KDncCompress": 28, "k_dnc_compress": 28}
+KERNEL_BYTES = {"k_boruvka_min": (24, 16), "KDncCompress": 28, "k_dnc_compress": 28}
 ROOF_KERNEL = "k_boruvka_min"
 ROUND_FLAG = 16  # counters: C_ACT + r = Borůvka round r found a cross-component edge
 
 
-def boruvka_min_units(counters, N):
-    """Pixels processed per batch by k_boruvka_min: round r >= 1 runs pass 0 for frames whose round
-    r - 1 found an edge and pass 1 for frames whose round r found one (dofs_pipeline.h boruvka())."""
+def boruvka_min_bytes(counters, N):
+    """Algorithmic bytes per batch of k_boruvka_min and its launches: round r >= 1 runs pass 0 for
+    frames whose round r - 1 found an edge and pass 1 for frames whose round r found one
+    (dofs_pipeline.h boruvka())."""
     R = min(ceil_log2(N) + 2, 40 - 1)
     act = counters[:, ROUND_FLAG:ROUND_FLAG + R] != 0
-    frames_launches = int(act[:, 0:R - 1].sum() + act[:, 1:R].sum())
-    return frames_launches * N, 2 * (R - 1)
-
-
-def ceil_log2(n):
-    k = 0
-    while (1 << k) < n:
-        k += 1
-    return k
-
-
-def dnc_L_edges(M):
-    """L edges (lanes doing work) of every global KRT depth launch: block size S > DEEP_BLOCK."""
-    out = []
-    S = 1 << ceil_log2(M)
-    while S > DEEP_BLOCK:
-        h, n = S // 2, 0
-        for s0 in range(0, M, S):
-            if s0 + h < M:
-                n += h
-        out.append(n)
-        S //= 2
-    return out
+    b0, b1 = KERNEL_BYTES["k_boruvka_min"]
+    return int(act[:, 0:R - 1].sum()) * N * b0 + int(act[:, 1:R].sum()) * N * b1, 2 * (R - 1)
 
 
 def parse():
@@ -182,8 +164,7 @@ def main():
                  "launches_per_batch": probe_n / a.steps}
     elif probe_n:
         if a.probe == "k_boruvka_min":
-            units, launches_per_batch = boruvka_min_units(ctx.batch_counters(B), N)
-            alg_batch = units * KERNEL_BYTES[a.probe]
+            alg_batch, launches_per_batch = boruvka_min_bytes(ctx.batch_counters(B), N)
         else:
             per_launch = [n * B * KERNEL_BYTES[a.probe] for n in dnc_L_edges(N - 1)]
             launches_per_batch, alg_batch = len(per_launch), sum(per_launch)
@@ -198,7 +179,9 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                 "kernel": a.probe, "launches": probe_n, "avg_launch_us": round(probe_ms / probe_n * 1e3, 2),
-                "alg_bytes_per_launch": round(alg / probe_n), "alg_bytes_per_unit": KERNEL_BYTES[a.probe],
+                "alg_bytes_per_launch": round(alg / probe_n),
+                "alg_bytes_per_unit": ("24 (pass 0) / 16 (pass 1) per active pixel" if a.probe == "k_boruvka_min"
+                                       else KERNEL_BYTES[a.probe]),
                 "path_input_roofline_frac": None}
 
     # per-stage device-event timing of extra profiled batches (not part of the timed region)

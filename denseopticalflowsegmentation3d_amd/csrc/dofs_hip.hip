@@ -1081,7 +1081,14 @@ __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
 constexpr int kTileX = 32, kTileY = 8, kMinHT = 512;  // 512 > 256 pixels + 82 halo keys per tile (no overflow)
 // Tiles whose pixels have no cross-component edge left are done for good (components only merge):
 // pass 0 marks them in `tdone` (per frame and tile) and later passes skip them.
-__global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass, unsigned char* tdone) {
+// Pass 0: every pixel takes the lexicographic minimum (weight, index) over ALL its incident
+// cross-component edges — the four it emits and the four its neighbours emit towards it — and
+// keeps it (candw / candi); its component's minimum weight is the minimum over its pixels (an edge
+// leaving the component has an end in it), reduced per wave and per tile before one global atomic.
+// Pass 1 then only compares each pixel's kept weight with its component's minimum and reduces the
+// kept indices of the equal ones — no weights recomputed, no neighbour reads.
+__global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass, unsigned char* tdone,
+                                                     unsigned long long* candw, unsigned* candi) {
     __shared__ int hk[kMinHT];
     __shared__ unsigned long long hv[kMinHT];
     __shared__ int any, tany;
@@ -1094,6 +1101,8 @@ __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass, unsi
     const F2* b = w.blur + f * d.N;
     unsigned long long* bw = w.bw + f * d.N;
     unsigned* bi = w.bi + f * d.N;
+    unsigned long long* cw = candw + f * d.N;
+    unsigned* ci = candi + f * d.N;
     const int tid = threadIdx.x;
     for (int x = tid; x < kMinHT; x += 256) {
         hk[x] = -1;
@@ -1117,46 +1126,55 @@ __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass, unsi
         if (td[t]) continue;  // block-uniform
         const int x = (t % tiles_x) * kTileX + (tid % kTileX), y = (t / tiles_x) * kTileY + tid / kTileX;
         int cp = -1;
-        unsigned long long own_best = ~0ull;  // this pixel's candidates for its own component,
-        if (x < d.W && y < d.H) {             // reduced in registers first
+        unsigned long long own = ~0ull;  // pass 0: the pixel's minimum weight; pass 1: its index
+        if (x < d.W && y < d.H) {
             const int64_t p = (int64_t)y * d.W + x;
             cp = comp[p];
-            bool mine = false;
-            unsigned long long cpw = ~0ull;
-            for (int k = 0; k < 4; ++k) {
-                if (!edge_exists(d, x, y, k) || !edge_allowed(w, f, p, k)) continue;
-                const int64_t q = edge_end(d, p, k);
-                const int cq = comp[q];
-                if (cp == cq) continue;
-                const unsigned long long wb = dbits(edge_weight(b, p, q));
-                if (pass && !mine) cpw = bw[cp];
-                mine = true;
-                if (pass == 0) {
-                    own_best = wb < own_best ? wb : own_best;
-                    put(cq, wb);
-                } else {
-                    const unsigned idx = (unsigned)(4 * p + k);
-                    if (wb == cpw) own_best = idx < own_best ? idx : own_best;
-                    if (wb == bw[cq]) put(cq, idx);
-                }
+            if (pass == 0) {
+                unsigned long long best = ~0ull;
+                unsigned bidx = kNoEdge;
+                auto take = [&](int64_t s, int k, int64_t e, int cq) {
+                    if (cq == cp || !edge_allowed(w, f, s, k)) return;
+                    const unsigned long long wb = dbits(edge_weight(b, s, e));
+                    const unsigned idx = (unsigned)(4 * s + k);
+                    if (wb < best || (wb == best && idx < bidx)) {
+                        best = wb;
+                        bidx = idx;
+                    }
+                };
+                for (int k = 0; k < 4; ++k)
+                    if (edge_exists(d, x, y, k)) {
+                        const int64_t q = edge_end(d, p, k);
+                        take(p, k, q, comp[q]);
+                    }
+                if (x + 1 < d.W) take(p + 1, 0, p, comp[p + 1]);                                   // right
+                if (y + 1 < d.H) take(p + d.W, 1, p, comp[p + d.W]);                               // below
+                if (d.nbr8 && x + 1 < d.W && y + 1 < d.H) take(p + d.W + 1, 2, p, comp[p + d.W + 1]);  // down-right
+                if (d.nbr8 && x + 1 < d.W && y >= 1) take(p - d.W + 1, 3, p, comp[p - d.W + 1]);     // up-right
+                cw[p] = best;
+                ci[p] = bidx;
+                own = best;
+                if (bidx != kNoEdge) any = tany = 1;
+            } else {
+                const unsigned long long wb = cw[p];
+                if (wb != ~0ull && wb == bw[cp]) own = ci[p];
             }
-            if (mine && pass == 0) any = tany = 1;
         }
         {  // the lanes of a wave mostly share the component (a tile row of a contiguous region): one
            // put for the first such lane's component, reduced across the lanes that share it
-            const bool has = own_best != ~0ull;
+            const bool has = own != ~0ull;
             const unsigned long long on = __ballot(has);
             if (on) {
                 const int leader = __ffsll((long long)on) - 1;
                 const int c0 = __shfl(cp, leader, 64);
                 const bool same = has && cp == c0;
-                unsigned long long m = same ? own_best : ~0ull;
+                unsigned long long m = same ? own : ~0ull;
                 for (int o = 32; o >= 1; o >>= 1) {
                     const unsigned long long v = __shfl_xor(m, o, 64);
                     m = v < m ? v : m;
                 }
                 if (__lane_id() == leader) put(c0, m);
-                if (has && !same) put(cp, own_best);
+                if (has && !same) put(cp, own);
             }
         }
         __syncthreads();
@@ -2062,8 +2080,10 @@ struct HipBackend {
         static_assert(sizeof(*w.hlB) == 1, "tile flags are bytes");
         if (r == 1 && pass == 0) memset(tdone, 0, (size_t)tiles * w.d.B);  // tiles <= M per frame
         timed("k_boruvka_min", [&] {
+            // kept candidates: the row-blur temporary (8 B per pixel, dead after the blur) and the
+            // MST-count words (written only after the MST)
             hipLaunchKernelGGL(k_boruvka_min, dim3((unsigned)gx, (unsigned)w.d.B), dim3(256), 0, stream, w, r, pass,
-                               tdone);
+                               tdone, reinterpret_cast<unsigned long long*>(w.tmp), reinterpret_cast<unsigned*>(w.cnt));
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_boruvka_min launch");
     }
