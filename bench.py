@@ -55,6 +55,27 @@ def boruvka_min_bytes(counters, N):
     return int(act[:, 0:R - 1].sum()) * N * b0 + int(act[:, 1:R].sum()) * N * b1, 2 * (R - 1)
 
 
+def ceil_log2(n):
+    k = 0
+    while (1 << k) < n:
+        k += 1
+    return k
+
+
+def dnc_L_edges(M):
+    """L edges (lanes doing work) of every global KRT depth launch: block size S > DEEP_BLOCK."""
+    out = []
+    S = 1 << ceil_log2(M)
+    while S > DEEP_BLOCK:
+        h, n = S // 2, 0
+        for s0 in range(0, M, S):
+            if s0 + h < M:
+                n += h
+        out.append(n)
+        S //= 2
+    return out
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)

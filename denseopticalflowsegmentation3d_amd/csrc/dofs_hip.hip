@@ -822,28 +822,28 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
             atomicMax(sh.MX + r, t);
         }
         __syncthreads();
-        for (int t = tid; t < cnt; t += kDeepT) {  // L-roots: sizes of the new components
-            const bool isL = (t & (S - 1)) < half && s0 + (t & ~(S - 1)) + half < d.M;
-            if (!isL) continue;
-            const int r = sh.P[sh.own[t]];
-            if (sh.MX[r] != t) {
-                sh.lrr[t] = -1;
-                continue;
-            }
-            sh.lrr[t] = (short)r;
-            const int sz = sh.CS[r] + sh.SZ[r];
-            sh.SZ[kDeepK + t] = sz;
-            w.SZ[lb + d.N + s0 + t] = sz;
-        }
-        __syncthreads();
-        for (int t = tid; t < cnt; t += kDeepT) {  // relabel R edges
-            if ((t & (S - 1)) < half) continue;
-            for (int side = 0; side < 2; ++side) {
-                short* lp = side ? sh.lv : sh.lu;
-                const int x = lp[t];
-                const int r = sh.P[x];
-                const int li = sh.MX[r];
-                if (r != x || li >= 0) lp[t] = (short)(kDeepK + li);
+        // L-roots: sizes of the new components; R edges: relabel (both only read P, MX, CS)
+        for (int t = tid; t < cnt; t += kDeepT) {
+            if ((t & (S - 1)) < half) {
+                const bool isL = s0 + (t & ~(S - 1)) + half < d.M;
+                if (!isL) continue;
+                const int r = sh.P[sh.own[t]];
+                if (sh.MX[r] != t) {
+                    sh.lrr[t] = -1;
+                    continue;
+                }
+                sh.lrr[t] = (short)r;
+                const int sz = sh.CS[r] + sh.SZ[r];
+                sh.SZ[kDeepK + t] = sz;
+                w.SZ[lb + d.N + s0 + t] = sz;
+            } else {
+                for (int side = 0; side < 2; ++side) {
+                    short* lp = side ? sh.lv : sh.lu;
+                    const int x = lp[t];
+                    const int r = sh.P[x];
+                    const int li = sh.MX[r];
+                    if (r != x || li >= 0) lp[t] = (short)(kDeepK + li);
+                }
             }
         }
         __syncthreads();
