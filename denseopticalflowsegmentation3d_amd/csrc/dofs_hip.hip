@@ -505,11 +505,23 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can
 // and the bbox. Each step's chain latency grows (~54 vs 41 ns, tools/replay_micro.hip) but the
 // path holds a third of the wave slots, which the graph stage of the next batches running beside it
 // uses: +1.5 % end to end at B = 96 once the graph stage got shorter than the replay stage's slack.
-struct OneRec {  // step record (32 B)
-    float fs, wbx, wby;
-    int meta;  // StepIn meta | kLongOk
+// Rank and root of a running set travel as one key K = rank << 27 | root (H*W < 2^26, rank <= 26): the
+// union-by-rank step (step_merge) becomes K' = max(K, LK) for unequal ranks and, for equal ranks,
+// (B ? LK : K) + (1 << 27) — five VALU ops instead of eleven, which matters because one wave issues at
+// most one instruction per four cycles and this loop is issue-bound, not latency-bound.
+constexpr int kRankShift = 27;
+__device__ inline unsigned rk_pack(int rank, int root) { return ((unsigned)rank << kRankShift) | (unsigned)root; }
+struct OneRec {  // step record (32 B; {wbx, wby} first so the packed add reads an aligned pair)
+    float wbx, wby, fs;
+    unsigned lk;   // light child's key (rank << 27 | root)
     double r;
-    int lrank, lroot;
+    unsigned bm;   // kStepB ? ~0 : 0
+    unsigned lkp;  // lk + (1 << 27)
+};
+struct OneOut {  // per-step chain outputs, staged in LDS (one ds_write_b128 per step)
+    float mx, my;
+    unsigned k;
+    unsigned pad;
 };
 __device__ inline int one_resolve(const Ws& w, int64_t lb, int p, int top, int round, OneRec* o, B4* lbb,
                                   int accept = -1) {
@@ -518,8 +530,7 @@ __device__ inline int one_resolve(const Ws& w, int64_t lb, int p, int top, int r
     if (p < top) return 0;
     const StepIn in = w.In[lb + p];
     int meta = in.meta;
-    o->lrank = 0;
-    o->lroot = in.lb;
+    int lrank = 0, lroot = in.lb;
     if (in.meta & kStepDyn) {
         const int lq = in.lb;
         const int phase = 2 * round + 1;
@@ -527,8 +538,8 @@ __device__ inline int one_resolve(const Ws& w, int64_t lb, int p, int top, int r
         const RepVal lv = w.Rv[lb + lq];
         o->wbx = lv.mx * (float)in.la;
         o->wby = lv.my * (float)in.la;
-        o->lrank = lv.rank;
-        o->lroot = lv.root;
+        lrank = lv.rank;
+        lroot = lv.root;
         *lbb = lv.bb;
     } else {
         o->wbx = in.wbx;
@@ -539,11 +550,14 @@ __device__ inline int one_resolve(const Ws& w, int64_t lb, int p, int top, int r
     meta |= kLongOk;
     o->fs = in.fs;
     o->r = in.r;
-    o->meta = meta;
+    o->lk = rk_pack(lrank, lroot);
+    o->lkp = o->lk + (1u << kRankShift);
+    o->bm = (meta & kStepB) ? ~0u : 0u;
     return meta;
 }
 
-__device__ void replay_long_path1(const Ws& w, int f, int jj, int round, bool can_wait, OneRec (*buf)[64]) {
+__device__ void replay_long_path1(const Ws& w, int f, int jj, int round, bool can_wait, OneRec (*buf)[64],
+                                  OneOut* ob) {
     const Dims& d = w.d;
     const int j = w.list_long[f * d.N + jj];
     int* curp = w.cur + f * d.N + j;
@@ -554,9 +568,13 @@ __device__ void replay_long_path1(const Ws& w, int f, int jj, int round, bool ca
     if (q < 0) return;
     const int64_t lb = f * d.NL;
     float mx, my;
-    int rank, root;
+    unsigned K;
     B4 bb;
-    path_start(w, f, q + 1, &mx, &my, &rank, &root, &bb);
+    {
+        int rank, root;
+        path_start(w, f, q + 1, &mx, &my, &rank, &root, &bb);
+        K = rk_pack(rank, root);
+    }
     int cb = 0;
     OneRec rec;
     B4 lbb;
@@ -574,23 +592,30 @@ __device__ void replay_long_path1(const Ws& w, int f, int jj, int round, bool ca
         const int n = finished ? ft + 1 : fb;
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this chunk's LDS records have landed
         __builtin_amdgcn_wave_barrier();
-        float omx = 0.f, omy = 0.f;
-        int orank = 0, oroot = 0;
         const OneRec* c = buf[cb];
-#pragma unroll 4
-        for (int k = 0; k < n; ++k) {
+        auto step = [&](int k) {
             const OneRec st = c[k];
             mx = (float)((double)(mx * st.fs + st.wbx) * st.r);
             my = (float)((double)(my * st.fs + st.wby) * st.r);
-            const int nroot = (st.meta & kStepB) ? (rank > st.lrank ? root : st.lroot)
-                                                 : (st.lrank > rank ? st.lroot : root);
-            rank = (rank == st.lrank) ? rank + 1 : (rank > st.lrank ? rank : st.lrank);
-            root = nroot;
-            omx = lane == k ? mx : omx;
-            omy = lane == k ? my : omy;
-            orank = lane == k ? rank : orank;
-            oroot = lane == k ? root : oroot;
+            unsigned eq = (st.bm & st.lkp) | (~st.bm & (K + (1u << kRankShift)));
+            unsigned ne = K > st.lk ? K : st.lk;
+            asm volatile("" : "+v"(eq), "+v"(ne));  // both arms in registers: a select, not a branch
+            K = (K ^ st.lk) < (1u << kRankShift) ? eq : ne;
+            OneOut o;
+            o.mx = mx;
+            o.my = my;
+            o.k = K;
+            o.pad = 0;
+            ob[k] = o;
+        };
+        int k = 0;
+        for (; k + 4 <= n; k += 4) {  // unrolled by hand (the asm barrier is convergent: no auto-unroll)
+            step(k);
+            step(k + 1);
+            step(k + 2);
+            step(k + 3);
         }
+        for (; k < n; ++k) step(k);
         B4 obb;
         {  // bbox: inclusive prefix join over the chunk (lane = step), then the carried box
             B4 x = lbb;
@@ -611,16 +636,21 @@ __device__ void replay_long_path1(const Ws& w, int f, int jj, int round, bool ca
                 bb.y1 = (int16_t)(hi >> 16);
             }
         }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // the chunk's output records are in LDS
+        __builtin_amdgcn_wave_barrier();
         if (lane < n) {
+            const OneOut so = ob[lane];
             RepVal o;
-            o.mx = omx;
-            o.my = omy;
-            o.rank = orank;
-            o.root = oroot;
+            o.mx = so.mx;
+            o.my = so.my;
+            o.rank = (int)(so.k >> kRankShift);
+            o.root = (int)(so.k & ((1u << kRankShift) - 1));
             o.bb = obb;
             o.pad0 = o.pad1 = 0;
             w.Rv[lb + q - lane] = o;
         }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // ob reads done before the next chunk overwrites it
+        __builtin_amdgcn_wave_barrier();
         if (finished) {  // publish the top: output stores, agent-scope release, then the flag
             __builtin_amdgcn_s_waitcnt(0);
             __builtin_amdgcn_wave_barrier();
@@ -671,10 +701,11 @@ __device__ void replay_long_path1(const Ws& w, int f, int jj, int round, bool ca
 
 __global__ __launch_bounds__(64) void k_replay_long1(Ws w, int round, int wait) {
     __shared__ OneRec buf[2][64];
+    __shared__ OneOut ob[64];
     const int f = blockIdx.y;
     const int n = w.C(f)[C_LONG];
     const bool can_wait = wait && n <= (int)gridDim.x;
-    for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path1(w, f, jj, round, can_wait, buf);
+    for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path1(w, f, jj, round, can_wait, buf, ob);
 }
 
 __global__ __launch_bounds__(192) void k_replay_long(Ws w, int round, int wait) {
