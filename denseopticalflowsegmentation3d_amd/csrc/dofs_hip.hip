@@ -511,17 +511,21 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can
 // most one instruction per four cycles and this loop is issue-bound, not latency-bound.
 constexpr int kRankShift = 27;
 __device__ inline unsigned rk_pack(int rank, int root) { return ((unsigned)rank << kRankShift) | (unsigned)root; }
-struct OneRec {  // step record (32 B; {wbx, wby} first so the packed add reads an aligned pair)
-    float wbx, wby, fs;
-    unsigned lk;   // light child's key (rank << 27 | root)
+struct alignas(16) OneHalf {  // the part of a step record one chain reads: x (even lanes) or y (odd lanes)
     double r;
+    float wb;  // wbx or wby
+    float fs;
+};
+struct OneRec {  // step record (48 B): two reads per lane and step
+    unsigned lk;   // light child's key (rank << 27 | root)
     unsigned bm;   // kStepB ? ~0 : 0
     unsigned lkp;  // lk + (1 << 27)
-};
-struct OneOut {  // per-step chain outputs, staged in LDS (one ds_write_b128 per step)
-    float mx, my;
-    unsigned k;
     unsigned pad;
+    OneHalf h[2];
+};
+struct OneOut {  // per-step chain outputs, staged in LDS (one ds_write_b64 per lane per step)
+    float v;     // mx (h = 0) or my (h = 1)
+    unsigned k;  // key
 };
 __device__ inline int one_resolve(const Ws& w, int64_t lb, int p, int top, int round, OneRec* o, B4* lbb,
                                   int accept = -1) {
@@ -536,20 +540,21 @@ __device__ inline int one_resolve(const Ws& w, int64_t lb, int p, int top, int r
         const int phase = 2 * round + 1;
         if (w.ready[lb + lq] >= (p == accept ? phase + 1 : phase)) return meta;
         const RepVal lv = w.Rv[lb + lq];
-        o->wbx = lv.mx * (float)in.la;
-        o->wby = lv.my * (float)in.la;
+        o->h[0].wb = lv.mx * (float)in.la;
+        o->h[1].wb = lv.my * (float)in.la;
         lrank = lv.rank;
         lroot = lv.root;
         *lbb = lv.bb;
     } else {
-        o->wbx = in.wbx;
-        o->wby = in.wby;
+        o->h[0].wb = in.wbx;
+        o->h[1].wb = in.wby;
         lbb->x0 = lbb->x1 = (int16_t)(in.la & 0xffff);
         lbb->y0 = lbb->y1 = (int16_t)(in.la >> 16);
     }
     meta |= kLongOk;
-    o->fs = in.fs;
-    o->r = in.r;
+    o->h[0].fs = o->h[1].fs = in.fs;
+    o->h[0].r = o->h[1].r = in.r;
+    o->pad = 0;
     o->lk = rk_pack(lrank, lroot);
     o->lkp = o->lk + (1u << kRankShift);
     o->bm = (meta & kStepB) ? ~0u : 0u;
@@ -567,12 +572,16 @@ __device__ void replay_long_path1(const Ws& w, int f, int jj, int round, bool ca
     __builtin_amdgcn_wave_barrier();
     if (q < 0) return;
     const int64_t lb = f * d.NL;
-    float mx, my;
+    const int h = lane & 1;  // even lanes carry the x mean, odd lanes the y mean: one instruction
+                             // stream advances both chains (the wave issues one VALU op per 4 cycles)
+    float v;
     unsigned K;
     B4 bb;
     {
+        float mx, my;
         int rank, root;
         path_start(w, f, q + 1, &mx, &my, &rank, &root, &bb);
+        v = h ? my : mx;
         K = rk_pack(rank, root);
     }
     int cb = 0;
@@ -593,29 +602,36 @@ __device__ void replay_long_path1(const Ws& w, int f, int jj, int round, bool ca
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this chunk's LDS records have landed
         __builtin_amdgcn_wave_barrier();
         const OneRec* c = buf[cb];
-        auto step = [&](int k) {
-            const OneRec st = c[k];
-            mx = (float)((double)(mx * st.fs + st.wbx) * st.r);
-            my = (float)((double)(my * st.fs + st.wby) * st.r);
-            unsigned eq = (st.bm & st.lkp) | (~st.bm & (K + (1u << kRankShift)));
-            unsigned ne = K > st.lk ? K : st.lk;
+        auto step = [&](int k, uint4 a, OneHalf b) {  // a = {lk, bm, lkp}, b = {r, wb, fs}
+            v = (float)((double)(v * b.fs + b.wb) * b.r);
+            const unsigned lk = a.x, bm = a.y, lkp = a.z;
+            unsigned eq = (bm & lkp) | (~bm & (K + (1u << kRankShift)));
+            unsigned ne = K > lk ? K : lk;
             asm volatile("" : "+v"(eq), "+v"(ne));  // both arms in registers: a select, not a branch
-            K = (K ^ st.lk) < (1u << kRankShift) ? eq : ne;
+            K = (K ^ lk) < (1u << kRankShift) ? eq : ne;
             OneOut o;
-            o.mx = mx;
-            o.my = my;
+            o.v = v;
             o.k = K;
-            o.pad = 0;
-            ob[k] = o;
+            ob[2 * k + h] = o;
         };
+        auto lda = [&](int k) { return *reinterpret_cast<const uint4*>(&c[k]); };
         int k = 0;
-        for (; k + 4 <= n; k += 4) {  // unrolled by hand (the asm barrier is convergent: no auto-unroll)
-            step(k);
-            step(k + 1);
-            step(k + 2);
-            step(k + 3);
+        // unrolled by hand (the asm barrier is convergent: no auto-unroll) and software-pipelined: the
+        // next group's records (indices wrapped into the 64-entry buffer) are read while this one runs
+        uint4 a0 = lda(0), a1 = lda(1), a2 = lda(2), a3 = lda(3);
+        OneHalf b0 = c[0].h[h], b1 = c[1].h[h], b2 = c[2].h[h], b3 = c[3].h[h];
+        for (; k + 4 <= n; k += 4) {
+            const int m = (k + 4) & 63;
+            const uint4 na0 = lda(m), na1 = lda(m + 1), na2 = lda(m + 2), na3 = lda(m + 3);
+            const OneHalf nb0 = c[m].h[h], nb1 = c[m + 1].h[h], nb2 = c[m + 2].h[h], nb3 = c[m + 3].h[h];
+            step(k, a0, b0);
+            step(k + 1, a1, b1);
+            step(k + 2, a2, b2);
+            step(k + 3, a3, b3);
+            a0 = na0, a1 = na1, a2 = na2, a3 = na3;
+            b0 = nb0, b1 = nb1, b2 = nb2, b3 = nb3;
         }
-        for (; k < n; ++k) step(k);
+        for (; k < n; ++k) step(k, lda(k), c[k].h[h]);
         B4 obb;
         {  // bbox: inclusive prefix join over the chunk (lane = step), then the carried box
             B4 x = lbb;
@@ -639,12 +655,12 @@ __device__ void replay_long_path1(const Ws& w, int f, int jj, int round, bool ca
         __builtin_amdgcn_s_waitcnt(0xc07f);  // the chunk's output records are in LDS
         __builtin_amdgcn_wave_barrier();
         if (lane < n) {
-            const OneOut so = ob[lane];
+            const OneOut sx = ob[2 * lane], sy = ob[2 * lane + 1];
             RepVal o;
-            o.mx = so.mx;
-            o.my = so.my;
-            o.rank = (int)(so.k >> kRankShift);
-            o.root = (int)(so.k & ((1u << kRankShift) - 1));
+            o.mx = sx.v;
+            o.my = sy.v;
+            o.rank = (int)(sx.k >> kRankShift);
+            o.root = (int)(sx.k & ((1u << kRankShift) - 1));
             o.bb = obb;
             o.pad0 = o.pad1 = 0;
             w.Rv[lb + q - lane] = o;
@@ -701,7 +717,7 @@ __device__ void replay_long_path1(const Ws& w, int f, int jj, int round, bool ca
 
 __global__ __launch_bounds__(64) void k_replay_long1(Ws w, int round, int wait) {
     __shared__ OneRec buf[2][64];
-    __shared__ OneOut ob[64];
+    __shared__ OneOut ob[128];
     const int f = blockIdx.y;
     const int n = w.C(f)[C_LONG];
     const bool can_wait = wait && n <= (int)gridDim.x;
