@@ -1176,35 +1176,60 @@ __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass, unsi
         unsigned long long own = ~0ull;  // pass 0: the pixel's minimum weight; pass 1: its index
         if (x < d.W && y < d.H) {
             const int64_t p = (int64_t)y * d.W + x;
-            cp = comp[p];
             if (pass == 0) {
+                // all loads first, from in-frame addresses (an absent neighbour reads the pixel
+                // itself and is masked below), so the wave waits on memory once per tile instead of
+                // once per edge. Slots 0-3: the edges p emits (left, up, up-left, down-left); 4-7:
+                // the edges its right, lower, lower-right and upper-right neighbours emit towards it.
+                const int64_t W = d.W;
+                const bool xl = x > 0, xr = x + 1 < d.W, yu = y > 0, yd = y + 1 < d.H;
+                const bool ok[8] = {xl, yu, d.nbr8 && xl && yu, d.nbr8 && xl && yd,
+                                    xr, yd, d.nbr8 && xr && yd, d.nbr8 && xr && yu};
+                const int64_t nb[8] = {p - 1, p - W, p - W - 1, p + W - 1, p + 1, p + W, p + W + 1, p - W + 1};
+                int64_t q[8];
+                int cq[8];
+                F2 bq[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) q[j] = ok[j] ? nb[j] : p;
+                cp = comp[p];
+                const F2 bp = b[p];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    cq[j] = comp[q[j]];
+                    bq[j] = b[q[j]];
+                }
+                unsigned allow_bits = 0xff;  // bit j: slot j's edge may be in the MST
+                if (w.allow) {               // launch-uniform
+                    const unsigned char* al = w.allow + f * d.N;
+                    const unsigned ap = al[p];
+                    allow_bits = ap & 0xf;
+#pragma unroll
+                    for (int j = 4; j < 8; ++j) allow_bits |= ((al[q[j]] >> (j - 4)) & 1u) << j;
+                }
                 unsigned long long best = ~0ull;
                 unsigned bidx = kNoEdge;
-                auto take = [&](int64_t s, int k, int64_t e, int cq) {
-                    if (cq == cp || !edge_allowed(w, f, s, k)) return;
-                    const unsigned long long wb = dbits(edge_weight(b, s, e));
-                    const unsigned idx = (unsigned)(4 * s + k);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if (!ok[j] || cq[j] == cp || !((allow_bits >> j) & 1)) continue;
+                    // edge_weight(b, s, e) with s the emitting pixel: float differences, double squares
+                    const F2 bs = j < 4 ? bp : bq[j], be = j < 4 ? bq[j] : bp;
+                    const double dx = bs.x - be.x, dy = bs.y - be.y;
+                    const unsigned long long wb = dbits(sqrt(dx * dx + dy * dy));
+                    const unsigned idx = (unsigned)(4 * (j < 4 ? p : q[j]) + (j & 3));
                     if (wb < best || (wb == best && idx < bidx)) {
                         best = wb;
                         bidx = idx;
                     }
-                };
-                for (int k = 0; k < 4; ++k)
-                    if (edge_exists(d, x, y, k)) {
-                        const int64_t q = edge_end(d, p, k);
-                        take(p, k, q, comp[q]);
-                    }
-                if (x + 1 < d.W) take(p + 1, 0, p, comp[p + 1]);                                   // right
-                if (y + 1 < d.H) take(p + d.W, 1, p, comp[p + d.W]);                               // below
-                if (d.nbr8 && x + 1 < d.W && y + 1 < d.H) take(p + d.W + 1, 2, p, comp[p + d.W + 1]);  // down-right
-                if (d.nbr8 && x + 1 < d.W && y >= 1) take(p - d.W + 1, 3, p, comp[p - d.W + 1]);     // up-right
+                }
                 cw[p] = best;
                 ci[p] = bidx;
                 own = best;
                 if (bidx != kNoEdge) any = tany = 1;
             } else {
+                cp = comp[p];
                 const unsigned long long wb = cw[p];
-                if (wb != ~0ull && wb == bw[cp]) own = ci[p];
+                const unsigned ix = ci[p];  // read beside the weight (one wait, then the minimum)
+                if (wb != ~0ull && wb == bw[cp]) own = ix;
             }
         }
         {  // the lanes of a wave mostly share the component (a tile row of a contiguous region): one
