@@ -716,6 +716,9 @@ __device__ void replay_long_path1(const Ws& w, int f, int jj, int round, bool ca
 }
 
 __global__ __launch_bounds__(64) void k_replay_long1(Ws w, int round, int wait) {
+    // the chain loop issues one instruction per slot it gets: it goes first in its SIMD's arbitration
+    // over the graph-stage waves sharing it (which are memory-bound and lose little)
+    __builtin_amdgcn_s_setprio(3);
     __shared__ OneRec buf[2][64];
     __shared__ OneOut ob[128];
     const int f = blockIdx.y;
