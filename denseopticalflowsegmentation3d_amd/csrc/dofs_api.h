@@ -209,10 +209,13 @@ struct Context {
         p0.krt_dnc = p1.krt_dnc = p2.krt_dnc = kd && kd[0] == '1';
         const char* sp = getenv("DOFS_SPLIT");
         p0.preorder_in_b = p1.preorder_in_b = p2.preorder_in_b = sp && sp[0] == '1';
-        const char* pr = getenv("DOFS_PRIO");  // experiment: 1 = graph stage urgent, replay stage least
-        const bool prio = pr && pr[0] == '1';
-        sA = be.new_stream(prio ? 1 : 0);
-        sB = be.new_stream(prio ? -1 : 0);
+        // stream priorities: DOFS_PRIO=2 (default) replay stage urgent — its workgroups are dispatched
+        // first when a CU frees up, since the replay rounds are the pipeline's critical chain;
+        // 1 = graph stage urgent, replay stage least (experiment); 0 = equal
+        const char* pr = getenv("DOFS_PRIO");
+        const int prio = pr ? atoi(pr) : 2;
+        sA = be.new_stream(prio == 1 ? 1 : 0);
+        sB = be.new_stream(prio == 1 ? -1 : (prio == 2 ? 1 : 0));
         evIn = be.new_event();
         for (int s = 0; s < kSlots; ++s) {
             evA[s] = be.new_event();

@@ -2102,16 +2102,18 @@ struct HipBackend {
     void krt_seq(const Ws& w) {
         if (fused()) {  // sweep + LDS KRT in one persistent launch (k_krt_fused); dnc_deep is a no-op
             launch(w.d.B, w.d.N, KSeqInitRec{reinterpret_cast<SeqRec*>(w.In), 2 * w.d.NL});
-            // persistent workgroups: the frames' sweeps plus `extra` LDS-KRT workers, one per CU
-            // by default (DOFS_FUSED_EXTRA; measured at B = 96: 0 / 32 / 64 / 96 / 160 extra ->
-            // 647 / 729 / 783 / 818 / 823 Mpix/s — the other stream's replay loses little)
+            // persistent workgroups: the frames' sweeps plus `extra` LDS-KRT workers (DOFS_FUSED_EXTRA),
+            // at most one per CU. A workgroup holds a whole CU (151 KB of LDS, all VGPRs), so the
+            // other stream's replay cannot run beside it: by default 1/8 of the CUs stay free for it
+            // (measured at B = 96: 224 workgroups 982 Mpix/s, 256 workgroups 957, 160 workgroups 909)
             static const int extra = [] {
                 const char* e = getenv("DOFS_FUSED_EXTRA");
-                return e ? atoi(e) : 1 << 20;
+                return e ? atoi(e) : -1;
             }();
             int dev_cus = 256;
             (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, device);
-            const int nwg = std::max(1, std::min(dev_cus, w.d.B + extra));
+            const int cap = extra < 0 ? dev_cus - dev_cus / 8 : dev_cus;
+            const int nwg = std::max(1, std::min(cap, extra < 0 ? cap : w.d.B + extra));
             timed("k_krt_fused", [&] {
                 hipLaunchKernelGGL(k_krt_fused, dim3((unsigned)nwg), dim3(kDeepT), 0, stream, w, w.ctr + C_PROG);
             });
