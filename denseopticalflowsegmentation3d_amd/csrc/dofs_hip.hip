@@ -18,6 +18,7 @@
 
 #define DOFS_HD __device__
 #define DOFS_HDM __host__ __device__
+#define DOFS_UNROLL _Pragma("unroll")
 
 __device__ inline int dofs_ld(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ inline void dofs_st(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }

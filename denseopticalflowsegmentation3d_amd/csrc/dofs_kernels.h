@@ -327,25 +327,44 @@ struct KBoruvkaFirst {
         const Dims& d = w.d;
         const int x = (int)(p % d.W), y = (int)(p / d.W);
         const F2* b = w.blur + f * d.N;
+        // all loads first (in-frame addresses; an absent neighbour reads the pixel itself and is
+        // masked), as in k_boruvka_min's pass 0: slots 0-3 the edges p emits (left, up, up-left,
+        // down-left), 4-7 the edges its right, lower, lower-right and upper-right neighbours emit
+        const int64_t W = d.W;
+        const bool xl = x > 0, xr = x + 1 < d.W, yu = y > 0, yd = y + 1 < d.H;
+        const bool ok[8] = {xl, yu, d.nbr8 && xl && yu, d.nbr8 && xl && yd,
+                            xr, yd, d.nbr8 && xr && yd, d.nbr8 && xr && yu};
+        const int64_t nb[8] = {p - 1, p - W, p - W - 1, p + W - 1, p + 1, p + W, p + W + 1, p - W + 1};
+        int64_t q[8];
+        F2 bq[8];
+DOFS_UNROLL
+        for (int j = 0; j < 8; ++j) q[j] = ok[j] ? nb[j] : p;
+        const F2 bp = b[p];
+DOFS_UNROLL
+        for (int j = 0; j < 8; ++j) bq[j] = b[q[j]];
+        unsigned allow_bits = 0xff;  // bit j: slot j's edge may be in the MST
+        if (w.allow) {
+            const unsigned char* al = w.allow + f * d.N;
+            allow_bits = al[p] & 0xfu;
+            for (int j = 4; j < 8; ++j) allow_bits |= ((al[q[j]] >> (j - 4)) & 1u) << j;
+        }
         unsigned long long best = ~0ull;
         unsigned bidx = kNoEdge;
         int64_t far = p;
-        auto take = [&](int64_t s, int k, int64_t e) {
-            if (!edge_allowed(w, f, s, k)) return;
-            const unsigned long long wb = dbits(edge_weight(b, s, e));
-            const unsigned idx = (unsigned)(4 * s + k);
+DOFS_UNROLL
+        for (int j = 0; j < 8; ++j) {
+            if (!ok[j] || !((allow_bits >> j) & 1)) continue;
+            // edge_weight(b, s, e) with s the emitting pixel: float differences, double squares
+            const F2 bs = j < 4 ? bp : bq[j], be = j < 4 ? bq[j] : bp;
+            const double dx = bs.x - be.x, dy = bs.y - be.y;
+            const unsigned long long wb = dbits(sqrt(dx * dx + dy * dy));
+            const unsigned idx = (unsigned)(4 * (j < 4 ? p : q[j]) + (j & 3));
             if (wb < best || (wb == best && idx < bidx)) {
                 best = wb;
                 bidx = idx;
-                far = s == p ? e : s;
+                far = q[j];
             }
-        };
-        for (int k = 0; k < 4; ++k)
-            if (edge_exists(d, x, y, k)) take(p, k, edge_end(d, p, k));
-        if (x + 1 < d.W) take(p + 1, 0, p);                                       // right: its left edge
-        if (y + 1 < d.H) take(p + d.W, 1, p);                                     // below: its up edge
-        if (d.nbr8 && x + 1 < d.W && y + 1 < d.H) take(p + d.W + 1, 2, p);       // down-right: up-left
-        if (d.nbr8 && x + 1 < d.W && y >= 1) take(p - d.W + 1, 3, p);            // up-right: down-left
+        }
         const int64_t o = f * d.N + p;
         w.bw[o] = ~0ull;
         w.bi[o] = kNoEdge;

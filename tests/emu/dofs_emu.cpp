@@ -16,6 +16,7 @@
 
 #define DOFS_HD
 #define DOFS_HDM
+#define DOFS_UNROLL
 inline int dofs_ld(int* p) { return *p; }
 inline void dofs_st(int* p, int v) { *p = v; }
 inline int dofs_cas(int* p, int e, int v) {
