@@ -541,10 +541,17 @@ struct KMstEmit {
         if (!bits) return;
         int64_t j = w.off[f * d.N + p];
         const F2* b = w.blur + f * d.N;
+        // the flow of p and of its MST edges' far ends read together (an unused slot re-reads p)
+        const F2 bp = b[p];
+        F2 bq[4];
+        DOFS_UNROLL
+        for (int k = 0; k < 4; ++k) bq[k] = b[(bits >> k) & 1 ? edge_end(d, p, k) : p];
+        DOFS_UNROLL
         for (int k = 0; k < 4; ++k) {
             if (!(bits & (1 << k))) continue;
             if (j < d.M) {
-                w.key_in[f * d.M + j] = dbits(edge_weight(b, p, edge_end(d, p, k)));
+                const double dx = bp.x - bq[k].x, dy = bp.y - bq[k].y;  // edge_weight(b, p, q)
+                w.key_in[f * d.M + j] = dbits(sqrt(dx * dx + dy * dy));
                 w.val_in[f * d.M + j] = (unsigned)(4 * p + k);
             }
             ++j;
@@ -1317,8 +1324,16 @@ struct KLabel {
     DOFS_HD void operator()(int f, int64_t q) const {
         const Dims& d = w.d;
         const int* seg = w.seg + f * 2 * d.P2;
+        // the leaf-to-root walk's addresses are known up front: eight levels' loads per round are
+        // issued together (levels above the root read the root again, which the walk visits anyway)
         int lab = -1;
-        for (int64_t t = q + d.P2; t >= 1; t >>= 1) lab = seg[t] > lab ? seg[t] : lab;
+        for (int64_t t = q + d.P2; t >= 1; t >>= 8) {
+            int v[8];
+            DOFS_UNROLL
+            for (int k = 0; k < 8; ++k) v[k] = seg[(t >> k) >= 1 ? (t >> k) : 1];
+            DOFS_UNROLL
+            for (int k = 0; k < 8; ++k) lab = v[k] > lab ? v[k] : lab;
+        }
         w.labels[f * d.N + w.leaf_order[f * d.N + q]] = lab;
     }
 };
