@@ -73,6 +73,7 @@ enum Counter {
     C_SQ = 8,     // C_SQ + (r + 1) % 3: short paths parked in replay round r (three rotating counters)
     C_PROG = 11,  // KRT sweep progress (blocks whose labels are published; k_krt_fused)
     C_FUSE = 12,  // frame 0 only: [C_FUSE] sweep claims, [C_FUSE + 1] LDS-KRT block claims
+    C_TINY = 15,  // short heavy paths of at most kTinyPath merges (listed from the back of list_short)
     C_ACT = 16  // C_ACT + r: Borůvka round r found a cross-component edge
 };
 

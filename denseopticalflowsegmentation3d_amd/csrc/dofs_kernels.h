@@ -929,6 +929,7 @@ struct KLeafOrder {
     }
 };
 
+constexpr int kTinyPath = 8;    // short heavy paths of at most this many merges form round 0's first list
 constexpr int kLongPath = 256;  // default: heavy paths at least this long go to the wave-cooperative replay
 // ready[] at a heavy-path top: the replay phase its path completed in, or one of these pending
 // states (all compare >= any phase, i.e. "not ready")
@@ -976,13 +977,21 @@ struct KPathInit {  // one lane per merge node x = N + k; path ids and lists thr
             }
             w.ready[lb + q] = islong ? kPendLong : kIntMax;
         }
+        // short paths in two lists by length, so round 0's waves hold paths of like length (a wave
+        // runs as long as its longest path): tiny ones from the back of list_short, the rest from
+        // its front (together at most one per merge < N: the two never meet)
+        const bool tiny = top && !islong && qb - q <= kTinyPath;
         int j, jl, js;
-        t.take3(w.C(f) + C_PATHS, top, w.C(f) + C_LONG, islong, w.C(f) + C_SHORT, top && !islong, &j, &jl, &js);
+        t.take3(w.C(f) + C_PATHS, top, w.C(f) + C_LONG, islong, w.C(f) + C_SHORT, top && !islong && !tiny, &j, &jl,
+                &js);
+        const int jt = t.take(w.C(f) + C_TINY, tiny);
         if (top) {
             w.cur[f * d.N + j] = qb - 1;
             w.ptop[f * d.N + j] = q;
             if (islong)
                 w.list_long[f * d.N + jl] = j;
+            else if (tiny)
+                w.list_short[f * d.N + d.N - 1 - jt] = j;
             else
                 w.list_short[f * d.N + js] = j;
         }
@@ -1053,7 +1062,8 @@ struct KReplay {
     const int* list;
     int count;  // counter index of list's length (the launch is bounded by it)
     int* out;
-    int outc;   // counter index of out's length
+    int outc;          // counter index of out's length
+    bool rev = false;  // list is filled from the back (the tiny short paths)
     static constexpr bool kBlockTake = true;
     template <class T>
     DOFS_HD void operator()(int f, int64_t jj, bool valid, T& t) const {
@@ -1066,7 +1076,7 @@ struct KReplay {
     }
     DOFS_HD bool advance(int f, int64_t jj, int* jo) const {  // true: parked
         const Dims& d = w.d;
-        const int j = list[f * d.N + jj];
+        const int j = list[f * d.N + (rev ? d.N - 1 - jj : jj)];
         *jo = j;
         int* curp = w.cur + f * d.N + j;
         int q = *curp;

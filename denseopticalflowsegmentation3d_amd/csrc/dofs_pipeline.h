@@ -308,6 +308,8 @@ struct Pipeline {
                 // round r appends to counter (r + 1) % 3 (zero: the batch's counter reset, or round
                 // r - 1) and zeroes (r + 2) % 3 for round r + 1 (last read by round r - 1)
                 const int oc = C_SQ + (r + 1) % 3;
+                if (r == 0)  // the tiny short paths first, then the rest of list_short
+                    be.launch_counted(B, N, KReplay{w, 0, w.list_short, C_TINY, park[0], oc, true}, C_TINY);
                 be.launch_counted(B, N, KReplay{w, 2 * r, in, inc, park[r & 1], oc}, inc, C_SQ + (r + 2) % 3);
                 in = park[r & 1];
                 inc = oc;
