@@ -107,6 +107,18 @@ struct KLiftBatch {
     }
 };
 
+// get_intersect (lifting_3d.cpp:63-89) on the device: the same intersect() the lifting kernels call
+struct KIntersectBatch {
+    const float* pts;  // n x (a1, a2, b1, b2) x (x, y)
+    float* out;        // n x 2
+    DOFS_HD void operator()(int, int64_t i) const {
+        const float* q = pts + 8 * i;
+        P2 r = intersect(mk(q[0], q[1]), mk(q[2], q[3]), mk(q[4], q[5]), mk(q[6], q[7]));
+        out[2 * i] = r.x;
+        out[2 * i + 1] = r.y;
+    }
+};
+
 // Synthetic benchmark flow (DESIGN.md §Synthetic input): splitmix64 noise quantised to 2^-10 in
 // [-0.0996, 0.0996] plus three constant-flow rectangles, jittered by ±5 % for seeds != 0.
 DOFS_HD inline unsigned long long splitmix64(unsigned long long x) {
@@ -369,16 +381,17 @@ int api_fetch(Context<Backend>* cx, int frame, dofs_result* out) {
     out->stats.n_scored = ctr[C_SCORED];
     out->stats.n_qualified = ctr[C_QUAL];
     out->stats.n_snapshots = ns;
-    if (out->snapshots) {
-        if (ns > out->snapshot_capacity || ns > w.snap_cap) return cx->fail(DOFS_ERR_CAPACITY, "snapshot capacity");
-        if (ns) be.d2h(out->snapshots, w.snaps + (int64_t)frame * w.snap_cap, sizeof(dofs_snapshot) * (size_t)ns);
-    } else if (ns > w.snap_cap) {
-        return cx->fail(DOFS_ERR_CAPACITY, "snapshot capacity");
-    }
+    // labels, leaf order and blurred field are exact whatever the snapshot capacity (KPaint is per slot)
     if (out->labels) be.d2h(out->labels, w.labels + (int64_t)frame * d.N, sizeof(int) * (size_t)d.N);
     if (out->leaf_order) be.d2h(out->leaf_order, w.leaf_order + (int64_t)frame * d.N, sizeof(int) * (size_t)d.N);
     if (out->blurred) be.d2h(out->blurred, w.blur + (int64_t)frame * d.N, sizeof(F2) * (size_t)d.N);
     be.sync();
+    if (ns > w.snap_cap || (out->snapshots && ns > out->snapshot_capacity))
+        return cx->fail(DOFS_ERR_CAPACITY, "snapshot capacity");
+    if (out->snapshots && ns) {
+        be.d2h(out->snapshots, w.snaps + (int64_t)frame * w.snap_cap, sizeof(dofs_snapshot) * (size_t)ns);
+        be.sync();
+    }
     return cx->check();
 }
 
@@ -458,6 +471,19 @@ int api_segment(Context<Backend>* cx, const float* flow, int H, int W, size_t st
     return api_fetch(cx, 0, out);
 }
 
+// Snapshot records beyond the per-frame capacity are not written (labels stay exact: KPaint works
+// per slot). A batch that overflowed is reported, never copied silently: waits for the batch and
+// returns DOFS_ERR_CAPACITY if any frame's count exceeded the capacity (C_OVF_ANY); the per-frame
+// counts (C_OVF) say which. Grow it with dofs_set_snapshot_capacity and run the batch again.
+template <class Backend>
+int check_overflow(Context<Backend>* cx, int64_t batch) {
+    const int slot = cx->slot_of(batch);
+    cx->be.event_sync(cx->evDone[slot]);
+    const int ovf = cx->be.read_int(cx->pipe(slot).w.ctr + C_OVF_ANY);
+    if (ovf) return cx->fail(DOFS_ERR_CAPACITY, "snapshot records overflowed the per-frame capacity");
+    return cx->check();
+}
+
 template <class Backend>
 int api_records_copy(Context<Backend>* cx, int64_t batch, void* dst, int per_frame, void* stream) {
     if (!cx->live(batch) || !dst || per_frame < 0) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
@@ -465,6 +491,7 @@ int api_records_copy(Context<Backend>* cx, int64_t batch, void* dst, int per_fra
     const Ws& w = cx->pipe(slot).w;
     const int B = cx->meta[slot].B;
     const int k = per_frame < w.snap_cap ? per_frame : w.snap_cap;
+    if (int rc = check_overflow(cx, batch)) return rc;
     cx->be.set_stream(stream);
     cx->join(batch);
     cx->be.copy2d(dst, sizeof(int), w.ctr + C_SNAP, sizeof(int) * kCounters, sizeof(int), B);
@@ -513,12 +540,35 @@ int api_lift_batch(Context<Backend>* cx, int n, const float* dirs, const int* bo
     return cx->check();
 }
 
+template <class Backend>
+int api_set_snapshot_capacity(Context<Backend>* cx, int64_t cap) {
+    if (cap < 1 || cap > (1 << 24)) return cx->fail(DOFS_ERR_INVALID_ARG, "capacity must be 1 .. 2^24");
+    cx->snap_cap = cap;  // taken by each workspace at its next batch (re-layout)
+    return DOFS_OK;
+}
+
+template <class Backend>
+int api_intersect_batch(Context<Backend>* cx, int n, const float* pts, float* out) {
+    if (n <= 0 || !pts || !out) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
+    cx->be.use_own();
+    const size_t b_in = 32 * (size_t)n, o_out = (b_in + 255) & ~(size_t)255, b_out = 8 * (size_t)n;
+    char* s = (char*)cx->scratch(o_out + b_out);
+    if (!s) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    Backend& be = cx->be;
+    be.h2d(s, pts, b_in);
+    be.launch(1, n, KIntersectBatch{(const float*)s, (float*)(s + o_out)});
+    be.d2h(out, s + o_out, b_out);
+    be.sync();
+    return cx->check();
+}
+
 // plot_best_segments_simple + draw_cube (draw.cpp:85-160) for the frames of batch `batch`:
 // d_frames / d_out = B x H x W x 3 BGR (packed; d_out may equal d_frames). Ordered after the batch
 // on the caller's stream; the edge map belongs to the batch's workspace, so overlays of one batch
 // must be issued on one stream (or before the workspace is reused, batch + slots).
 template <class Backend>
-int api_overlay(Context<Backend>* cx, int64_t batch, const unsigned char* d_frames, unsigned char* d_out) {
+int api_overlay(Context<Backend>* cx, int64_t batch, const unsigned char* d_frames, unsigned char* d_out,
+                bool check = true) {
     if (!cx->live(batch) || !d_frames || !d_out) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
     const int slot = cx->slot_of(batch);
     const typename Context<Backend>::Meta& m = cx->meta[slot];
@@ -535,6 +585,8 @@ int api_overlay(Context<Backend>* cx, int64_t batch, const unsigned char* d_fram
         cx->d_lmap_bytes[slot] = cx->d_lmap[slot] ? lbytes : 0;
         if (!cx->d_lmap[slot]) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
     }
+    if (check)  // cubes are drawn from the snapshot records (the video loop reports counts instead)
+        if (int rc = check_overflow(cx, batch)) return rc;
     OverlayWs o;
     o.frame = d_frames;
     o.out = d_out;
@@ -566,6 +618,9 @@ int api_overlay_host(Context<Backend>* cx, int frame, const unsigned char* bgr, 
     const size_t row = (size_t)m.W * 3, bytes = row * (size_t)m.H;
     if (stride == 0) stride = row;
     if (stride < row) return cx->fail(DOFS_ERR_INVALID_ARG, "row stride too small");
+    cx->be.event_sync(cx->evDone[slot]);
+    if (cx->be.read_int(cx->pipe(slot).w.ctr + (int64_t)frame * kCounters + C_OVF))
+        return cx->fail(DOFS_ERR_CAPACITY, "snapshot records overflowed the per-frame capacity");
     // a one-frame view of the batch: labels / snapshots / counters of `frame`
     unsigned char* d = (unsigned char*)cx->scratch(2 * bytes + 256);
     if (!d) return cx->fail(DOFS_ERR_OOM, "device allocation failed");

@@ -122,6 +122,13 @@ int32_t dofs_batch_counters(dofs_ctx* ctx, int32_t* out, int64_t capacity) {
     return ctx->check();
 }
 
+int32_t dofs_set_snapshot_capacity(dofs_ctx* ctx, int32_t per_frame) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    return dofs::api_set_snapshot_capacity(ctx, per_frame);
+}
+
+int32_t dofs_snapshot_capacity(dofs_ctx* ctx) { return ctx ? (int32_t)ctx->snap_cap : -1; }
+
 int64_t dofs_batch_count(dofs_ctx* ctx) { return ctx ? ctx->nbatch : -1; }
 
 int32_t dofs_batch_slots(dofs_ctx* ctx) { return ctx ? ctx->nslots : -1; }
@@ -166,6 +173,11 @@ int32_t dofs_lift_batch(dofs_ctx* ctx, int32_t n, const float* dirs, const int32
                         const float mat[9], const float inv[9], const float inv_upper[27], dofs_solution* out) {
     if (!ctx) return DOFS_ERR_INVALID_ARG;
     return dofs::api_lift_batch(ctx, n, dirs, boxes, cls, mat, inv, inv_upper, out);
+}
+
+int32_t dofs_intersect_batch(dofs_ctx* ctx, int32_t n, const float* pts, float* out) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    return dofs::api_intersect_batch(ctx, n, pts, out);
 }
 
 int32_t dofs_synth_flow_device(float* d_out, int32_t B, int32_t H, int32_t W, uint64_t seed0, void* stream) {

@@ -74,6 +74,8 @@ enum Counter {
     C_PROG = 11,  // KRT sweep progress (blocks whose labels are published; k_krt_fused)
     C_FUSE = 12,  // frame 0 only: [C_FUSE] sweep claims, [C_FUSE + 1] LDS-KRT block claims
     C_TINY = 15,  // short heavy paths of at most kTinyPath merges (listed from the back of list_short)
+    C_OVF = 14,   // snapshot count of a frame whose records overflowed the capacity (0: no overflow)
+    C_OVF_ANY = 10,  // frame 0 only: 1 if any frame of the batch overflowed
     C_ACT = 16  // C_ACT + r: Borůvka round r found a cross-component edge
 };
 

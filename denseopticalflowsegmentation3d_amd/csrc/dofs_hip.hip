@@ -1916,6 +1916,12 @@ struct HipBackend {
         note(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync D2H");
     }
     void sync() { note(hipStreamSynchronize(stream), "hipStreamSynchronize"); }
+    // one device int, read synchronously (the caller has waited for the work that wrote it)
+    int read_int(const int* d) {
+        int v = 0;
+        note(hipMemcpy(&v, d, sizeof(int), hipMemcpyDeviceToHost), "hipMemcpy D2H");
+        return v;
+    }
     void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height) {
         note(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToDevice, stream),
              "hipMemcpy2DAsync");
@@ -2424,7 +2430,8 @@ int video_clip(dofs_ctx* ctx, const unsigned char* d_bgr, int n, int H, int W, i
         const int64_t id = ctx->nbatch - 1;
         ctx->be.set_stream(v.so);
         if (d_overlay) {
-            rc = dofs::api_overlay(ctx, id, d_bgr + (int64_t)(i + 1) * N * 3, d_overlay + (int64_t)i * N * 3);
+            rc = dofs::api_overlay(ctx, id, d_bgr + (int64_t)(i + 1) * N * 3, d_overlay + (int64_t)i * N * 3,
+                                   false);
             if (rc != DOFS_OK) return rc;
         } else {
             ctx->join(id);

@@ -1282,7 +1282,12 @@ struct KSnapCount {
     DOFS_HD void operator()(int f, int64_t) const {
         const Dims& d = w.d;
         const int64_t last = f * d.N + d.N - 1;
-        w.C(f)[C_SNAP] = w.soff[last] + w.sflag[last];
+        const int n = w.soff[last] + w.sflag[last];
+        w.C(f)[C_SNAP] = n;
+        if (n > w.snap_cap) {  // records beyond the capacity are not written: reported, never silent
+            w.C(f)[C_OVF] = n;
+            dofs_st(w.C(0) + C_OVF_ANY, 1);
+        }
     }
 };
 
@@ -1310,19 +1315,25 @@ struct KSegInit {
     DOFS_HD void operator()(int f, int64_t t) const { w.seg[f * 2 * w.d.P2 + t] = -1; }
 };
 
+// One lane per history slot (not per compacted snapshot record), so the labels stay exact whatever
+// the snapshot-record capacity: a slot with a winning event paints its member range if its score
+// (the slot's arg-max score bits, KLift) exceeds the overlay threshold.
 struct KPaint {
     Ws w;
-    DOFS_HD void operator()(int f, int64_t k) const {
+    const int* pre;
+    DOFS_HD void operator()(int f, int64_t s) const {
         const Dims& d = w.d;
-        const int n = w.C(f)[C_SNAP];
-        if (k >= n || k >= w.snap_cap) return;
-        const dofs_snapshot& sn = w.snaps[(int64_t)f * w.snap_cap + k];
-        if (!(sn.score > w.overlay_min_score)) return;
+        const int i = w.sevent[f * d.N + s];
+        if (i == kIntMax) return;
+        if (!(bitsd(w.sbest[f * d.N + s]) > w.overlay_min_score)) return;
+        const int64_t x = d.N + i;
+        const int begin = w.lscan[f * d.NL + pre[f * d.NL + x]];
+        const int size = w.SZ[f * d.NL + x];
         int* seg = w.seg + f * 2 * d.P2;
-        int64_t l = sn.seg_begin + d.P2, r = (int64_t)sn.seg_begin + sn.size + d.P2;
+        int64_t l = begin + d.P2, r = (int64_t)begin + size + d.P2;
         while (l < r) {
-            if (l & 1) dofs_amax(seg + l++, sn.slot);
-            if (r & 1) dofs_amax(seg + --r, sn.slot);
+            if (l & 1) dofs_amax(seg + l++, (int)s);
+            if (r & 1) dofs_amax(seg + --r, (int)s);
             l >>= 1;
             r >>= 1;
         }

@@ -332,7 +332,7 @@ struct Pipeline {
         be.mark(7);
         // K7 overlay labels
         be.launch(B, 2 * d.P2, KSegInit{w});
-        be.launch(B, snap_cap, KPaint{w});
+        be.launch(B, N, KPaint{w, pre});
         be.launch(B, N, KLabel{w});
         be.mark(8);
     }

@@ -69,6 +69,10 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_batch_records_copy_id.restype = C.c_int32
     L.dofs_batch_counters.argtypes = [C.c_void_p, _ip, C.c_int64]
     L.dofs_batch_counters.restype = C.c_int32
+    L.dofs_set_snapshot_capacity.argtypes = [C.c_void_p, C.c_int32]
+    L.dofs_set_snapshot_capacity.restype = C.c_int32
+    L.dofs_snapshot_capacity.argtypes = [C.c_void_p]
+    L.dofs_snapshot_capacity.restype = C.c_int32
     L.dofs_batch_count.argtypes = [C.c_void_p]
     L.dofs_batch_count.restype = C.c_int64
     L.dofs_batch_slots.argtypes = [C.c_void_p]
@@ -85,6 +89,8 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_lift.restype = C.c_int32
     L.dofs_lift_batch.argtypes = [C.c_void_p, C.c_int32, _fp, _ip, _ip, _fp, _fp, _fp, C.POINTER(DofsSolution)]
     L.dofs_lift_batch.restype = C.c_int32
+    L.dofs_intersect_batch.argtypes = [C.c_void_p, C.c_int32, _fp, _fp]
+    L.dofs_intersect_batch.restype = C.c_int32
     L.dofs_synth_flow_device.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_uint64, C.c_void_p]
     L.dofs_synth_flow_device.restype = C.c_int32
     if hasattr(L, "dofs_farneback"):  # the optical-flow stage (HIP build; the test emulator has none)
@@ -280,6 +286,13 @@ class Dofs:
         self._err(self.lib.dofs_batch_counters(self.ctx, _p(out, C.c_int32), out.size), "dofs_batch_counters")
         return out
 
+    def set_snapshot_capacity(self, per_frame: int) -> None:
+        """Per-frame snapshot-record capacity of the batch API (default 4096)."""
+        self._err(self.lib.dofs_set_snapshot_capacity(self.ctx, per_frame), "dofs_set_snapshot_capacity")
+
+    def snapshot_capacity(self) -> int:
+        return int(self.lib.dofs_snapshot_capacity(self.ctx))
+
     def batch_count(self) -> int:
         return int(self.lib.dofs_batch_count(self.ctx))
 
@@ -328,6 +341,13 @@ class Dofs:
                                       _p(_f32(mat).ravel()), _p(_f32(inv).ravel()), _p(_f32(inv_upper27).ravel()),
                                       out.ctypes.data_as(C.POINTER(DofsSolution)))
         self._err(rc, "dofs_lift_batch")
+        return out
+
+    def intersect_batch(self, pts) -> np.ndarray:
+        """get_intersect on the device for n queries (n x 4 x 2 points: a1, a2, b1, b2) -> n x 2."""
+        pts = _f32(pts).reshape(-1, 8)
+        out = np.zeros((len(pts), 2), np.float32)
+        self._err(self.lib.dofs_intersect_batch(self.ctx, len(pts), _p(pts), _p(out)), "dofs_intersect_batch")
         return out
 
     # ---- overlay (downstream of the path; SURVEY.md §8(f) #2) ----

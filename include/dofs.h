@@ -195,11 +195,17 @@ int32_t dofs_segment_masked_device(dofs_ctx* ctx, const float* d_flow, int32_t H
 int32_t dofs_batch_records_device(dofs_ctx* ctx, void** d_records, void** d_counts, int32_t* capacity);
 
 /* Copy the batch's box records to a caller device buffer on `stream`: int32 counts[B] (snapshots per
- * frame), then B × per_frame dofs_box_record (the first per_frame records of each frame). */
+ * frame), then B × per_frame dofs_box_record (the first per_frame records of each frame).
+ * Capacity: each frame keeps at most dofs_snapshot_capacity() records (default 4096). Waits on the
+ * host for the batch to finish, then returns DOFS_ERR_CAPACITY (copying nothing) if any frame's
+ * snapshot count exceeded it — records are never dropped silently. The labels are exact either way. */
 int32_t dofs_batch_records_copy(dofs_ctx* ctx, void* d_dst, int32_t per_frame, void* stream);
 /* Same for batch id `batch` (one of the last three issued); ordered after that batch on `stream`. */
 int32_t dofs_batch_records_copy_id(dofs_ctx* ctx, int64_t batch, void* d_dst, int32_t per_frame,
                                    void* stream);
+/* Per-frame snapshot-record capacity of the batch API (taken by each workspace at its next batch). */
+int32_t dofs_set_snapshot_capacity(dofs_ctx* ctx, int32_t per_frame);
+int32_t dofs_snapshot_capacity(dofs_ctx* ctx);
 /* Number of batches issued on ctx (the last batch id + 1). */
 int64_t dofs_batch_count(dofs_ctx* ctx);
 /* Number of batch workspaces (batches whose results stay readable; a caller that reads batch k's
@@ -232,6 +238,9 @@ int32_t dofs_lift_batch(dofs_ctx* ctx, int32_t n, const float* dirs, const int32
 
 /* get_intersect (host code, exact float semantics of lifting_3d.cpp:63-89). */
 void dofs_intersect(const float a1[2], const float a2[2], const float b1[2], const float b2[2], float out[2]);
+/* The same on the device (the intersect() the lifting kernels use): pts = n x {a1, a2, b1, b2} x {x, y}
+ * (8 floats per query), out = n x 2. Synchronous. */
+int32_t dofs_intersect_batch(dofs_ctx* ctx, int32_t n, const float* pts, float* out);
 
 /* ---- Upstream of the path: dense optical flow --------------------------------
  * dofs_farneback ← cv::calcOpticalFlowFarneback(prev, next, flow, pyr_scale, levels, winsize,
@@ -268,7 +277,8 @@ int32_t dofs_bgr_to_gray_device(const uint8_t* d_bgr, int64_t n_pixels, uint8_t*
  *   bev, forest, 0.7) (:258) — decode and display are the caller's. d_bgr = n_frames x H x W x 3 BGR
  *   uint8 (device). Pair p = (frame p, frame p + 1) writes, for frame p + 1:
  *     d_overlay + p*H*W*3     the overlay (H x W x 3; NULL = skip),
- *     d_counts[p]             its snapshot count (NULL = skip),
+ *     d_counts[p]             its snapshot count (NULL = skip; a count above the snapshot capacity
+ *                             means its records and cubes were truncated — the loop does not wait to check),
  *     d_records + p*per_frame its first per_frame 3D-box records (NULL = skip).
  *   Pairs run in chunks of `batch` through dofs_farneback_batch_device and the two-stage segment
  *   pipeline, the Farneback of one chunk overlapping the segmentation of the previous one. Asynchronous
@@ -288,7 +298,8 @@ int32_t dofs_video_clip_device(dofs_ctx* ctx, const uint8_t* d_bgr, int32_t n_fr
  *   (cv::line, thickness 1, 8-connected) into frame and painted copy, then
  *   addWeighted(frame, 0.6, seg, 0.4, 0). d_frames / d_out = B x H x W x 3 BGR uint8 (packed) of
  *   batch id `batch` (one of the last dofs_batch_slots issued); d_out may equal d_frames (the
- *   reference draws into `frame`). Asynchronous on `stream`, ordered after the batch.
+ *   reference draws into `frame`). Asynchronous on `stream`, ordered after the batch; waits on the host
+ *   for the batch and returns DOFS_ERR_CAPACITY if a frame's snapshots overflowed the capacity.
  * dofs_overlay: the same for frame `frame` of the last batch, host buffers (row stride in bytes,
  *   0 = packed W*3; out is packed). Synchronous. */
 int32_t dofs_overlay_batch_device(dofs_ctx* ctx, int64_t batch, const uint8_t* d_frames, uint8_t* d_out,

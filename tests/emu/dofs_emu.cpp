@@ -77,6 +77,7 @@ struct HostBackend {
     void* new_event() { return nullptr; }
     void record(void*, void*) {}
     void wait(void*, void*) {}
+    int read_int(const int* d) { return *d; }
     void event_sync(void*) {}
     bool profiling() const { return false; }
     void* alloc(size_t bytes) { return malloc(bytes); }
