@@ -1,13 +1,21 @@
 """Benchmark: Mpixels/s of segment + lifting_3d on synthetic 1080p flow fields (BASELINE.json metric).
 
-One step = one batch of `--batch` synthetic 1920x1080 flow fields per GPU pushed through the whole
-HIP path (blur → MST → Kruskal replay → per-merge filters + 3D lifting → snapshots → labels), then
-the fixed-size 3D-box records of every frame gathered to all ranks (RCCL all_gather over xGMI when
-N > 1). Inputs are generated on device before timing (resident in HBM); frames are independent, so
-ranks shard frames with no data-path collective besides the box gather ("scaling": "weak").
+Default (weak scaling, the driver's `--gpus N --steps K --warmup W`): one step = one batch of `--batch`
+synthetic 1920x1080 flow fields PER GPU pushed through the whole HIP path (blur → MST → Kruskal
+replay → per-merge filters + 3D lifting → snapshots → labels), then the fixed-size 3D-box records of
+every frame gathered to all ranks (RCCL all_gather over xGMI when N > 1). Inputs are generated on
+device before timing (resident in HBM); frames are independent, so ranks shard frames with no
+data-path collective besides the box gather ("scaling": "weak").
 
-Usage: python bench.py [--gpus N --steps K --warmup W --batch B]
-       (N > 1 under torch.distributed.run, one process per GPU)
+`--frames F` (BASELINE config 4: F = 512): a fixed job of F frames split over the N ranks (contiguous
+blocks, frame f = seed f), each rank running its share in batches of at most `--batch`; one step = the
+whole job ("scaling": "strong").
+
+N > 1: run under torch.distributed.run (one process per GPU), or pass `--gpus N` alone and this script
+launches torch.distributed.run itself (as a child process, before any GPU call). It never reports
+fewer GPUs than asked for: a mismatch exits non-zero.
+
+Usage: python bench.py [--gpus N --steps K --warmup W --batch B --frames F]
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -15,44 +23,33 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
-from denseopticalflowsegmentation3d_amd import runtime  # noqa: E402
-from denseopticalflowsegmentation3d_amd.abi import default_params  # noqa: E402
-from denseopticalflowsegmentation3d_amd.frames import FrameParallel  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 GATHER_PER_FRAME = 64  # box records per frame in the gathered block
-DEEP_BLOCK = int(os.environ.get("DOFS_DEEP_S", "4096"))  # KRT depths with block size <= this run in LDS (k_dnc_deep), the rest globally
+ROUNDS_MAX = 40        # dofs_common.h kRoundsMax (Borůvka round flags and tile census entries per frame)
+ROUND_FLAG = 16        # counters: C_ACT + r = Borůvka round r found a cross-component edge
+C_LONGM = 57           # counters: merges on long heavy paths
 
-# Algorithmic (compulsory) bytes of the probed kernels:
-#   k_boruvka_min, per pixel of a frame still active in that Borůvka pass:
-#     pass 0: its component label (4 B) and blurred flow (8 B) read once, its kept incident-minimum
-#             candidate (weight 8 B + index 4 B) written once = 24 B (neighbours' words are other
-#             pixels' own reads; the per-component minima are LDS-aggregated per tile);
-#     pass 1: its label (4 B) and kept candidate (12 B) read once = 16 B.
-#   k_dnc_compress (DOFS_KRT_DNC=1 only), per L edge of a depth: own label 4 B, parent 4 B, size 4 B,
-#     component size RMW 8 B, max rank RMW 8 B.
-KERNEL_BYTES = {"k_boruvka_min": (24, 16), "KDncCompress": 28, "k_dnc_compress": 28}
+# Algorithmic (compulsory) bytes of the probed kernels, per unit:
+#   k_boruvka_min — unit: a pixel of a tile the launch processes (tiles found done are skipped;
+#     dofs_batch_tile_pixels says which): pass 0 reads its component label (4 B) and blurred flow (8 B)
+#     and writes its kept incident-minimum candidate (weight 8 B + index 4 B) = 24 B; pass 1 reads its
+#     label and kept candidate = 16 B. Neighbours' words are other pixels' own reads.
+#   k_krt_fused — unit: a merge: its endpoints in (8 B), its node size out (4 B), two child seed words
+#     of the preorder's pointer jumping out (16 B), heavy/light and path-top flags out (3 B), and one
+#     16-B union-find record of the sweep read = 47 B.
+#   k_replay_long — unit: a merge on a long heavy path: its step inputs (StepIn, 32 B) in and its
+#     replay record (RepVal, 32 B) out = 64 B (a light merge child's 32-B record read is not counted).
+BYTES = {"k_boruvka_min": (24, 16), "k_krt_fused": 47, "k_replay_long": 64}
+PROBES = ("k_boruvka_min", "k_krt_fused", "k_replay_long")
 ROOF_KERNEL = "k_boruvka_min"
-ROUND_FLAG = 16  # counters: C_ACT + r = Borůvka round r found a cross-component edge
-
-
-def boruvka_min_bytes(counters, N):
-    """Algorithmic bytes per batch of k_boruvka_min and its launches: round r >= 1 runs pass 0 for
-    frames whose round r - 1 found an edge and pass 1 for frames whose round r found one
-    (dofs_pipeline.h boruvka())."""
-    R = min(ceil_log2(N) + 2, 40 - 1)
-    act = counters[:, ROUND_FLAG:ROUND_FLAG + R] != 0
-    b0, b1 = KERNEL_BYTES["k_boruvka_min"]
-    return int(act[:, 0:R - 1].sum()) * N * b0 + int(act[:, 1:R].sum()) * N * b1, 2 * (R - 1)
 
 
 def ceil_log2(n):
@@ -62,63 +59,184 @@ def ceil_log2(n):
     return k
 
 
-def dnc_L_edges(M):
-    """L edges (lanes doing work) of every global KRT depth launch: block size S > DEEP_BLOCK."""
-    out = []
-    S = 1 << ceil_log2(M)
-    while S > DEEP_BLOCK:
-        h, n = S // 2, 0
-        for s0 in range(0, M, S):
-            if s0 + h < M:
-                n += h
-        out.append(n)
-        S //= 2
-    return out
+def boruvka_rounds(N):
+    return min(ceil_log2(N) + 2, ROUNDS_MAX - 1)
 
 
-def parse():
+def boruvka_min_units(tile_px, counters, N):
+    """(pass-0 pixels, pass-1 pixels, launches) of k_boruvka_min over one batch.
+
+    tile_px[f][m] = pixels of frame f's tiles found done by round m's pass 0 (m >= 1): processed by
+    pass 0 in rounds 1..m and by pass 1 in rounds 1..m-1. m = 0 (never found done): processed by every
+    launch that ran for the frame (pass 0 of round r runs if round r - 1 found an edge, pass 1 of round
+    r if round r did; dofs_pipeline.h boruvka())."""
+    R = boruvka_rounds(N)
+    p0 = p1 = 0
+    for f in range(tile_px.shape[0]):
+        act = counters[f, ROUND_FLAG:ROUND_FLAG + R] != 0
+        for m in range(1, R):
+            px = int(tile_px[f, m])
+            p0 += px * m
+            p1 += px * (m - 1)
+        px = int(tile_px[f, 0])
+        p0 += px * int(act[0:R - 1].sum())
+        p1 += px * int(act[1:R].sum())
+    return p0, p1, 2 * (R - 1)
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=96, help="frames per GPU per step")
+    ap.add_argument("--batch", type=int, default=96, help="frames per GPU per step (--frames: per batch)")
+    ap.add_argument("--frames", type=int, default=0, help="fixed job of F frames over all GPUs (config 4: 512)")
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--cpu-frames", type=int, default=1, help="frames of the CPU baseline sample (0 = skip)")
+    ap.add_argument("--cpu-frames", type=int, default=1, help="frames per CPU-baseline process (0 = skip)")
+    ap.add_argument("--cpu-procs", type=int, default=0, help="concurrent CPU-baseline processes (0 = auto)")
+    ap.add_argument("--cpu-opt", default="O2,O0", help="oracle builds timed for the CPU baseline")
     ap.add_argument("--no-stages", action="store_true", help="skip the per-stage event timing pass")
-    ap.add_argument("--probe", default=ROOF_KERNEL, help="kernel timed with device events for the roofline")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01", "pmc_summary.json"),
-                    help="PMC summary JSON (tools/pmc_summary.py) for roofline.traffic")
-    return ap.parse_args()
+    ap.add_argument("--no-h2d", action="store_true", help="skip the with-H2D (host input) pass")
+    ap.add_argument("--probe", default=",".join(PROBES), help="kernels timed with device events (comma list)")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02", "pmc_summary.json"),
+                    help="PMC summary JSON (tools/pmc_summary.py) for the roofline traffic")
+    ap.add_argument("--cpu-worker", nargs=4, metavar=("OPT", "H", "W", "SEED"), help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(H, W, frames):
-    """Reference-faithful CPU restatement (oracle mode 1: std::multiset / std::set structures, -O2,
-    one thread) on a bounded sample of the same workload."""
+# ---- CPU baseline (oracle = the reference-faithful CPU restatement; test infrastructure) ---------------
+def cpu_worker(opt, H, W, seed):
+    """One frame of the faithful CPU restatement (std::multiset edge sort, std::set unions, set-copy
+    snapshots), one thread; prints its seconds."""
     from oracle import binding as ob
     persp, inv, up = ob.calib()
-    total = 0.0
-    for s in range(frames):
-        flow = ob.synth_flow(H, W, s)
+    flow = ob.synth_flow(H, W, seed)
+    t0 = time.perf_counter()
+    ob.segment(flow, persp, inv, up, mode=1, opt=opt)
+    print(f"{time.perf_counter() - t0:.6f}", flush=True)
+
+
+def _cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _mem_avail_gb():
+    try:
+        for ln in open("/proc/meminfo"):
+            if ln.startswith("MemAvailable:"):
+                return int(ln.split()[1]) / 1048576
+    except OSError:
+        pass
+    return 16.0
+
+
+def cpu_baseline(a):
+    """`procs` concurrent single-thread processes (the reference is single-threaded; one frame per core),
+    capped by the box's CPU share (16 per GPU) and by ~1.5 GB of host RAM per 1080p frame; each runs
+    --cpu-frames synthetic frames of the bench workload. Runs before this process touches the GPU."""
+    from oracle import binding as ob
+    H, W = a.height, a.width
+    share = len(os.sched_getaffinity(0))
+    per_frame_gb = 1.5 * H * W / 2073600
+    procs = a.cpu_procs or max(1, min(16, share, int(_mem_avail_gb() * 0.5 / per_frame_gb)))
+    out = {"unit": "Mpixels/sec", "kind": "port", "cores": procs, "nproc": os.cpu_count(), "affinity": share,
+           "cpu_model": _cpu_model()}
+    for opt in a.cpu_opt.split(","):
+        ob.lib(opt)  # built before timing
         t0 = time.perf_counter()
-        ob.segment(flow, persp, inv, up, mode=1)
-        total += time.perf_counter() - t0
-    return {"value": round(frames * H * W / total / 1e6, 4), "unit": "Mpixels/sec", "cores": 1, "kind": "port",
-            "sample": f"{frames} synthetic {W}x{H} frame(s) (seed 0..{frames - 1}), faithful mode "
-                      f"(std::multiset edge sort + std::set unions + set-copy snapshots), g++ -O2, "
-                      f"{total:.1f} s"}
+        per = []
+        for k in range(a.cpu_frames):  # `procs` frames at a time, one per process
+            ps = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", opt, str(H), str(W),
+                                    str(p * a.cpu_frames + k)], stdout=subprocess.PIPE, text=True)
+                  for p in range(procs)]
+            for p in ps:
+                o, _ = p.communicate()
+                if p.returncode != 0:
+                    raise RuntimeError(f"cpu baseline worker failed ({p.returncode})")
+                per.append(float(o.split()[-1]))
+        wall = time.perf_counter() - t0
+        frames = procs * a.cpu_frames
+        per.sort()
+        out[opt] = {"value": round(frames * H * W / wall / 1e6, 4), "frames": frames, "wall_s": round(wall, 2),
+                    "s_per_frame": {"min": round(per[0], 2), "median": round(per[len(per) // 2], 2),
+                                    "max": round(per[-1], 2)},
+                    "single_core_mpix_s": round(H * W / per[len(per) // 2] / 1e6, 4)}
+    first = a.cpu_opt.split(",")[0]
+    out["value"] = out[first]["value"]
+    out["sample"] = (f"{procs} concurrent processes x {a.cpu_frames} synthetic {W}x{H} frame(s) each (seeds "
+                     f"0..{procs * a.cpu_frames - 1}), faithful mode (std::multiset edge sort + std::set unions + "
+                     f"set-copy snapshots), one thread per process; value = {first} build; g++ "
+                     + " and ".join(f"-{o}: {out[o]['wall_s']} s wall" for o in a.cpu_opt.split(",")))
+    return out
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+# ---- launcher --------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(a, argv):
+    """--gpus N > 1 without a launcher: start torch.distributed.run as a child process (nothing here has
+    touched the GPU) and exit with its status."""
+    import torch
+    n = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if n < a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but only {n} device(s) visible", file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ---- GPU bench -------------------------------------------------------------------------------------------
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if a.cpu_worker:
+        opt, H, W, seed = a.cpu_worker
+        cpu_worker(opt, int(H), int(W), int(seed))
+        return 0
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0:
+        if a.gpus > 1:
+            return self_launch(a, argv)
+        world = 1
+    if world != a.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}", file=sys.stderr)
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    cpu = None
+    if world == 1 and rank == 0 and a.cpu_frames > 0:  # before any GPU call: the workers are child processes
+        cpu = cpu_baseline(a)
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from denseopticalflowsegmentation3d_amd import runtime
+    from denseopticalflowsegmentation3d_amd.abi import default_params
+    from denseopticalflowsegmentation3d_amd.frames import FrameParallel, frame_shard
+
     if world > 1:
         dist.init_process_group("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    B, H, W = a.batch, a.height, a.width
+    H, W = a.height, a.width
     N = H * W
 
     ctx = runtime.Dofs(local)
@@ -126,24 +244,46 @@ def main():
     prm = default_params()
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
-
-    flows = torch.empty((B, H, W, 2), dtype=torch.float32, device=dev)
-    runtime.synth_flow_device(flows.data_ptr(), B, H, W, seed0=rank * B, stream=sh)
     fp = FrameParallel(ctx, world, GATHER_PER_FRAME)
-    pending = []
     lag = ctx.batch_slots() - 1
 
-    # one step = submit a batch, then gather the records of the batch submitted `lag` steps before
-    # (the context overlaps earlier batches' replay stages with this batch's graph stage); flush()
-    # gathers the rest.
-    def step():
-        pending.append(fp.submit(flows, persp, inv, up, params=prm, stream=sh))
+    if a.frames:  # config 4: a fixed job split over the ranks
+        mine = frame_shard(a.frames, rank, world)
+        per_rank = -(-a.frames // world)
+        flows = torch.empty((max(len(mine), 1), H, W, 2), dtype=torch.float32, device=dev)
+        if len(mine):
+            runtime.synth_flow_device(flows.data_ptr(), len(mine), H, W, seed0=mine.start, stream=sh)
+        chunks = [(s, min(a.batch, per_rank - s)) for s in range(0, per_rank, a.batch)]
+        frames_per_step = a.frames
+        B = chunks[0][1]
+    else:
+        B = a.batch
+        flows = torch.empty((B, H, W, 2), dtype=torch.float32, device=dev)
+        runtime.synth_flow_device(flows.data_ptr(), B, H, W, seed0=rank * B, stream=sh)
+        chunks = [(0, B)]
+        frames_per_step = world * B
+
+    pending = []
+
+    def submit(s, n, src=None):
+        # ranks with fewer real frames (F not a multiple of N) still run every chunk (the gather is
+        # collective); their padding frames repeat the first frame and are not counted in `value`
+        v = (src if src is not None else flows)
+        n_real = max(1, min(n, v.shape[0] - s))
+        part = v[s:s + n_real] if n_real == n else torch.cat([v[s:s + n_real], v[:n - n_real]])
+        pending.append(fp.submit(part, persp, inv, up, params=prm, stream=sh))
         if len(pending) > lag:
             fp.collect(pending.pop(0), stream=sh)
 
     def flush():
         while pending:
             fp.collect(pending.pop(0), stream=sh)
+
+    def step(src=None):
+        for s, n in chunks:
+            submit(s, n, src)
+        if a.frames:  # one step = the whole job
+            flush()
 
     for _ in range(a.warmup):
         step()
@@ -152,62 +292,109 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ctx.probe(a.probe)
-    ctx.probe_read()
+    ctx.probe_read_n(8)
+    ev_step = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
     t0 = time.perf_counter()
-    e0.record(stream)
-    for _ in range(a.steps):
+    ev_step[0].record(stream)
+    for k in range(a.steps):
         step()
+        ev_step[k + 1].record(stream)
     flush()
+    e1 = torch.cuda.Event(enable_timing=True)
     e1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    ms_ev = e0.elapsed_time(e1)
-    probe_ms, probe_n = ctx.probe_read()
+    ms_ev = ev_step[0].elapsed_time(e1)
+    per_step = sorted(ev_step[k].elapsed_time(ev_step[k + 1]) for k in range(a.steps))
+    probes = dict(zip(a.probe.split(","), ctx.probe_read_n(8))) if a.probe else {}
     ctx.probe(None)
     t = torch.tensor([max(wall, ms_ev / 1e3)], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    frames = world * B * a.steps
-    value = frames * N / elapsed / 1e6
+    value = frames_per_step * a.steps * N / elapsed / 1e6
 
-    # roofline of the probed kernel: algorithmic bytes of its launches in the timed region over their
-    # device-event time (events recorded on the stream the kernel runs on)
+    # roofline: algorithmic bytes of each probed kernel's launches in the timed region over their
+    # device-event time (events recorded on the stream the kernel runs on); units from the last batch
+    # (every batch of the bench is the same workload shape)
+    counters = ctx.batch_counters(chunks[-1][1])
+    tiles = ctx.tile_pixels(chunks[-1][1])
+    pmc = {}
+    if a.pmc and os.path.exists(a.pmc):
+        pj = json.load(open(a.pmc))
+        if pj.get("batch") == B and pj.get("height", H) == H and pj.get("width", W) == W:
+            pmc = pj.get("kernels", {})
+    batches = a.steps * len(chunks)
+    kern = []
+    for name, (ms, launches) in probes.items():
+        if not launches:
+            continue
+        entry = {"kernel": name, "ms_per_batch": round(ms / batches, 3), "launches": launches,
+                 "avg_launch_us": round(ms / launches * 1e3, 2),
+                 "share_of_step": round(ms / a.steps / (elapsed * 1e3 / a.steps), 4)}
+        alg = None
+        if name == "k_boruvka_min" and len(chunks) == 1:
+            p0, p1, lpb = boruvka_min_units(tiles, counters, N)
+            assert launches == lpb * batches, (launches, lpb, batches)
+            alg = (p0 * BYTES[name][0] + p1 * BYTES[name][1]) * batches
+            entry["alg_bytes_per_unit"] = "24 (pass 0) / 16 (pass 1) per pixel of a processed tile"
+            entry["units_per_batch"] = {"pass0_px": p0, "pass1_px": p1}
+        elif name == "k_krt_fused" and len(chunks) == 1:
+            alg = BYTES[name] * (N - 1) * B * batches
+            entry["alg_bytes_per_unit"] = f"{BYTES[name]} per merge"
+        elif name == "k_replay_long" and len(chunks) == 1:
+            alg = BYTES[name] * int(counters[:, C_LONGM].sum()) * batches
+            entry["alg_bytes_per_unit"] = f"{BYTES[name]} per long-path merge"
+            entry["units_per_batch"] = int(counters[:, C_LONGM].sum())
+        if alg is not None:
+            ach = alg / (ms / 1e3) / 1e9
+            entry.update({"achieved": round(ach, 3), "frac": round(ach / HBM_PEAK_GBS, 6),
+                          "alg_bytes_per_launch": round(alg / launches)})
+            pk = pmc.get(name)
+            if pk:
+                entry["traffic"] = pk["hbm_bytes_per_launch"]
+                entry["traffic_over_alg"] = round(pk["hbm_bytes_per_launch"] / (alg / launches), 3)
+        kern.append(entry)
+    kern.sort(key=lambda e: -e["ms_per_batch"])
     roof = None
-    probe = None
-    if probe_n and a.probe not in KERNEL_BYTES:  # a kernel without a roofline model: its time only
-        probe = {"kernel": a.probe, "ms_per_batch": round(probe_ms / a.steps, 3),
-                 "launches_per_batch": probe_n / a.steps}
-    elif probe_n:
-        if a.probe == "k_boruvka_min":
-            alg_batch, launches_per_batch = boruvka_min_bytes(ctx.batch_counters(B), N)
-        else:
-            per_launch = [n * B * KERNEL_BYTES[a.probe] for n in dnc_L_edges(N - 1)]
-            launches_per_batch, alg_batch = len(per_launch), sum(per_launch)
-        assert launches_per_batch and probe_n == launches_per_batch * a.steps, (probe_n, launches_per_batch)
-        alg = alg_batch * a.steps
-        achieved = alg / (probe_ms / 1e3) / 1e9
-        traffic = None
-        if a.pmc and os.path.exists(a.pmc):
-            pm = json.load(open(a.pmc))
-            if pm.get("kernel") == a.probe and pm.get("batch") == B:
-                traffic = pm["hbm_bytes_per_launch"]
-        roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                "kernel": a.probe, "launches": probe_n, "avg_launch_us": round(probe_ms / probe_n * 1e3, 2),
-                "alg_bytes_per_launch": round(alg / probe_n),
-                "alg_bytes_per_unit": ("24 (pass 0) / 16 (pass 1) per active pixel" if a.probe == "k_boruvka_min"
-                                       else KERNEL_BYTES[a.probe]),
-                "path_input_roofline_frac": None}
+    main_k = next((e for e in kern if e["kernel"] == ROOF_KERNEL and "achieved" in e), None)
+    if main_k:
+        roof = {"bound": "hbm", "achieved": main_k["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": main_k["frac"], "traffic": main_k.get("traffic"), "kernel": ROOF_KERNEL,
+                "launches": main_k["launches"], "avg_launch_us": main_k["avg_launch_us"],
+                "alg_bytes_per_launch": main_k["alg_bytes_per_launch"],
+                "alg_bytes_per_unit": main_k["alg_bytes_per_unit"],
+                "top_kernels_by_time": kern[:3],
+                "path_input_roofline_frac": round(frames_per_step * a.steps * N * 8 / world / elapsed / 1e9
+                                                  / HBM_PEAK_GBS, 8)}
+
+    # with host input: each batch's flow fields copied H2D from pinned host memory on the caller stream
+    # before the call (two device buffers in turn), the PCIe-inclusive rate (never `value`)
+    h2d = None
+    if not a.no_h2d and not a.frames:
+        host = flows.cpu().pin_memory()
+        dbuf = [flows, torch.empty_like(flows)]
+        hs = max(3, a.steps // 2)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for k in range(hs):
+            d = dbuf[k & 1]
+            d.copy_(host, non_blocking=True)
+            step(d)
+        flush()
+        torch.cuda.synchronize()
+        th = time.perf_counter() - t1
+        h2d = {"value": round(world * B * hs * N / th / 1e6, 3), "unit": "Mpixels/sec", "steps": hs,
+               "ms_per_step": round(th / hs * 1e3, 3)}
+        del host
 
     # per-stage device-event timing of extra profiled batches (not part of the timed region)
     stages = None
-    if not a.no_stages:
+    if not a.no_stages and not a.frames:
         ctx.profile(True)
         for _ in range(max(2, a.steps // 2)):
             step()
@@ -216,11 +403,17 @@ def main():
         ms, nb = ctx.profile_read()
         ctx.profile(False)
         stages = {k: round(v / nb, 3) for k, v in ms.items()}
-    if roof is not None:  # the north star's whole-path figure: 8 B/px input read over the wall time
-        roof["path_input_roofline_frac"] = round(B * a.steps * N * 8 / elapsed / 1e9 / HBM_PEAK_GBS, 8)
 
     if rank == 0:
         res = ctx.fetch(0, want_blur=False)
+        med = per_step[len(per_step) // 2]
+        cfg = {"workload": (f"{a.frames} synthetic {W}x{H} flow fields over {world} GPU(s) (BASELINE config 4), "
+                            f"full segment + lifting_3d" if a.frames else
+                            f"{W}x{H} synthetic flow, full segment + lifting_3d (BASELINE config 3 shape)"),
+               "frames_per_step": frames_per_step, "frames_per_gpu_per_batch": B,
+               "frames_per_sec": round(frames_per_step * a.steps / elapsed, 3),
+               "parallelism": f"frame-parallel x{world}", "snapshots_frame0": int(len(res.snapshots)),
+               "candidates_frame0": int(res.stats["n_candidates"])}
         out = {
             "metric": "Mpixels/sec segment+lifting_3d @1080p",
             "value": round(value, 3),
@@ -229,28 +422,26 @@ def main():
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "ms_per_step_median": round(med, 3),
+            "ms_per_step_p10_p90": [round(per_step[len(per_step) // 10], 3),
+                                    round(per_step[min(len(per_step) - 1, (9 * len(per_step)) // 10)], 3)],
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if a.frames else "weak",
             "vs_baseline": None,
             "dtype": "f32+f64",
-            "data": "synthetic (on-device splitmix64 flow fields, DESIGN.md §Synthetic input)",
-            "config": {"workload": f"{W}x{H} synthetic flow, full segment + lifting_3d (BASELINE config 3 shape)",
-                       "frames_per_gpu_per_step": B, "frames_per_sec": round(frames / elapsed, 3),
-                       "parallelism": f"frame-parallel x{world}", "snapshots_frame0": int(len(res.snapshots)),
-                       "candidates_frame0": int(res.stats["n_candidates"])},
+            "data": "synthetic (on-device splitmix64 flow fields, SURVEY.md §8(d) spec)",
+            "config": cfg,
             "roofline": roof,
+            "with_h2d": h2d,
             "stages_ms_per_batch": stages,
-            "cpu_baseline": None,
+            "cpu_baseline": cpu,
         }
-        if probe is not None:
-            out["probe"] = probe
-        if world == 1 and a.cpu_frames > 0:
-            out["cpu_baseline"] = cpu_baseline(H, W, a.cpu_frames)
         print(json.dumps(out), flush=True)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

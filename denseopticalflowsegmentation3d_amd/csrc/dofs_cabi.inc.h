@@ -161,6 +161,25 @@ int32_t dofs_probe_read(dofs_ctx* ctx, double* ms, int64_t* launches) {
     return ctx->check();
 }
 
+int32_t dofs_probe_read_n(dofs_ctx* ctx, int32_t n, double* ms, int64_t* launches) {
+    if (!ctx || !ms || n < 0) return -DOFS_ERR_INVALID_ARG;
+    ctx->drain();
+    const int k = ctx->be.probe_read_n(n, ms, launches);
+    return ctx->check() == DOFS_OK ? k : -DOFS_ERR_DEVICE;
+}
+
+int32_t dofs_batch_tile_pixels(dofs_ctx* ctx, int32_t* out, int64_t capacity) {
+    if (!ctx || !out || !ctx->have_batch()) return DOFS_ERR_INVALID_ARG;
+    const int slot = ctx->last_slot();
+    const int64_t n = (int64_t)ctx->meta[slot].B * dofs::kRoundsMax;
+    if (capacity < n) return DOFS_ERR_CAPACITY;
+    ctx->be.use_own();
+    ctx->join(ctx->nbatch - 1);
+    ctx->be.d2h(out, ctx->pipe(slot).w.tpx, sizeof(int32_t) * (size_t)n);
+    ctx->be.sync();
+    return ctx->check();
+}
+
 int32_t dofs_lift(dofs_ctx* ctx, const float dir[2], const int32_t box[4], const float mat[9], const float inv[9],
                   const float inv_upper[9], int32_t cls, dofs_solution* out) {
     if (!ctx || cls < 0 || cls > 2 || !inv_upper) return DOFS_ERR_INVALID_ARG;

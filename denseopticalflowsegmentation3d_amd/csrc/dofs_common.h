@@ -75,8 +75,9 @@ enum Counter {
     C_FUSE = 12,  // frame 0 only: [C_FUSE] sweep claims, [C_FUSE + 1] LDS-KRT block claims
     C_TINY = 15,  // short heavy paths of at most kTinyPath merges (listed from the back of list_short)
     C_OVF = 14,   // snapshot count of a frame whose records overflowed the capacity (0: no overflow)
-    C_OVF_ANY = 10,  // frame 0 only: 1 if any frame of the batch overflowed
-    C_ACT = 16  // C_ACT + r: Borůvka round r found a cross-component edge
+    C_ACT = 16,  // C_ACT + r: Borůvka round r found a cross-component edge (r < kRoundsMax)
+    C_OVF_ANY = 56,  // frame 0 only: 1 if any frame of the batch overflowed its snapshot records
+    C_LONGM = 57     // merges on long heavy paths (replayed by the wave-per-path kernel)
 };
 
 constexpr uint32_t kNoEdge = 0xFFFFFFFFu;

@@ -1255,7 +1255,7 @@ __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass, unsi
         }
         __syncthreads();
         if (pass == 0 && tid == 0) {
-            if (!tany) td[t] = 1;
+            if (!tany) td[t] = (unsigned char)r;  // r >= 1: the last round that processed the tile
             tany = 0;
         }
         for (int x = tid; x < kMinHT; x += 256) {
@@ -1273,6 +1273,28 @@ __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass, unsi
         __syncthreads();
     }
     if (pass == 0 && tid == 0 && any) w.C(f)[C_ACT + r] = 1;
+}
+
+// Pixels of each frame's tiles by the round whose pass 0 found them done (0: never marked): tile t
+// marked at round m was processed by pass 0 of rounds 1..m and pass 1 of rounds 1..m-1, so the host
+// charges k_boruvka_min's bytes for exactly the pixels it touched (bench.py).
+__global__ __launch_bounds__(256) void k_tile_hist(Ws w, const unsigned char* tdone) {
+    __shared__ int bins[kRoundsMax];
+    const Dims& d = w.d;
+    const int f = blockIdx.y;
+    const int tiles_x = (d.W + kTileX - 1) / kTileX;
+    const int tiles = tiles_x * ((d.H + kTileY - 1) / kTileY);
+    for (int k = threadIdx.x; k < kRoundsMax; k += blockDim.x) bins[k] = 0;
+    __syncthreads();
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < tiles; t += gridDim.x * blockDim.x) {
+        const int tx = t % tiles_x, ty = t / tiles_x;
+        const int px = min(kTileX, d.W - tx * kTileX) * min(kTileY, d.H - ty * kTileY);
+        const int m = tdone[(int64_t)f * tiles + t];
+        atomicAdd(bins + (m < kRoundsMax ? m : 0), px);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < kRoundsMax; k += blockDim.x)
+        if (bins[k]) atomicAdd(w.tpx + (int64_t)f * kRoundsMax + k, bins[k]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2005,46 +2027,78 @@ struct HipBackend {
     static int launch_static(void* s, int nf, int64_t n, const F& f) {
         return launch_on((hipStream_t)s, nf, n, f);
     }
-    // ---- kernel probe: device events around every launch of one named per-element kernel ----
-    std::string probe_name;
-    std::vector<std::array<hipEvent_t, 2>> probe_ev;
-    double probe_ms_acc = 0;
-    int64_t probe_launches = 0;
+    // ---- kernel probe: device events around every launch of the named kernels ----------------
+    // names: comma-separated kernel names (functor names of dofs_kernels.h or the HIP kernels'
+    // names passed to timed()); per name, the accumulated event time and launch count
+    std::vector<std::string> probe_names;
+    std::vector<std::pair<int, std::array<hipEvent_t, 2>>> probe_ev;
+    std::vector<double> probe_ms_acc;
+    std::vector<int64_t> probe_launches;
     template <class F>
     static const char* type_name() {
         return __PRETTY_FUNCTION__;  // "... [F = dofs::KDncCompress]"
     }
-    void probe(const char* name) { probe_name = name ? name : ""; }
-    int64_t probe_read(double* ms) {
-        for (auto& e : probe_ev) {
+    void probe(const char* names) {
+        probe_names.clear();
+        std::string s = names ? names : "";
+        size_t a = 0;
+        while (a < s.size()) {
+            size_t b = s.find(',', a);
+            if (b == std::string::npos) b = s.size();
+            if (b > a) probe_names.push_back(s.substr(a, b - a));
+            a = b + 1;
+        }
+        probe_ms_acc.assign(probe_names.size(), 0.0);
+        probe_launches.assign(probe_names.size(), 0);
+    }
+    // per probed name: ms[i], launches[i] (n entries at most); returns the number of names
+    int probe_read_n(int n, double* ms, int64_t* launches) {
+        for (auto& pe : probe_ev) {
+            auto& e = pe.second;
             note(hipEventSynchronize(e[1]), "hipEventSynchronize");
             float t = 0.f;
             note(hipEventElapsedTime(&t, e[0], e[1]), "hipEventElapsedTime");
-            probe_ms_acc += t;
-            ++probe_launches;
+            probe_ms_acc[pe.first] += t;
+            ++probe_launches[pe.first];
             pool.push_back(e[0]);
             pool.push_back(e[1]);
         }
         probe_ev.clear();
-        *ms = probe_ms_acc;
-        const int64_t n = probe_launches;
-        probe_ms_acc = 0;
-        probe_launches = 0;
+        const int k = (int)probe_names.size();
+        for (int i = 0; i < k && i < n; ++i) {
+            ms[i] = probe_ms_acc[i];
+            if (launches) launches[i] = probe_launches[i];
+            probe_ms_acc[i] = 0;
+            probe_launches[i] = 0;
+        }
+        return k;
+    }
+    int64_t probe_read(double* ms) {  // the first probed name
+        int64_t n = 0;
+        *ms = 0;
+        std::vector<double> m(probe_names.size() + 1);
+        std::vector<int64_t> l(probe_names.size() + 1);
+        if (probe_read_n((int)probe_names.size(), m.data(), l.data()) > 0) {
+            *ms = m[0];
+            n = l[0];
+        }
         return n;
     }
     // run `fn` (which enqueues one kernel on `stream`) between probe events if `name` is probed
     template <class Fn>
     void timed(const std::string& name, Fn&& fn) {
-        const bool probed = !probe_name.empty() && name == probe_name;
+        int idx = -1;
+        for (size_t i = 0; i < probe_names.size(); ++i)
+            if (probe_names[i] == name) idx = (int)i;
         std::array<hipEvent_t, 2> ev{};
-        if (probed) {
+        if (idx >= 0) {
             ev = {ev_get(), ev_get()};
             note(hipEventRecord(ev[0], stream), "hipEventRecord");
         }
         fn();
-        if (probed) {
+        if (idx >= 0) {
             note(hipEventRecord(ev[1], stream), "hipEventRecord");
-            probe_ev.push_back(ev);
+            probe_ev.push_back({idx, ev});
         }
     }
     template <class F>
@@ -2061,7 +2115,7 @@ struct HipBackend {
         auto fn = [&] {
             if (launch_on(stream, nf, n, f) != DOFS_OK) note(hipErrorLaunchFailure, "kernel launch");
         };
-        if (probe_name.empty())
+        if (probe_names.empty())
             fn();
         else
             timed(functor_name<F>(), fn);
@@ -2170,6 +2224,14 @@ struct HipBackend {
                                tdone, reinterpret_cast<unsigned long long*>(w.tmp), reinterpret_cast<unsigned*>(w.cnt));
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_boruvka_min launch");
+    }
+    void boruvka_tiles(const Ws& w) {
+        const int64_t tiles = (int64_t)((w.d.W + kTileX - 1) / kTileX) * ((w.d.H + kTileY - 1) / kTileY);
+        memset(w.tpx, 0, sizeof(int) * kRoundsMax * (size_t)w.d.B);
+        if (w.d.N <= 1) return;  // no Borůvka round ran (the tile flags were never cleared)
+        const unsigned gx = (unsigned)std::min<int64_t>((tiles + 255) / 256, 64);
+        hipLaunchKernelGGL(k_tile_hist, dim3(gx, (unsigned)w.d.B), dim3(256), 0, stream, w, (const unsigned char*)w.hlB);
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_tile_hist launch");
     }
     void dnc_compress(const Ws& w, int64_t S, int ep) {
         int64_t gx = (w.d.M + kAggT - 1) / kAggT;

@@ -110,6 +110,8 @@ struct Ws {
     int snap_cap;
     // counters (stride kCounters)
     int* ctr;
+    // pixels of the Borůvka tiles by the round that found them done (stride kRoundsMax; 0: never)
+    int* tpx;
     // parameters
     LiftMats L;
     int min_size;
@@ -976,6 +978,7 @@ struct KPathInit {  // one lane per merge node x = N + k; path ids and lists thr
                 islong = qb - q >= w.long_path;
             }
             w.ready[lb + q] = islong ? kPendLong : kIntMax;
+            if (islong) dofs_aadd(w.C(f) + C_LONGM, qb - q);
         }
         // short paths in two lists by length, so round 0's waves hold paths of like length (a wave
         // runs as long as its longest path): tiny ones from the back of list_short, the rest from

@@ -152,6 +152,7 @@ struct Pipeline {
         w.snaps = (dofs_snapshot*)take(sizeof(dofs_snapshot) * B * snap_cap);
         w.recs = (dofs_box_record*)take(sizeof(dofs_box_record) * B * snap_cap);
         w.ctr = (int*)take(4 * B * kCounters);
+        w.tpx = (int*)take(4 * B * kRoundsMax);
         w.snap_cap = (int)snap_cap;
         return off + 256;
     }
@@ -190,6 +191,7 @@ struct Pipeline {
             }
             be.boruvka_relabel(w, r);  // KBoruvkaRelabelFind
         }
+        be.boruvka_tiles(w);  // HIP: pixels per tile-done round (the roofline's processed-pixel count)
     }
 
     // Minimum spanning forest of the row band [r0, r1) of an H x W frame (edges with both ends in the

@@ -85,6 +85,10 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_probe.restype = C.c_int32
     L.dofs_probe_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
     L.dofs_probe_read.restype = C.c_int32
+    L.dofs_probe_read_n.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+    L.dofs_probe_read_n.restype = C.c_int32
+    L.dofs_batch_tile_pixels.argtypes = [C.c_void_p, _ip, C.c_int64]
+    L.dofs_batch_tile_pixels.restype = C.c_int32
     L.dofs_lift.argtypes = [C.c_void_p, _fp, _ip, _fp, _fp, _fp, C.c_int32, C.POINTER(DofsSolution)]
     L.dofs_lift.restype = C.c_int32
     L.dofs_lift_batch.argtypes = [C.c_void_p, C.c_int32, _fp, _ip, _ip, _fp, _fp, _fp, C.POINTER(DofsSolution)]
@@ -321,6 +325,21 @@ class Dofs:
         ms, n = C.c_double(), C.c_int64()
         self._err(self.lib.dofs_probe_read(self.ctx, C.byref(ms), C.byref(n)), "dofs_probe_read")
         return ms.value, n.value
+
+    def probe_read_n(self, n: int) -> list[tuple[float, int]]:
+        """Per probed kernel (the order given to probe(), comma-separated): (ms, launches); resets."""
+        ms = (C.c_double * max(n, 1))()
+        ln = (C.c_int64 * max(n, 1))()
+        k = self.lib.dofs_probe_read_n(self.ctx, n, ms, ln)
+        if k < 0:
+            self._err(-k, "dofs_probe_read_n")
+        return [(ms[i], ln[i]) for i in range(min(k, n))]
+
+    def tile_pixels(self, B: int) -> np.ndarray:
+        """The last batch's Borůvka tile census (B x 40 int32, see include/dofs.h)."""
+        out = np.zeros((B, 40), np.int32)
+        self._err(self.lib.dofs_batch_tile_pixels(self.ctx, _p(out, C.c_int32), out.size), "dofs_batch_tile_pixels")
+        return out
 
     def lift(self, direction, box, mat, inv, inv_upper, cls: int) -> dict:
         """get_bottom_variants on the GPU."""

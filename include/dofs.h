@@ -214,7 +214,9 @@ int32_t dofs_batch_slots(dofs_ctx* ctx);
 
 /* The last batch's per-frame counter blocks (B x 64 int32: candidates, snapshots, MST edges, ... and
  * at 16 + r the flag "Borůvka round r found a cross-component edge"), copied to host; waits for the
- * batch. Diagnostics and the bench's roofline model. capacity = ints available at out. */
+ * batch. Diagnostics and the bench's roofline model. capacity = ints available at out.
+ * Also: [14] snapshot count of a frame whose records overflowed (else 0), [56] (frame 0) any overflow,
+ * [57] merges on long heavy paths (the wave-per-path replay's work). */
 int32_t dofs_batch_counters(dofs_ctx* ctx, int32_t* out, int64_t capacity);
 
 /* Stage timing with device events (0 = off). Stages: 0 blur, 1 MST (Borůvka), 2 MST sort, 3 KRT,
@@ -228,6 +230,15 @@ int32_t dofs_profile_read(dofs_ctx* ctx, double ms[8], int32_t* batches);
  * dofs_probe_read returns the accumulated milliseconds and the launch count, then resets. */
 int32_t dofs_probe(dofs_ctx* ctx, const char* kernel);
 int32_t dofs_probe_read(dofs_ctx* ctx, double* ms, int64_t* launches);
+/* Several kernels at once: dofs_probe(ctx, "k_boruvka_min,k_krt_fused,...") then per name (in that order,
+ * at most n) the accumulated milliseconds and launch count; returns the number of probed names
+ * (negative status on error) and resets. */
+int32_t dofs_probe_read_n(dofs_ctx* ctx, int32_t n, double* ms, int64_t* launches);
+
+/* The last batch's Borůvka tile census (B x 40 int32): entry [f][m] = pixels of frame f's 32x8 tiles
+ * that round m's minimum search found done (m >= 1; m = 0: never), so k_boruvka_min processed them in
+ * pass 0 of rounds 1..m and pass 1 of rounds 1..m-1 (bench.py's roofline unit count). */
+int32_t dofs_batch_tile_pixels(dofs_ctx* ctx, int32_t* out, int64_t capacity);
 
 /* get_bottom_variants on the GPU (one candidate, or n candidates with per-candidate class). */
 int32_t dofs_lift(dofs_ctx* ctx, const float dir[2], const int32_t box[4], const float mat[9],

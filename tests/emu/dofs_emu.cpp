@@ -156,6 +156,7 @@ struct HostBackend {
         else
             launch(w.d.B, w.d.N, KBoruvkaMinI{w, r});
     }
+    void boruvka_tiles(const Ws& w) { ::memset(w.tpx, 0, sizeof(int) * kRoundsMax * (size_t)w.d.B); }  // no tiles here
     void dnc_compress(const Ws& w, int64_t S, int ep) { launch(w.d.B, w.d.M, KDncCompress{w, S, ep}); }
     void replay_long(const Ws& w, int r) {
         launch_counted(w.d.B, w.d.N, KReplay{w, 2 * r + 1, w.list_long, C_LONG, nullptr, 0}, C_LONG);
@@ -171,6 +172,7 @@ struct HostBackend {
     }
     void profile(bool) {}
     void probe(const char*) {}
+    int probe_read_n(int, double*, int64_t*) { return 0; }
     int64_t probe_read(double* ms) {
         *ms = 0;
         return 0;

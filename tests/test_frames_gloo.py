@@ -60,3 +60,68 @@ def test_gather_world2():
         for f in range(B):
             expect += [(r * B + f, 1000 * r + 10 * f + k) for k in range(counts[f])]
     assert res[0] == expect and res[1] == expect
+
+
+# ---- the real batch path on every rank: host emulator of the product pipeline (tests/emu) -------------
+EH, EW, EB, EPER, EMIN = 61, 47, 2, 16, 40
+
+
+def _emu_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from denseopticalflowsegmentation3d_amd.abi import default_params
+    from denseopticalflowsegmentation3d_amd.frames import FrameParallel
+    from denseopticalflowsegmentation3d_amd.runtime import Dofs
+    from oracle import binding as ob
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ctx = Dofs(0, lib=EMU)
+        persp, inv, up = ob.calib()
+        prm = default_params()
+        prm.min_size = EMIN
+        mine = frame_shard(world * EB, rank, world)
+        flows = torch.from_numpy(np.stack([ob.synth_flow(EH, EW, s) for s in mine]))
+        fp = FrameParallel(ctx, world, EPER)
+        g = fp.step(flows, persp, inv, up, params=prm).numpy()
+        if rank == 0:
+            frames = decode_gathered(g, world, EB, EPER)
+            q.put([(f["frame"].tolist(), f["slot"].tolist(), f["size"].tolist(), f["cls"].tolist(),
+                    f["score"].tolist()) for f in frames])
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EMU = os.path.join(ROOT, "tests", "emu", "_build", "libdofs_emu.so")
+
+
+def test_gather_real_pipeline_world2(calib):
+    """Each gloo rank segments its frames through the product pipeline (host emulator, same kernel
+    bodies) and the gathered box records equal the oracle's snapshots of every frame, in frame order."""
+    import subprocess
+    from oracle import binding as ob
+    from parity import params
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "emu")], check=True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + os.getpid() % 500
+    ps = [ctx.Process(target=_emu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=300)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    persp, inv, up = calib
+    assert len(got) == 2 * EB
+    nsnap = 0
+    for gf, (frame, slot, size, cls, score) in enumerate(got):
+        o = ob.segment(ob.synth_flow(EH, EW, gf), persp, inv, up, params=params(EMIN, 8), mode=0)
+        s = o.snapshots
+        nsnap += len(s)
+        assert slot == s["slot"].tolist() and size == s["size"].tolist() and cls == s["sol"]["cls"].tolist()
+        assert frame == [gf % EB] * len(s)  # frame index within the rank's batch
+        assert np.allclose(score, s["score"].astype(np.float32), rtol=0, atol=1e-6)
+    assert nsnap > 0
