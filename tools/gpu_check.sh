@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU session: parity tests, a short bench, a rocprofv3 kernel-trace summary.
+# One GPU session: parity tests, the default bench line, a rocprofv3 kernel-trace summary.
 # Stops at the first step that faults, aborts or times out (exit >= 2 other than pytest's 1).
 set -u
 mkdir -p gpurun_out
@@ -13,7 +13,11 @@ step() {  # name timeout cmd...
     return 0
 }
 export TMPDIR=/tmp
-step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
-step bench 600 python bench.py --steps 5 --warmup 2 --batch ${BATCH:-4} --cpu-frames 0
-step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --batch ${BATCH:-4} --cpu-frames 0 --no-stages
+if [ -z "${SKIP_TESTS:-}" ]; then
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ${TESTS:-}
+fi
+step bench 600 python bench.py ${BENCH_ARGS:-}
+if [ -n "${ROCPROF:-}" ]; then
+step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --cpu-frames 0 --no-stages --no-h2d
+fi
 exit 0
