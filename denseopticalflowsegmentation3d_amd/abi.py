@@ -111,6 +111,15 @@ class DofsResult(C.Structure):
     ]
 
 
+class DofsEdge(C.Structure, _NpMixin):
+    """Edge (graph.hpp:13-17): {int start; int end; double weight;} — 16 bytes."""
+    _fields_ = [
+        ("start", C.c_int32),
+        ("end", C.c_int32),
+        ("weight", C.c_double),
+    ]
+
+
 class DofsEvent(C.Structure, _NpMixin):
     _fields_ = [
         ("start", C.c_int32),

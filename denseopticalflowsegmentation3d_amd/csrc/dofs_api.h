@@ -181,6 +181,8 @@ struct Context {
     struct Meta {
         int B = 0, H = 0, W = 0;
         dofs_params prm;
+        int64_t n_edges = -1;  // segment_graph: the caller's edge count (else build_graph's)
+        int64_t mreal = -1;    // segment_graph: merges of the caller's graph (else H*W - 1)
     };
     Backend be;
     Pipeline<Backend> p0, p1, p2;
@@ -190,6 +192,8 @@ struct Context {
     size_t d_in_bytes = 0;
     void* d_scratch = nullptr;
     size_t d_scratch_bytes = 0;
+    void* d_graph = nullptr;  // caller edge lists (segment_graph) and build_graph's sort buffers
+    size_t d_graph_bytes = 0;
     int* d_lmap[kSlots] = {nullptr, nullptr, nullptr};  // overlay edge maps per workspace (api_overlay)
     size_t d_lmap_bytes[kSlots] = {0, 0, 0};
     int64_t nbatch = 0;  // batches issued; batch id b uses workspace b % nslots
@@ -238,6 +242,7 @@ struct Context {
         drain();
         if (d_in) be.free(d_in);
         if (d_scratch) be.free(d_scratch);
+        if (d_graph) be.free(d_graph);
         for (int k = 0; k < kSlots; ++k)
             if (d_lmap[k]) be.free(d_lmap[k]);
     }
@@ -261,6 +266,17 @@ struct Context {
         }
         return d_scratch;
     }
+    void* graph_buf(size_t bytes) {
+        if (bytes > d_graph_bytes) {
+            if (d_graph) {
+                be.sync();
+                be.free(d_graph);
+            }
+            d_graph = be.alloc(bytes);
+            d_graph_bytes = d_graph ? bytes : 0;
+        }
+        return d_graph;
+    }
     int fail(int code, const std::string& msg) {
         err = msg;
         return code;
@@ -277,7 +293,8 @@ struct Context {
 template <class Backend>
 int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int H, int W, const float persp[9],
             const float inv[9], const float inv_upper[27], const dofs_params* params,
-            const unsigned char* allow = nullptr) {
+            const unsigned char* allow = nullptr, const dofs_edge* d_edges = nullptr, int64_t n_edges = 0,
+            int* d_acc = nullptr) {
     if (B <= 0 || H <= 0 || W <= 0 || !persp || !inv || !inv_upper) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
     if (H > 32767 || W > 32767) return cx->fail(DOFS_ERR_INVALID_ARG, "H and W must be < 32768");
     if ((int64_t)H * W >= (1 << 26)) return cx->fail(DOFS_ERR_INVALID_ARG, "H*W must be < 2^26");
@@ -310,7 +327,13 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     if (cx->used[s]) be.wait(sa, cx->evDone[s]);
     be.use(sa);
     P.w.allow = allow;
-    P.run_a(d_flow, fstride);
+    int64_t mreal = d.M;
+    if (d_edges || n_edges > 0) {  // segment_graph on the caller's edge list (one frame)
+        mreal = P.run_a_edges(d_flow, d_edges, n_edges, d_acc, d_acc + n_edges);
+        if (mreal < 0) return cx->fail(DOFS_ERR_INVALID_ARG, "too many edges");
+    } else {
+        P.run_a(d_flow, fstride);
+    }
     P.w.allow = nullptr;
     be.record(cx->evA[s], sa);
     if (sb != sa) be.wait(sb, cx->evA[s]);
@@ -327,6 +350,8 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     m.H = H;
     m.W = W;
     m.prm = prm;
+    m.n_edges = (d_edges || n_edges > 0) ? n_edges : graph_edges(H, W, nbr8);
+    m.mreal = mreal;
     return cx->check();
 }
 
@@ -375,8 +400,8 @@ int api_fetch(Context<Backend>* cx, int frame, dofs_result* out) {
     be.sync();
     const int ns = ctr[C_SNAP];
     out->n_snapshots = ns;
-    out->stats.n_edges = graph_edges(m.H, m.W, m.prm.neighbor == 8);
-    out->stats.n_merges = d.M;
+    out->stats.n_edges = m.n_edges;
+    out->stats.n_merges = m.mreal;
     out->stats.n_candidates = ctr[C_CAND];
     out->stats.n_scored = ctr[C_SCORED];
     out->stats.n_qualified = ctr[C_QUAL];
@@ -403,8 +428,9 @@ int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity
     cx->join(cx->nbatch - 1);
     const Ws& w = cx->pipe(slot).w;
     const Dims& d = w.d;
-    if (capacity < d.M) return cx->fail(DOFS_ERR_CAPACITY, "event capacity");
-    if (d.M <= 0) return DOFS_OK;
+    const int64_t M = cx->meta[slot].mreal;  // merges of the caller's graph (segment_graph: may be < H*W-1)
+    if (capacity < M) return cx->fail(DOFS_ERR_CAPACITY, "event capacity");
+    if (M <= 0) return DOFS_OK;
     Backend& be = cx->be;
     std::vector<int> eu((size_t)d.M), evv((size_t)d.M), pre((size_t)d.M), sz((size_t)d.M);
     std::vector<RepVal> rv((size_t)d.NL);
@@ -417,7 +443,7 @@ int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity
     be.d2h(rv.data(), w.Rv + fo, sizeof(RepVal) * (size_t)d.NL);
     be.d2h(sz.data(), w.SZ + fo + d.N, 4 * (size_t)d.M);
     be.sync();
-    for (int64_t i = 0; i < d.M; ++i) {
+    for (int64_t i = 0; i < M; ++i) {
         dofs_event& e = ev[i];
         const int q = pre[i];
         e.start = eu[i];
@@ -466,6 +492,99 @@ int api_segment(Context<Backend>* cx, const float* flow, int H, int W, size_t st
     if (n > cx->snap_cap) {
         while (cx->snap_cap < n) cx->snap_cap *= 2;
         rc = api_run(cx, (const F2*)cx->d_in, (int64_t)H * W, 1, H, W, persp, inv, inv_upper, params);
+        if (rc) return rc;
+    }
+    return api_fetch(cx, 0, out);
+}
+
+// Upload a host flow field (row stride in bytes, 0 = packed) into the context's input buffer.
+template <class Backend>
+int upload_flow(Context<Backend>* cx, const float* flow, int H, int W, size_t stride) {
+    const size_t row = (size_t)W * 2 * sizeof(float);
+    if (stride == 0) stride = row;
+    if (stride < row) return cx->fail(DOFS_ERR_INVALID_ARG, "row stride too small");
+    const size_t bytes = row * (size_t)H;
+    if (bytes > cx->d_in_bytes) {
+        if (cx->d_in) {
+            cx->be.sync();
+            cx->be.free(cx->d_in);
+        }
+        cx->d_in = cx->be.alloc(bytes);
+        cx->d_in_bytes = cx->d_in ? bytes : 0;
+        if (!cx->d_in) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    }
+    if (stride == row) {
+        cx->be.h2d(cx->d_in, flow, bytes);
+    } else {
+        for (int y = 0; y < H; ++y) cx->be.h2d((char*)cx->d_in + row * y, (const char*)flow + stride * y, row);
+    }
+    return DOFS_OK;
+}
+
+// build_graph (graph.cpp:51-103) on a host field used as given: every edge of the 4- or 8-neighbourhood
+// (neighborhood_8, graph.hpp:23) sorted stably by weight, i.e. by (weight, emission order) — the
+// reference's multiset order. Writes min(E, capacity) edges; *n_edges = E; DOFS_ERR_CAPACITY if E > capacity.
+template <class Backend>
+int api_build_graph(Context<Backend>* cx, const float* flow, int H, int W, size_t stride, int nbr8, dofs_edge* edges,
+                    int64_t capacity, int64_t* n_edges) {
+    if (!flow || H <= 0 || W <= 0 || (!edges && capacity > 0)) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
+    if ((int64_t)H * W >= (1 << 26) || H > 32767 || W > 32767) return cx->fail(DOFS_ERR_INVALID_ARG, "frame too large");
+    const Dims d = Pipeline<Backend>::dims_for(1, H, W, nbr8 ? 1 : 0);
+    const int64_t E = graph_edges(H, W, nbr8 != 0), n4 = 4 * d.N;
+    if (n_edges) *n_edges = E;
+    if (E > capacity) return cx->fail(DOFS_ERR_CAPACITY, "edge capacity");
+    cx->be.use_own();
+    if (int rc = upload_flow(cx, flow, H, W, stride)) return rc;
+    if (E == 0) return DOFS_OK;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t o_kout = al(8 * (size_t)n4), o_vin = o_kout + al(8 * (size_t)n4), o_vout = o_vin + al(4 * (size_t)n4),
+                 o_edges = o_vout + al(4 * (size_t)n4), total = o_edges + al(sizeof(dofs_edge) * (size_t)E);
+    char* g = (char*)cx->graph_buf(total);
+    if (!g) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    Backend& be = cx->be;
+    auto* kin = (unsigned long long*)g;
+    auto* kout = (unsigned long long*)(g + o_kout);
+    auto* vin = (unsigned*)(g + o_vin);
+    auto* vout = (unsigned*)(g + o_vout);
+    auto* de = (dofs_edge*)(g + o_edges);
+    be.launch(1, n4, KGraphKeys{(const F2*)cx->d_in, d, kin, vin});
+    be.sort_pairs(kin, kout, vin, vout, n4, 1, ceil_log2(n4));
+    be.launch(1, E, KGraphEdges{kout, vout, d, de});
+    be.d2h(edges, de, sizeof(dofs_edge) * (size_t)E);
+    be.sync();
+    return cx->check();
+}
+
+// segment_graph(flow, sorted_graph, ...) (graph.cpp:503-536) on a host field (used as given) and a host
+// edge list taken in its order; results as dofs_segment (stats.n_merges = the unions performed).
+template <class Backend>
+int api_segment_graph(Context<Backend>* cx, const float* flow, int H, int W, size_t stride, const dofs_edge* edges,
+                      int64_t E, const float persp[9], const float inv[9], const float inv_upper[27],
+                      const dofs_params* params, dofs_result* out) {
+    if (!flow || H <= 0 || W <= 0 || !out || E < 0 || (E > 0 && !edges))
+        return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
+    if (E >= (int64_t)0x7FFFFFFF) return cx->fail(DOFS_ERR_INVALID_ARG, "too many edges");
+    const int64_t N = (int64_t)H * W;
+    for (int64_t i = 0; i < E; ++i)  // the reference would index out of its node vector
+        if (edges[i].start < 0 || edges[i].start >= N || edges[i].end < 0 || edges[i].end >= N)
+            return cx->fail(DOFS_ERR_INVALID_ARG, "edge endpoint outside the frame");
+    cx->be.use_own();
+    if (int rc = upload_flow(cx, flow, H, W, stride)) return rc;
+    const size_t eb = (sizeof(dofs_edge) * (size_t)E + 255) & ~(size_t)255;
+    char* g = (char*)cx->graph_buf(eb + 8 * (size_t)(E > 0 ? E : 1));
+    if (!g) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    if (E > 0) cx->be.h2d(g, edges, sizeof(dofs_edge) * (size_t)E);
+    const dofs_edge* de = (const dofs_edge*)g;
+    int* acc = (int*)(g + eb);
+    int rc = api_run(cx, (const F2*)cx->d_in, N, 1, H, W, persp, inv, inv_upper, params, nullptr, de, E, acc);
+    if (rc) return rc;
+    int n = 0;  // more history slots than the device snapshot capacity: grow it and run again
+    cx->join(cx->nbatch - 1);
+    cx->be.d2h(&n, cx->pipe(cx->last_slot()).w.ctr + C_SNAP, sizeof(int));
+    cx->be.sync();
+    if (n > cx->snap_cap) {
+        while (cx->snap_cap < n) cx->snap_cap *= 2;
+        rc = api_run(cx, (const F2*)cx->d_in, N, 1, H, W, persp, inv, inv_upper, params, nullptr, de, E, acc);
         if (rc) return rc;
     }
     return api_fetch(cx, 0, out);

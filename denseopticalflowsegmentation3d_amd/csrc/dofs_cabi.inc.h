@@ -55,6 +55,20 @@ int32_t dofs_segment(dofs_ctx* ctx, const float* flow_uv, int32_t H, int32_t W, 
     return dofs::api_segment(ctx, flow_uv, H, W, row_stride_bytes, persp, inv, inv_upper, params, out);
 }
 
+int32_t dofs_build_graph(dofs_ctx* ctx, const float* flow_uv, int32_t H, int32_t W, size_t row_stride_bytes,
+                         int32_t neighborhood_8, dofs_edge* edges, int64_t capacity, int64_t* n_edges) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    return dofs::api_build_graph(ctx, flow_uv, H, W, row_stride_bytes, neighborhood_8, edges, capacity, n_edges);
+}
+
+int32_t dofs_segment_graph(dofs_ctx* ctx, const float* flow_uv, int32_t H, int32_t W, size_t row_stride_bytes,
+                           const dofs_edge* edges, int64_t n_edges, const float persp[9], const float inv[9],
+                           const float inv_upper[27], const dofs_params* params, dofs_result* out) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    return dofs::api_segment_graph(ctx, flow_uv, H, W, row_stride_bytes, edges, n_edges, persp, inv, inv_upper,
+                                   params, out);
+}
+
 int32_t dofs_events(dofs_ctx* ctx, int32_t frame, dofs_event* events, int64_t capacity) {
     if (!ctx) return DOFS_ERR_INVALID_ARG;
     return dofs::api_events(ctx, frame, events, capacity);
@@ -130,6 +144,11 @@ int32_t dofs_set_snapshot_capacity(dofs_ctx* ctx, int32_t per_frame) {
 int32_t dofs_snapshot_capacity(dofs_ctx* ctx) { return ctx ? (int32_t)ctx->snap_cap : -1; }
 
 int64_t dofs_batch_count(dofs_ctx* ctx) { return ctx ? ctx->nbatch : -1; }
+
+int32_t dofs_batch_frames(dofs_ctx* ctx) {
+    if (!ctx || !ctx->have_batch()) return 0;
+    return ctx->meta[ctx->last_slot()].B;
+}
 
 int32_t dofs_batch_slots(dofs_ctx* ctx) { return ctx ? ctx->nslots : -1; }
 

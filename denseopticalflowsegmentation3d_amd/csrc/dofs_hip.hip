@@ -1138,10 +1138,31 @@ constexpr int kTileX = 32, kTileY = 8, kMinHT = 512;  // 512 > 256 pixels + 82 h
 // leaving the component has an end in it), reduced per wave and per tile before one global atomic.
 // Pass 1 then only compares each pixel's kept weight with its component's minimum and reduces the
 // kept indices of the equal ones — no weights recomputed, no neighbour reads.
+// Pass 0 stages each tile's labels and blurred flows with a one-pixel halo in LDS (coalesced row loads,
+// each word once), and every pixel reads its eight neighbours from there.
+// Tile order: a block walks a contiguous run of tiles in raster order (a row segment's left / right halo
+// lines were just loaded by the same CU), and blocks that share an XCD (blockIdx.x % 8 when the grid
+// width is a multiple of 8) take contiguous bands of the frame, so the halo rows shared with the tiles
+// above and below are read through one L2 (MI355X_MICROARCH.md §Workgroup dispatch, XCD placement).
+constexpr int kHaloX = kTileX + 2, kHalo = kHaloX * (kTileY + 2);
+__device__ __forceinline__ void tile_run(int tiles, int& t0, int& t1) {
+    const int gx = gridDim.x, x = blockIdx.x;
+    if (gx % 8 == 0 && gx >= 64) {
+        const int g = x % 8, j = x / 8, G = gx / 8;
+        const int b0 = (int)((int64_t)g * tiles / 8), n = (int)((int64_t)(g + 1) * tiles / 8) - b0;
+        t0 = b0 + (int)((int64_t)j * n / G);
+        t1 = b0 + (int)((int64_t)(j + 1) * n / G);
+    } else {
+        t0 = (int)((int64_t)x * tiles / gx);
+        t1 = (int)((int64_t)(x + 1) * tiles / gx);
+    }
+}
 __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass, unsigned char* tdone,
-                                                     unsigned long long* candw, unsigned* candi) {
+                                                     unsigned long long* candw, unsigned* candi, int runs) {
     __shared__ int hk[kMinHT];
     __shared__ unsigned long long hv[kMinHT];
+    __shared__ int sl[kHalo];
+    __shared__ F2 sf[kHalo];
     __shared__ int any, tany;
     const Dims& d = w.d;
     const int f = blockIdx.y;
@@ -1173,34 +1194,54 @@ __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass, unsi
         }
         atomicMin(hv + slot, v);
     };
-    for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
+    int t0 = blockIdx.x, t1 = tiles, ts = gridDim.x;  // strided over the frame's tiles (balanced)
+    if (runs) {  // contiguous XCD-banded runs (DOFS_BMIN_RUNS=1)
+        tile_run(tiles, t0, t1);
+        ts = 1;
+    }
+    for (int t = t0; t < t1; t += ts) {
         if (td[t]) continue;  // block-uniform
-        const int x = (t % tiles_x) * kTileX + (tid % kTileX), y = (t / tiles_x) * kTileY + tid / kTileX;
+        const int tx0 = (t % tiles_x) * kTileX, ty0 = (t / tiles_x) * kTileY;
+        if (pass == 0) {  // the tile and its one-pixel halo into LDS, row by row (out-of-frame cells unused)
+            for (int e = tid; e < kHalo; e += 256) {
+                const int gx = tx0 - 1 + e % kHaloX, gy = ty0 - 1 + e / kHaloX;
+                if (gx >= 0 && gx < d.W && gy >= 0 && gy < d.H) {
+                    const int64_t q = (int64_t)gy * d.W + gx;
+                    sl[e] = comp[q];
+                    sf[e] = b[q];
+                }
+            }
+            __syncthreads();
+        }
+        const int x = tx0 + (tid % kTileX), y = ty0 + tid / kTileX;
         int cp = -1;
         unsigned long long own = ~0ull;  // pass 0: the pixel's minimum weight; pass 1: its index
         if (x < d.W && y < d.H) {
             const int64_t p = (int64_t)y * d.W + x;
             if (pass == 0) {
-                // all loads first, from in-frame addresses (an absent neighbour reads the pixel
-                // itself and is masked below), so the wave waits on memory once per tile instead of
-                // once per edge. Slots 0-3: the edges p emits (left, up, up-left, down-left); 4-7:
-                // the edges its right, lower, lower-right and upper-right neighbours emit towards it.
+                // Slots 0-3: the edges p emits (left, up, up-left, down-left); 4-7: the edges its right,
+                // lower, lower-right and upper-right neighbours emit towards it. An absent neighbour
+                // reads the pixel itself and is masked below.
                 const int64_t W = d.W;
                 const bool xl = x > 0, xr = x + 1 < d.W, yu = y > 0, yd = y + 1 < d.H;
                 const bool ok[8] = {xl, yu, d.nbr8 && xl && yu, d.nbr8 && xl && yd,
                                     xr, yd, d.nbr8 && xr && yd, d.nbr8 && xr && yu};
                 const int64_t nb[8] = {p - 1, p - W, p - W - 1, p + W - 1, p + 1, p + W, p + W + 1, p - W + 1};
+                const int e0 = (tid / kTileX + 1) * kHaloX + tid % kTileX + 1;
+                const int ne[8] = {e0 - 1, e0 - kHaloX, e0 - kHaloX - 1, e0 + kHaloX - 1,
+                                   e0 + 1, e0 + kHaloX, e0 + kHaloX + 1, e0 - kHaloX + 1};
                 int64_t q[8];
                 int cq[8];
                 F2 bq[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) q[j] = ok[j] ? nb[j] : p;
-                cp = comp[p];
-                const F2 bp = b[p];
+                cp = sl[e0];
+                const F2 bp = sf[e0];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    cq[j] = comp[q[j]];
-                    bq[j] = b[q[j]];
+                    const int ej = ok[j] ? ne[j] : e0;
+                    cq[j] = sl[ej];
+                    bq[j] = sf[ej];
                 }
                 unsigned allow_bits = 0xff;  // bit j: slot j's edge may be in the MST
                 if (w.allow) {               // launch-uniform
@@ -2213,7 +2254,12 @@ struct HipBackend {
     }
     void boruvka_min(const Ws& w, int r, int pass) {
         const int64_t tiles = (int64_t)((w.d.W + kTileX - 1) / kTileX) * ((w.d.H + kTileY - 1) / kTileY);
-        const int64_t gx = std::min<int64_t>(tiles, std::max<int64_t>(1, grid_cap() / w.d.B));
+        int64_t gx = std::min<int64_t>(tiles, std::max<int64_t>(1, grid_cap() / w.d.B));
+        static const int runs = [] {
+            const char* e = getenv("DOFS_BMIN_RUNS");
+            return e ? atoi(e) : 0;
+        }();
+        if (runs && gx >= 64) gx &= ~(int64_t)7;  // a multiple of 8: XCD-banded tile runs (tile_run)
         unsigned char* tdone = w.hlB;  // free during the MST (KDncParent fills it after the KRT)
         static_assert(sizeof(*w.hlB) == 1, "tile flags are bytes");
         if (r == 1 && pass == 0) memset(tdone, 0, (size_t)tiles * w.d.B);  // tiles <= M per frame
@@ -2221,7 +2267,8 @@ struct HipBackend {
             // kept candidates: the row-blur temporary (8 B per pixel, dead after the blur) and the
             // MST-count words (written only after the MST)
             hipLaunchKernelGGL(k_boruvka_min, dim3((unsigned)gx, (unsigned)w.d.B), dim3(256), 0, stream, w, r, pass,
-                               tdone, reinterpret_cast<unsigned long long*>(w.tmp), reinterpret_cast<unsigned*>(w.cnt));
+                               tdone, reinterpret_cast<unsigned long long*>(w.tmp), reinterpret_cast<unsigned*>(w.cnt),
+                               runs);
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_boruvka_min launch");
     }

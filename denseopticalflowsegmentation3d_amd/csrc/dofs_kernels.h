@@ -118,6 +118,7 @@ struct Ws {
     double score_threshold;
     double overlay_min_score;
     int long_path;  // heavy paths at least this long run on the wave-cooperative replay
+    int64_t mreal;  // merges of the caller's graph (scored); later ones only complete a forest (< M)
     double min_convexity[3];
 
     DOFS_HD int* C(int f) const { return ctr + (int64_t)f * kCounters; }
@@ -565,19 +566,158 @@ struct KMstEmit {
 struct KEdgeInit {  // endpoints by rank; labels = the endpoints (global-kernel KRT only: `labels`)
     Ws w;
     bool labels;
+    bool given = false;  // EU / EV already hold the merges (segment_graph on a caller's edge list)
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
         const int64_t o = f * d.M + i;
-        const unsigned idx = w.val_out[o];
-        const int64_t p = idx >> 2;
-        const int64_t q = edge_end(d, p, idx & 3);
-        w.EU[o] = (int)p;
-        w.EV[o] = (int)q;
+        int64_t p, q;
+        if (given) {
+            p = w.EU[o];
+            q = w.EV[o];
+        } else {
+            const unsigned idx = w.val_out[o];
+            p = idx >> 2;
+            q = edge_end(d, p, idx & 3);
+            w.EU[o] = (int)p;
+            w.EV[o] = (int)q;
+        }
         if (!labels) return;  // the sweep writes every merge's block-start labels
         w.lu[o] = (int)p;
         w.lv[o] = (int)q;
         w.own[o] = 0;
     }
+};
+
+// ---------------------------------------------------------------------------------------------
+// build_graph (graph.cpp:51-103) as a sorted edge list: every emitted edge's weight bits and emission
+// index, radix-sorted (stable) — the reference's multiset order (weight, emission order).
+// ---------------------------------------------------------------------------------------------
+struct KGraphKeys {
+    const F2* flow;
+    Dims d;
+    unsigned long long* key;
+    unsigned* val;
+    DOFS_HD void operator()(int, int64_t i) const {  // i = 4 p + k over all pixels
+        const int64_t p = i >> 2;
+        const int k = (int)(i & 3);
+        const int x = (int)(p % d.W), y = (int)(p / d.W);
+        if (edge_exists(d, x, y, k)) {
+            key[i] = dbits(edge_weight(flow, p, edge_end(d, p, k)));
+            val[i] = (unsigned)i;
+        } else {  // sorts behind every edge (weights are >= +0, NaN bits below ~0)
+            key[i] = ~0ull;
+            val[i] = kNoEdge;
+        }
+    }
+};
+struct KGraphEdges {  // Edge {start, end, weight} (graph.hpp:13-17, create_edge graph.cpp:43-49)
+    const unsigned long long* key;
+    const unsigned* val;
+    Dims d;
+    dofs_edge* out;
+    DOFS_HD void operator()(int, int64_t i) const {
+        const unsigned idx = val[i];
+        const int64_t p = idx >> 2;
+        dofs_edge e;
+        e.start = (int32_t)p;
+        e.end = (int32_t)edge_end(d, p, idx & 3);
+        e.weight = bitsd(key[i]);
+        out[i] = e;
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// segment_graph on a caller's edge list (graph.cpp:503-536): Kruskal over the list in its order
+// accepts exactly the minimum spanning forest under the strict order "position in the list", which
+// Borůvka finds in O(log N) rounds (per component the incident cross edge of least position; hooks
+// follow strictly decreasing positions except mutual pairs, rooted at the smaller id). Accepted edges
+// in list order are the merges; if they form a forest, the component roots are chained by extra
+// merges after them (Ws::mreal says where the caller's merges end; those are never scored).
+// Per-vertex arrays: comp (component root label), uf (hooks), bi (least incident position).
+// Round flags: counters C_ACT + r of frame 0.
+// ---------------------------------------------------------------------------------------------
+struct KElInit {
+    Ws w;
+    DOFS_HD void operator()(int, int64_t v) const {
+        w.comp[v] = (int)v;
+        w.uf[v] = (int)v;
+        w.bi[v] = kNoEdge;
+    }
+};
+struct KElMin {
+    Ws w;
+    const dofs_edge* e;
+    int r;
+    DOFS_HD void operator()(int, int64_t i) const {
+        if (r > 0 && !w.ctr[C_ACT + r - 1]) return;
+        const int a = w.comp[e[i].start], b = w.comp[e[i].end];
+        if (a == b) return;
+        dofs_amin_u32(w.bi + a, (unsigned)i);
+        dofs_amin_u32(w.bi + b, (unsigned)i);
+        if (!w.ctr[C_ACT + r]) dofs_st(w.ctr + C_ACT + r, 1);
+    }
+};
+struct KElHook {
+    Ws w;
+    const dofs_edge* e;
+    int* acc;  // per edge: accepted (an MSF edge)
+    int r;
+    DOFS_HD void operator()(int, int64_t c) const {
+        if (!w.ctr[C_ACT + r] || w.comp[c] != (int)c) return;
+        const unsigned m = w.bi[c];
+        if (m == kNoEdge) return;
+        const int a = w.comp[e[m].start], b = w.comp[e[m].end];
+        const int o = a == (int)c ? b : a;
+        acc[m] = 1;
+        if (w.bi[o] == m && (int)c < o) return;  // mutual pair: the smaller root stays a root
+        w.uf[c] = o;
+    }
+};
+struct KElRelabel {
+    Ws w;
+    int r;
+    DOFS_HD void operator()(int, int64_t p) const {
+        if (!w.ctr[C_ACT + r]) return;
+        const int c = w.comp[p];
+        const int root = uf_find(w.uf, c);
+        if (root != c) w.comp[p] = root;
+        w.bi[p] = kNoEdge;  // the hook has read every minimum of this round
+    }
+};
+struct KElEmit {  // accepted edges in list order: merge j = the j-th accepted edge
+    Ws w;
+    const dofs_edge* e;
+    const int* acc;
+    const int* off;
+    DOFS_HD void operator()(int, int64_t i) const {
+        if (!acc[i]) return;
+        const int j = off[i];
+        w.EU[j] = e[i].start;
+        w.EV[j] = e[i].end;
+        w.key_out[j] = dbits(e[i].weight);
+    }
+};
+struct KElRootFlag {
+    Ws w;
+    DOFS_HD void operator()(int, int64_t v) const { w.cnt[v] = w.comp[v] == (int)v ? 1 : 0; }
+};
+struct KElRootList {  // the forest's roots in ascending id
+    Ws w;
+    DOFS_HD void operator()(int, int64_t v) const {
+        if (w.comp[v] == (int)v) w.cur[w.off[v]] = (int)v;
+    }
+};
+struct KElChain {  // merge mreal + j joins the components of roots j and j + 1 (after every real merge)
+    Ws w;
+    DOFS_HD void operator()(int, int64_t j) const {
+        w.EU[w.mreal + j] = w.cur[j];
+        w.EV[w.mreal + j] = w.cur[j + 1];
+        w.key_out[w.mreal + j] = 0x7FF0000000000000ull;  // +inf: not an edge of the caller's graph
+    }
+};
+struct KCopyFlow {  // the flow as given (segment_graph does not blur)
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t p) const { w.blur[f * w.d.N + p] = w.flow[f * w.flow_fstride + p]; }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -1166,7 +1306,7 @@ struct KFilter {  // appends candidates through the backend's list taker (called
     DOFS_HD void operator()(int f, int64_t i, bool valid, T& t) const {
         const Dims& d = w.d;
         bool c = false;
-        if (valid) {
+        if (valid && i < w.mreal) {
             const NodeVal v = node_val(w, pre, f, d.N + i);
             const int y = v.root / d.W;
             c = v.size >= w.min_size && y >= d.H / 10 && !(vec_norm(v.mx, v.my) < 3 * (y + 1) / (double)d.H);

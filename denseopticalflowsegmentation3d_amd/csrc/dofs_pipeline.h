@@ -222,7 +222,8 @@ struct Pipeline {
     void run_a(const F2* flow, int64_t fstride) {
         const Dims& d = w.d;
         const int B = d.B;
-        const int64_t N = d.N, M = d.M, NL = d.NL;
+        const int64_t N = d.N, M = d.M;
+        w.mreal = M;
         w.flow = flow;
         w.flow_fstride = fstride;
         be.memset(w.ctr, 0, sizeof(int) * (size_t)B * kCounters);
@@ -245,10 +246,69 @@ struct Pipeline {
         be.scan_excl(w.cnt, w.off, N, B);
         be.launch(B, N, KMstEmit{w});
         be.sort_pairs(w.key_in, w.key_out, w.val_in, w.val_out, M, B, ceil_log2(4 * N));  // Kruskal order
+        krt(false);
+    }
 
+    // Phase A of segment_graph (graph.cpp:503-536) on a caller's edge list of one frame (device
+    // `edges`, E of them, in Kruskal order): the flow is used as given; Borůvka under the list order
+    // finds the accepted edges, which become the merges (a forest is completed by extra merges that
+    // are never scored). acc / off: E ints of scratch. Returns the number of accepted edges (waits
+    // for the device), or -1 if E is too large for 32-bit positions.
+    int64_t run_a_edges(const F2* flow, const dofs_edge* edges, int64_t E, int* acc, int* off) {
+        const Dims& d = w.d;
+        const int64_t N = d.N, M = d.M;
+        if (E >= (int64_t)0x7FFFFFFF) return -1;  // positions and the scan are 32-bit
+        w.flow = flow;
+        w.flow_fstride = N;
+        be.memset(w.ctr, 0, sizeof(int) * kCounters);
+        be.mark(0);
+        be.launch(1, N, KCopyFlow{w});
+        if (M <= 0) {
+            be.launch(1, N, KLabelInit{w, true});
+            be.launch(1, 1, KSingle{w});
+            pre = nullptr;
+            w.mreal = 0;
+            be.mark(8);
+            return 0;
+        }
+        be.mark(1);
+        be.launch(1, N, KElInit{w});
+        int64_t m = 0;
+        if (E > 0) {
+            be.memset(acc, 0, sizeof(int) * (size_t)E);
+            const int R = std::min(ceil_log2(N) + 1, kRoundsMax - 1);
+            for (int r = 0; r < R; ++r) {
+                be.launch(1, E, KElMin{w, edges, r});
+                be.launch(1, N, KElHook{w, edges, acc, r});
+                be.launch(1, N, KElRelabel{w, r});
+            }
+            be.scan_excl(acc, off, E, 1);
+            be.sync();
+            m = (int64_t)be.read_int(off + E - 1) + be.read_int(acc + E - 1);
+            be.launch(1, E, KElEmit{w, edges, acc, off});
+        }
+        w.mreal = m;
+        if (m < M) {  // a forest: chain its roots after the caller's merges
+            be.launch(1, N, KElRootFlag{w});
+            be.scan_excl(w.cnt, w.off, N, 1);
+            be.launch(1, N, KElRootList{w});
+            be.launch(1, M - m, KElChain{w});
+        }
+        be.mark(2);
+        krt(true);
+        return m;
+    }
+
+    // K3 Kruskal reconstruction tree of the merges EU / EV (given: already there; else decoded from the
+    // sorted MST edges), then the preorder unless it runs at the start of phase B
+    void krt(bool given) {
+        const Dims& d = w.d;
+        const int B = d.B;
+        const int64_t N = d.N, M = d.M, NL = d.NL;
         be.mark(3);
-        // K3 Kruskal reconstruction tree
-        be.launch(B, M, KEdgeInit{w, krt_dnc});
+        KEdgeInit ei{w, krt_dnc};
+        ei.given = given;
+        if (!given || krt_dnc) be.launch(B, M, ei);
         const bool words = krt_dnc || Backend::kKrtLabelWords;  // the global-kernel KRT reads them
         be.launch(B, words ? NL : N, KLabelInit{w, words});
         const int64_t deep = Backend::deep_block();  // levels with block size <= deep run per block

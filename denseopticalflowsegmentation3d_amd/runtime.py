@@ -12,7 +12,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from .abi import (DofsBoxRecord, DofsEvent, DofsFlowParams, DofsParams, DofsResult, DofsSnapshot, DofsSolution,
+from .abi import (DofsBoxRecord, DofsEdge, DofsEvent, DofsFlowParams, DofsParams, DofsResult, DofsSnapshot, DofsSolution,
                   default_flow_params, default_params, solution_dict)
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
@@ -48,6 +48,15 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_segment.argtypes = [C.c_void_p, _fp, C.c_int32, C.c_int32, C.c_size_t, _fp, _fp, _fp,
                                C.POINTER(DofsParams), C.POINTER(DofsResult)]
     L.dofs_segment.restype = C.c_int32
+    if hasattr(L, "dofs_build_graph"):  # (older builds kept for same-box A/B runs lack these)
+        L.dofs_build_graph.argtypes = [C.c_void_p, _fp, C.c_int32, C.c_int32, C.c_size_t, C.c_int32,
+                                       C.POINTER(DofsEdge), C.c_int64, C.POINTER(C.c_int64)]
+        L.dofs_build_graph.restype = C.c_int32
+        L.dofs_segment_graph.argtypes = [C.c_void_p, _fp, C.c_int32, C.c_int32, C.c_size_t, C.POINTER(DofsEdge),
+                                         C.c_int64, _fp, _fp, _fp, C.POINTER(DofsParams), C.POINTER(DofsResult)]
+        L.dofs_segment_graph.restype = C.c_int32
+        L.dofs_batch_frames.argtypes = [C.c_void_p]
+        L.dofs_batch_frames.restype = C.c_int32
     L.dofs_events.argtypes = [C.c_void_p, C.c_int32, C.POINTER(DofsEvent), C.c_int64]
     L.dofs_events.restype = C.c_int32
     L.dofs_segment_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, _fp, _fp, _fp,
@@ -169,6 +178,7 @@ class Dofs:
 
     def __init__(self, device: int = 0, lib: C.CDLL | str | None = None):
         self.lib = lib if isinstance(lib, C.CDLL) else load(lib)
+        self._last_merges = None
         self.ctx = self.lib.dofs_create(device)
         if not self.ctx:
             raise RuntimeError(f"dofs_create({device}) failed: no gfx950 device visible")
@@ -218,12 +228,43 @@ class Dofs:
                                    C.byref(params or default_params()), C.byref(r))
         self._err(rc, "dofs_segment")
         self._last_hw = (H, W)
+        self._last_merges = None
+        return FrameResult(H, W, snaps[:r.n_snapshots].copy(), labels, leaf, blurred, self._stats(r))
+
+    def build_graph(self, flow: np.ndarray, neighborhood_8: bool = False) -> np.ndarray:
+        """build_graph(img, W, H, diff, neighborhood_8) (graph.cpp:51-103) on a host (H, W, 2) float32 field
+        used as given: the edges sorted by weight (stable), structured array (start, end, weight)."""
+        flow = _f32(flow)
+        H, W = flow.shape[:2]
+        E = (W - 1) * H + W * (H - 1) + (2 * (W - 1) * (H - 1) if neighborhood_8 else 0)
+        out = np.zeros(max(E, 1), dtype=DofsEdge.np_dtype())
+        n = C.c_int64()
+        rc = self.lib.dofs_build_graph(self.ctx, _p(flow), H, W, 0, 1 if neighborhood_8 else 0,
+                                       out.ctypes.data_as(C.POINTER(DofsEdge)), len(out), C.byref(n))
+        self._err(rc, "dofs_build_graph")
+        return out[:n.value]
+
+    def segment_graph(self, flow: np.ndarray, edges: np.ndarray, persp, inv, inv_upper,
+                      params: DofsParams | None = None, capacity: int = 65536) -> FrameResult:
+        """segment_graph(flow, sorted_graph, ...) (graph.cpp:503-536): Kruskal over `edges` (structured
+        (start, end, weight), processed in order) on a host field used as given."""
+        flow = _f32(flow)
+        H, W = flow.shape[:2]
+        edges = np.ascontiguousarray(edges, dtype=DofsEdge.np_dtype())
+        p, i, u = self._mats(persp, inv, inv_upper)
+        r, snaps, labels, leaf, blurred = self._result(H, W, capacity)
+        rc = self.lib.dofs_segment_graph(self.ctx, _p(flow), H, W, 0, edges.ctypes.data_as(C.POINTER(DofsEdge)),
+                                         len(edges), _p(p), _p(i), _p(u), C.byref(params or default_params()),
+                                         C.byref(r))
+        self._err(rc, "dofs_segment_graph")
+        self._last_hw = (H, W)
+        self._last_merges = int(r.stats.n_merges)
         return FrameResult(H, W, snaps[:r.n_snapshots].copy(), labels, leaf, blurred, self._stats(r))
 
     def events(self, frame: int = 0) -> np.ndarray:
         """Per-merge records (Kruskal order) of `frame` of the last batch."""
         H, W = self._last_hw
-        n = max(H * W - 1, 0)
+        n = max(H * W - 1, 0) if self._last_merges is None else self._last_merges
         ev = np.zeros(max(n, 1), dtype=DofsEvent.np_dtype())
         rc = self.lib.dofs_events(self.ctx, frame, ev.ctypes.data_as(C.POINTER(DofsEvent)), n)
         self._err(rc, "dofs_events")
@@ -238,6 +279,7 @@ class Dofs:
                                                 C.byref(params or default_params()), C.c_void_p(stream or 0))
         self._err(rc, "dofs_segment_batch_device")
         self._last_hw = (H, W)
+        self._last_merges = None
         return int(self.lib.dofs_batch_count(self.ctx)) - 1
 
     def band_msf_device(self, d_rows: int, row0: int, rows: int, H: int, W: int, r0: int, r1: int, d_mask: int,
@@ -259,6 +301,7 @@ class Dofs:
                                                  C.c_void_p(stream or 0))
         self._err(rc, "dofs_segment_masked_device")
         self._last_hw = (H, W)
+        self._last_merges = None
         return int(self.lib.dofs_batch_count(self.ctx)) - 1
 
     def fetch(self, frame: int, capacity: int = 65536, want_blur: bool = True) -> FrameResult:
@@ -449,3 +492,97 @@ def synth_flow_device(d_out: int, B: int, H: int, W: int, seed0: int = 0, stream
     L = lib or load()
     if L.dofs_synth_flow_device(C.c_void_p(d_out), B, H, W, seed0, C.c_void_p(stream or 0)) != 0:
         raise RuntimeError("dofs_synth_flow_device failed")
+
+
+# ---- the C-ABI RCCL gather of box records (include/dofs_rccl.h, libdofs_rccl.so) ----------------------
+RCCL_LIB_PATH = os.path.join(_PKG, "_build", "libdofs_rccl.so")
+
+
+def load_rccl(path: str | None = None) -> C.CDLL:
+    """Load libdofs_rccl.so (after libdofs_hip.so, which it links)."""
+    path = os.path.abspath(path or RCCL_LIB_PATH)
+    if path in _LIBS:
+        return _LIBS[path]
+    if not os.path.exists(path):
+        raise RuntimeError(f"dofs RCCL library not built: {path} missing (run __graft_entry__.build())")
+    load()
+    L = C.CDLL(path)
+    vp = C.c_void_p
+    L.dofs_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
+    L.dofs_comm_unique_id.restype = C.c_int32
+    L.dofs_comm_init.argtypes = [C.POINTER(vp), C.c_int32, C.POINTER(C.c_uint8), C.c_int32, C.c_int32]
+    L.dofs_comm_init.restype = C.c_int32
+    L.dofs_comm_init_local.argtypes = [C.POINTER(vp), C.c_int32, _ip]
+    L.dofs_comm_init_local.restype = C.c_int32
+    L.dofs_comm_wrap.argtypes = [C.POINTER(vp), vp]
+    L.dofs_comm_wrap.restype = C.c_int32
+    L.dofs_comm_destroy.argtypes = [vp]
+    L.dofs_comm_rank.argtypes = [vp, _ip, _ip]
+    L.dofs_comm_rank.restype = C.c_int32
+    L.dofs_comm_last_error.argtypes = [vp]
+    L.dofs_comm_last_error.restype = C.c_char_p
+    L.dofs_records_block_bytes.argtypes = [C.c_int32, C.c_int32]
+    L.dofs_records_block_bytes.restype = C.c_size_t
+    L.dofs_gather_records.argtypes = [vp, vp, C.c_int32, C.c_int32, vp, vp]
+    L.dofs_gather_records.restype = C.c_int32
+    L.dofs_gather_bytes.argtypes = [vp, vp, C.c_size_t, C.c_int32, vp, vp]
+    L.dofs_gather_bytes.restype = C.c_int32
+    _LIBS[path] = L
+    return L
+
+
+class Comm:
+    """A dofs_comm (RCCL communicator) of include/dofs_rccl.h."""
+
+    def __init__(self, handle: int, lib: C.CDLL):
+        self.lib, self.h = lib, handle
+
+    @staticmethod
+    def unique_id() -> bytes:
+        L = load_rccl()
+        buf = (C.c_uint8 * 128)()
+        if L.dofs_comm_unique_id(buf) != 0:
+            raise RuntimeError("dofs_comm_unique_id failed")
+        return bytes(buf)
+
+    @classmethod
+    def init(cls, nranks: int, uid: bytes, rank: int, device: int) -> "Comm":
+        L = load_rccl()
+        h = C.c_void_p()
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        if L.dofs_comm_init(C.byref(h), nranks, buf, rank, device) != 0:
+            raise RuntimeError("dofs_comm_init failed")
+        return cls(h.value, L)
+
+    @classmethod
+    def local(cls, devices) -> list:
+        L = load_rccl()
+        n = len(devices)
+        hs = (C.c_void_p * n)()
+        devs = np.asarray(devices, np.int32)
+        if L.dofs_comm_init_local(hs, n, _p(devs, C.c_int32)) != 0:
+            raise RuntimeError("dofs_comm_init_local failed")
+        return [cls(hs[i], L) for i in range(n)]
+
+    def rank(self):
+        r, n = C.c_int32(), C.c_int32()
+        self.lib.dofs_comm_rank(self.h, C.byref(r), C.byref(n))
+        return r.value, n.value
+
+    def block_bytes(self, frames: int, per_frame: int) -> int:
+        return int(self.lib.dofs_records_block_bytes(frames, per_frame))
+
+    def gather_records(self, ctx: "Dofs", per_frame: int, d_recv: int | None, root: int = 0,
+                       stream: int | None = None) -> None:
+        rc = self.lib.dofs_gather_records(C.c_void_p(ctx.ctx), C.c_void_p(self.h), per_frame, root,
+                                          C.c_void_p(d_recv or 0), C.c_void_p(stream or 0))
+        if rc != 0:
+            raise RuntimeError(f"dofs_gather_records failed ({rc}): {self.lib.dofs_comm_last_error(self.h).decode()}")
+
+    def close(self):
+        if self.h:
+            self.lib.dofs_comm_destroy(C.c_void_p(self.h))
+            self.h = None
+
+    def __del__(self):
+        self.close()

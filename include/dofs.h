@@ -12,6 +12,15 @@
  *                              Forest::new_merge cpp/src/graph.cpp:272-384
  *                              Forest::get_best_segments cpp/src/graph.cpp:391-429
  *         and the overlay's label semantics      cpp/src/draw.cpp:118-147 (score > 0.7, ascending slots)
+ *   dofs_build_graph
+ *       ← std::vector<Edge> build_graph(const cv::Mat& img, int width, int height, const DiffFunction& diff,
+ *                                       bool neighborhood_8 = false)
+ *         cpp/inc/graph.hpp:22-23, cpp/src/graph.cpp:51-103 (with diff = segment.cpp:20-32)
+ *   dofs_segment_graph
+ *       ← Forest segment_graph(const cv::Mat& flow, const std::vector<Edge>& sorted_graph, const cv::Mat& bev,
+ *                              const cv::Matx33f& persp, const cv::Matx33f& inv,
+ *                              const std::vector<cv::Matx33f>& inv_upper)
+ *         cpp/inc/graph.hpp:120-122, cpp/src/graph.cpp:503-536
  *   dofs_lift / dofs_lift_batch
  *       ← Solution get_bottom_variants(const cv::Point2f& dir, const std::vector<cv::Point2i>& box,
  *                                      const cv::Matx33f& mat, const cv::Matx33f& inv,
@@ -111,6 +120,14 @@ typedef struct dofs_result {
     dofs_stats stats;
 } dofs_result;
 
+/* Edge (graph.hpp:13-17): same layout as the reference's struct {int start; int end; double weight;}
+ * (16 bytes), so a std::vector<Edge>'s data() can be passed as is. */
+typedef struct dofs_edge {
+    int32_t start;
+    int32_t end;
+    double weight;
+} dofs_edge;
+
 /* Per-merge record (debug / parity of the order-dependent replay): state of the merged set
  * right after Forest::merge (graph.cpp:170-218) for merge k in Kruskal order. */
 typedef struct dofs_event {
@@ -153,8 +170,26 @@ int32_t dofs_segment(dofs_ctx* ctx, const float* flow_uv, int32_t H, int32_t W, 
                      const float persp[9], const float inv[9], const float inv_upper[27],
                      const dofs_params* params, dofs_result* out);
 
+/* build_graph on a host field used AS GIVEN (get_segmented_array blurs first, segment.cpp:52-55): every
+ * edge of the 4-neighbourhood (neighborhood_8 == 0, the reference's default) or 8-neighbourhood, emitted
+ * per pixel in raster order as left, up, up-left, down-left (graph.cpp:62-93) with weight = diff
+ * (segment.cpp:20-32), sorted stably by weight (the std::multiset order, graph.cpp:55-60). Writes the
+ * sorted list to `edges` (host); *n_edges = E = build_graph's size; DOFS_ERR_CAPACITY (nothing written)
+ * if capacity < E. Synchronous. */
+int32_t dofs_build_graph(dofs_ctx* ctx, const float* flow_uv, int32_t H, int32_t W, size_t row_stride_bytes,
+                         int32_t neighborhood_8, dofs_edge* edges, int64_t capacity, int64_t* n_edges);
+
+/* segment_graph on a host field used AS GIVEN (the Forest's node flows, graph.cpp:129-148) and a host edge
+ * list processed in its order (graph.cpp:519-531: find both ends, new_merge if they differ) — any list,
+ * sorted or not, connected or not. Results as dofs_segment; stats.n_edges = n_edges, stats.n_merges =
+ * the unions performed (H*W-1 when the edges connect the frame); dofs_events then returns those merges.
+ * params: blur_sigma and neighbor are unused. An endpoint outside [0, H*W) is DOFS_ERR_INVALID_ARG. */
+int32_t dofs_segment_graph(dofs_ctx* ctx, const float* flow_uv, int32_t H, int32_t W, size_t row_stride_bytes,
+                           const dofs_edge* edges, int64_t n_edges, const float persp[9], const float inv[9],
+                           const float inv_upper[27], const dofs_params* params, dofs_result* out);
+
 /* Per-merge event stream of the last frame segmented by `ctx` (frame index within the last batch).
- * events must hold H*W-1 records. */
+ * events must hold H*W-1 records (dofs_segment_graph: stats.n_merges). */
 int32_t dofs_events(dofs_ctx* ctx, int32_t frame, dofs_event* events, int64_t capacity);
 
 /* Frame-parallel batch on device-resident input: d_flow = B×H×W×2 float32 (device pointer),
@@ -208,6 +243,8 @@ int32_t dofs_set_snapshot_capacity(dofs_ctx* ctx, int32_t per_frame);
 int32_t dofs_snapshot_capacity(dofs_ctx* ctx);
 /* Number of batches issued on ctx (the last batch id + 1). */
 int64_t dofs_batch_count(dofs_ctx* ctx);
+/* Frames (B) of the last batch issued on ctx (0 if none). */
+int32_t dofs_batch_frames(dofs_ctx* ctx);
 /* Number of batch workspaces (batches whose results stay readable; a caller that reads batch k's
  * results after submitting batch k + slots - 1 keeps every stage of the pipeline busy). */
 int32_t dofs_batch_slots(dofs_ctx* ctx);

@@ -51,6 +51,9 @@ def lib(opt: str = "O2") -> C.CDLL:
     L.oracle_segment.argtypes = [fp, C.c_int32, C.c_int32, fp, fp, fp, C.POINTER(DofsParams), C.c_int32,
                                  C.POINTER(DofsResult), C.POINTER(DofsEvent)]
     L.oracle_segment.restype = C.c_int32
+    L.oracle_segment_graph.argtypes = [fp, C.c_int32, C.c_int32, ip, ip, dp, C.c_int64, fp, fp, fp,
+                                       C.POINTER(DofsParams), C.c_int32, C.POINTER(DofsResult), C.POINTER(DofsEvent)]
+    L.oracle_segment_graph.restype = C.c_int32
     _LIBS[name] = L
     return L
 
@@ -175,6 +178,41 @@ def segment(flow: np.ndarray, persp, inv, inv_upper, params: DofsParams | None =
     st = {k: getattr(res.stats, k) for k, _ in res.stats._fields_}
     return OracleResult(H, W, snaps[:res.n_snapshots].copy(), labels, leaf, blurred, st,
                         ev[:max(N - 1, 0)] if events else None)
+
+
+def segment_graph(flow: np.ndarray, start, end, weight, persp, inv, inv_upper, params: DofsParams | None = None,
+                  mode: int = 0, events: bool = False) -> OracleResult:
+    """segment_graph(flow, edges, ...) restated on the CPU: Kruskal over the given edge list in order, on the
+    flow as given (no blur)."""
+    flow = _f(flow)
+    H, W = flow.shape[:2]
+    N = H * W
+    if params is None:
+        params = default_params()
+    s = np.ascontiguousarray(start, np.int32)
+    e = np.ascontiguousarray(end, np.int32)
+    w = np.ascontiguousarray(weight, np.float64)
+    cap = max(N, 1)
+    snaps = np.zeros(cap, dtype=DofsSnapshot.np_dtype())
+    labels = np.zeros(N, np.int32)
+    leaf = np.zeros(N, np.int32)
+    blurred = np.zeros((H, W, 2), np.float32)
+    ev = np.zeros(max(N - 1, 1), dtype=DofsEvent.np_dtype()) if events else None
+    res = DofsResult()
+    res.snapshots = snaps.ctypes.data_as(C.POINTER(DofsSnapshot))
+    res.snapshot_capacity = cap
+    res.labels = _ptr(labels, C.c_int32)
+    res.leaf_order = _ptr(leaf, C.c_int32)
+    res.blurred = _ptr(blurred, C.c_float)
+    rc = lib().oracle_segment_graph(_ptr(flow, C.c_float), H, W, _ptr(s, C.c_int32), _ptr(e, C.c_int32),
+                                    _ptr(w, C.c_double), C.c_int64(len(s)), _ptr(_f(persp), C.c_float),
+                                    _ptr(_f(inv), C.c_float), _ptr(_f(inv_upper), C.c_float), C.byref(params), mode,
+                                    C.byref(res), ev.ctypes.data_as(C.POINTER(DofsEvent)) if events else None)
+    if rc != 0:
+        raise RuntimeError(f"oracle_segment_graph failed with status {rc}")
+    st = {k: getattr(res.stats, k) for k, _ in res.stats._fields_}
+    return OracleResult(H, W, snaps[:res.n_snapshots].copy(), labels, leaf, blurred, st,
+                        ev[:int(res.stats.n_merges)] if events else None)
 
 
 # ---- Farneback dense optical flow (SURVEY.md §8(f) #1; oracle/farneback.cpp) ----------------------

@@ -544,10 +544,14 @@ void fill_snapshot(dofs_snapshot* s, int slot, const Slot& sl, int seg_begin) {
 }
 
 // --- fast mode ------------------------------------------------------------------------------
-int segment_fast(Ctx& cx, const float* blurred, std::vector<Slot>& hist, Krt& krt, std::vector<dofs_event>* ev) {
+// given: segment_graph on a caller's edge list (graph.cpp:503-536), else build_graph's (graph.cpp:51-103)
+int segment_fast(Ctx& cx, const float* blurred, std::vector<Slot>& hist, Krt& krt, std::vector<dofs_event>* ev,
+                 const std::vector<Edge>* given = nullptr) {
     const int W = cx.W, H = cx.H, N = W * H;
     bool nbr8 = (cx.prm->neighbor == 8);
-    std::vector<Edge> edges = build_graph_fast(blurred, W, H, nbr8);
+    std::vector<Edge> built;
+    if (!given) built = build_graph_fast(blurred, W, H, nbr8);
+    const std::vector<Edge>& edges = given ? *given : built;
     cx.st.n_edges = (int64_t)edges.size();
     std::vector<int> parent(N), rank(N, 0), size(N, 1);
     std::vector<float> fx(N), fy(N);
@@ -622,10 +626,12 @@ struct FSegmentData {  // graph.hpp:48-57
 };
 
 int segment_faithful(Ctx& cx, const float* blurred, std::vector<Slot>& hist, Krt& krt, std::vector<dofs_event>* ev,
-                     std::vector<std::set<int>>* snap_sets) {
+                     std::vector<std::set<int>>* snap_sets, const std::vector<Edge>* given = nullptr) {
     const int W = cx.W, H = cx.H, N = W * H;
     bool nbr8 = (cx.prm->neighbor == 8);
-    std::vector<Edge> edges = build_graph_faithful(blurred, W, H, nbr8);  // graph.cpp:51-103
+    std::vector<Edge> built;
+    if (!given) built = build_graph_faithful(blurred, W, H, nbr8);  // graph.cpp:51-103
+    const std::vector<Edge>& edges = given ? *given : built;
     cx.st.n_edges = (int64_t)edges.size();
     // Forest ctor, graph.cpp:129-148
     std::vector<FNode> nodes((size_t)N);
@@ -819,9 +825,36 @@ void oracle_synth_flow(float* out, int32_t H, int32_t W, uint64_t seed) {
 // get_segmented_array + get_best_segments + overlay labels. mode 0 = fast, 1 = faithful,
 // 2 = faithful with a self-check of every snapshot's std::set against its leaf range.
 // events (optional) must hold H*W-1 records. Returns DOFS_OK or an error code.
+static int32_t segment_common(const float* flow_uv, int32_t H, int32_t W, const float persp[9], const float inv[9],
+                              const float inv_upper[27], const dofs_params* params, int32_t mode, dofs_result* out,
+                              dofs_event* events, const std::vector<Edge>* given);
+
 int32_t oracle_segment(const float* flow_uv, int32_t H, int32_t W, const float persp[9], const float inv[9],
                        const float inv_upper[27], const dofs_params* params, int32_t mode, dofs_result* out,
                        dofs_event* events) {
+    return segment_common(flow_uv, H, W, persp, inv, inv_upper, params, mode, out, events, nullptr);
+}
+
+// segment_graph(flow, sorted_graph, ...) (graph.cpp:503-536) on a caller's edge list, taken in the given
+// order; the flow is used as given (no blur: get_segmented_array blurs before build_graph, segment.cpp:52).
+// events (optional) must hold H*W-1 records; n_merges in the stats says how many are written.
+int32_t oracle_segment_graph(const float* flow_uv, int32_t H, int32_t W, const int32_t* start, const int32_t* end,
+                             const double* weight, int64_t E, const float persp[9], const float inv[9],
+                             const float inv_upper[27], const dofs_params* params, int32_t mode, dofs_result* out,
+                             dofs_event* events) {
+    if (E < 0 || (E > 0 && (!start || !end || !weight))) return DOFS_ERR_INVALID_ARG;
+    const int64_t N = (int64_t)H * W;
+    std::vector<Edge> edges((size_t)E);
+    for (int64_t i = 0; i < E; ++i) {
+        if (start[i] < 0 || start[i] >= N || end[i] < 0 || end[i] >= N) return DOFS_ERR_INVALID_ARG;
+        edges[(size_t)i] = Edge{start[i], end[i], weight[i]};
+    }
+    return segment_common(flow_uv, H, W, persp, inv, inv_upper, params, mode, out, events, &edges);
+}
+
+static int32_t segment_common(const float* flow_uv, int32_t H, int32_t W, const float persp[9], const float inv[9],
+                              const float inv_upper[27], const dofs_params* params, int32_t mode, dofs_result* out,
+                              dofs_event* events, const std::vector<Edge>* given) {
     if (H <= 0 || W <= 0 || !flow_uv || !out) return DOFS_ERR_INVALID_ARG;
     dofs_params prm;
     if (params)
@@ -831,7 +864,10 @@ int32_t oracle_segment(const float* flow_uv, int32_t H, int32_t W, const float p
     const int N = W * H;
     Ctx cx{W, H, persp, inv, inv_upper, &prm, dofs_stats{}};
     std::vector<float> blurred((size_t)N * 2);
-    blur_flow(flow_uv, H, W, prm.blur_sigma, blurred.data());  // segment.cpp:52
+    if (given)
+        std::memcpy(blurred.data(), flow_uv, sizeof(float) * 2 * (size_t)N);
+    else
+        blur_flow(flow_uv, H, W, prm.blur_sigma, blurred.data());  // segment.cpp:52
     std::vector<Slot> hist;
     Krt krt;
     std::vector<dofs_event> ev;
@@ -839,9 +875,10 @@ int32_t oracle_segment(const float* flow_uv, int32_t H, int32_t W, const float p
     std::vector<std::set<int>> sets;
     int merges;
     if (mode == 0)
-        merges = segment_fast(cx, blurred.data(), hist, krt, events ? &ev : nullptr);
+        merges = segment_fast(cx, blurred.data(), hist, krt, events ? &ev : nullptr, given);
     else
-        merges = segment_faithful(cx, blurred.data(), hist, krt, events ? &ev : nullptr, mode == 2 ? &sets : nullptr);
+        merges = segment_faithful(cx, blurred.data(), hist, krt, events ? &ev : nullptr, mode == 2 ? &sets : nullptr,
+                                  given);
     cx.st.n_merges = merges;
     std::vector<int> leaf_order, first;
     krt.order(leaf_order, first);
@@ -878,7 +915,7 @@ int32_t oracle_segment(const float* flow_uv, int32_t H, int32_t W, const float p
     }
     if (out->leaf_order) std::memcpy(out->leaf_order, leaf_order.data(), sizeof(int) * (size_t)N);
     if (out->blurred) std::memcpy(out->blurred, blurred.data(), sizeof(float) * 2 * (size_t)N);
-    if (events && N > 1) std::memcpy(events, ev.data(), sizeof(dofs_event) * ((size_t)N - 1));
+    if (events && merges > 0) std::memcpy(events, ev.data(), sizeof(dofs_event) * (size_t)merges);
     return DOFS_OK;
 }
 

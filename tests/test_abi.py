@@ -6,8 +6,8 @@ import re
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_symbols():
-    src = open(os.path.join(ROOT, "include", "dofs.h")).read()
+def declared_symbols(header="dofs.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(dofs_[a-z0-9_]+)\s*\(", src)))
 
@@ -26,6 +26,17 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
 
 
+def test_rccl_library_exports_every_declared_symbol():
+    """libdofs_rccl.so (include/dofs_rccl.h) loads without a GPU and exports its entry points."""
+    from denseopticalflowsegmentation3d_amd import runtime
+    lib = runtime.load_rccl()
+    names = [n for n in declared_symbols("dofs_rccl.h") if n not in declared_symbols("dofs.h")]
+    assert "dofs_gather_records" in names and "dofs_comm_init" in names
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert lib.dofs_records_block_bytes(96, 64) == 4 * 96 + 88 * 96 * 64
+
+
 def test_abi_version_and_struct_layouts():
     from denseopticalflowsegmentation3d_amd import abi, runtime
     lib = runtime.load()
@@ -37,6 +48,7 @@ def test_abi_version_and_struct_layouts():
     # sizes fixed by the header (natural alignment, x86-64 and gfx950 alike)
     assert ctypes.sizeof(abi.DofsSolution) == 160 and ctypes.sizeof(abi.DofsSnapshot) == 208
     assert ctypes.sizeof(abi.DofsEvent) == 56 and ctypes.sizeof(abi.DofsBoxRecord) == 88
+    assert ctypes.sizeof(abi.DofsEdge) == 16
 
 
 def test_no_device_fails_loudly():

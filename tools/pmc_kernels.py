@@ -1,0 +1,100 @@
+"""Per-kernel PMC summary of a bench run (rocprofv3 --pmc passes, one counter group per pass).
+
+usage: python tools/pmc_kernels.py OUT_DIR CALIB_JSON K1,K2,... > summary.json
+
+OUT_DIR holds the pass directories pmc_fetch/ (FETCH_SIZE), pmc_write/ (WRITE_SIZE), pmc_sq/ (SQ
+issue/wait counters) and pmc_tcc/ (L2 hits / misses). For each kernel (functor or kernel name, e.g.
+k_krt_fused, KJump) the per-dispatch values are averaged.
+
+Counter semantics, from the calibration of tools/fetch_calib.hip (CALIB_JSON, tools/calib.py, gfx950):
+coalesced reads of 4, 8 and 16 B per lane all count exactly half their bytes in FETCH_SIZE (128-B
+lines tallied at 64 B), so their HBM bytes are 2 x FETCH_SIZE; a random 4- or 16-B read counts 64 B
+(one request); WRITE_SIZE counts coalesced stores exactly and a random 8-B store as 32 B. So
+hbm_read_bytes = 2 x FETCH_SIZE for kernels whose reads are coalesced (pattern "stream"), and FETCH_SIZE
+(one 64-B request per access, a lower bound) for kernels dominated by random accesses ("random").
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+# dominant access pattern of each kernel's reads (see the docstring)
+PATTERN = {
+    "k_boruvka_min": "stream",   # tile label / flow rows (LDS-staged), candidate words per pixel
+    "k_krt_fused": "random",     # union-find records, label / seed stores
+    "k_replay_long1": "stream",  # StepIn / RepVal records by preorder position (64-step chunks)
+    "KJump": "random",
+    "KPathInit": "random",
+    "KLift": "random",
+    "KFilter": "random",
+}
+
+
+def rows(d):
+    out = []
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        out.extend(csv.DictReader(open(f)))
+    return out
+
+
+def match(name, k):
+    return f"dofs::{k}(" in name or f"dofs::{k}>" in name or f"::{k}(" in name
+
+
+def per_dispatch(rs, k):
+    """{counter: mean over dispatches of the per-dispatch sum}"""
+    acc = {}
+    for r in rs:
+        if not match(r.get("Kernel_Name", ""), k):
+            continue
+        c = r["Counter_Name"]
+        acc.setdefault(c, {}).setdefault(r["Dispatch_Id"], 0.0)
+        acc[c][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return {c: (sum(v.values()) / len(v), len(v)) for c, v in acc.items()}
+
+
+def main():
+    out_dir, calib_path, kernels = sys.argv[1], sys.argv[2], sys.argv[3].split(",")
+    calib = json.load(open(calib_path)) if os.path.exists(calib_path) else {}
+    passes = {p: rows(os.path.join(out_dir, p)) for p in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_tcc")}
+    if not passes["pmc_fetch"]:  # tools/gpu_ab.sh layout: one directory per counter
+        passes["pmc_fetch"] = rows(os.path.join(out_dir, "FETCH_SIZE"))
+        passes["pmc_write"] = rows(os.path.join(out_dir, "WRITE_SIZE"))
+    res = {}
+    for k in kernels:
+        e = {}
+        f = per_dispatch(passes["pmc_fetch"], k).get("FETCH_SIZE")
+        w = per_dispatch(passes["pmc_write"], k).get("WRITE_SIZE")
+        pat = PATTERN.get(k, "stream")
+        e["read_pattern"] = pat
+        if f:
+            raw = f[0] * 1024  # KB -> B
+            e["dispatches"] = f[1]
+            e["fetch_size_raw_bytes"] = raw
+            e["hbm_read_bytes"] = 2 * raw if pat == "stream" else raw
+        if w:
+            e["write_size_raw_bytes"] = w[0] * 1024
+        if f and w:
+            e["hbm_bytes_per_launch"] = e["hbm_read_bytes"] + e["write_size_raw_bytes"]
+        e["calibration"] = {k2: v.get("fetch_over_known", v.get("write_over_known")) for k2, v in calib.items()}
+        sq = per_dispatch(passes["pmc_sq"], k)
+        if sq:
+            v = {c: x[0] for c, x in sq.items()}
+            e["sq"] = v
+            if v.get("SQ_WAVE_CYCLES"):
+                e["wait_any_frac"] = v.get("SQ_WAIT_ANY", 0) / v["SQ_WAVE_CYCLES"]
+                e["active_inst_frac"] = v.get("SQ_ACTIVE_INST_ANY", 0) / v["SQ_WAVE_CYCLES"]
+        tcc = per_dispatch(passes["pmc_tcc"], k)
+        if tcc:
+            v = {c: x[0] for c, x in tcc.items()}
+            e["tcc"] = v
+            h, m = v.get("TCC_HIT_sum"), v.get("TCC_MISS_sum")
+            if h is not None and m is not None and h + m > 0:
+                e["l2_hit_rate"] = h / (h + m)
+        res[k] = e
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
