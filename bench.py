@@ -100,7 +100,7 @@ def parse(argv=None):
     ap.add_argument("--no-h2d", action="store_true", help="skip the with-H2D (host input) pass")
     ap.add_argument("--probe", default=",".join(PROBES), help="kernels timed with device events (comma list)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02", "pmc_summary.json"),
-                    help="PMC summary JSON (tools/pmc_summary.py) for the roofline traffic")
+                    help="PMC summary JSON (tools/pmc_kernels.py via tools/pmc_round.sh) for the roofline traffic")
     ap.add_argument("--cpu-worker", nargs=4, metavar=("OPT", "H", "W", "SEED"), help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -354,10 +354,11 @@ def main(argv=None):
             ach = alg / (ms / 1e3) / 1e9
             entry.update({"achieved": round(ach, 3), "frac": round(ach / HBM_PEAK_GBS, 6),
                           "alg_bytes_per_launch": round(alg / launches)})
-            pk = pmc.get(name)
-            if pk:
-                entry["traffic"] = pk["hbm_bytes_per_launch"]
+            pk = pmc.get(name) or pmc.get(name + "1")  # k_replay_long's one-wave kernel is k_replay_long1
+            if pk and pk.get("hbm_bytes_per_launch"):
+                entry["traffic"] = round(pk["hbm_bytes_per_launch"])
                 entry["traffic_over_alg"] = round(pk["hbm_bytes_per_launch"] / (alg / launches), 3)
+                entry["traffic_read_pattern"] = pk.get("read_pattern")
         kern.append(entry)
     kern.sort(key=lambda e: -e["ms_per_batch"])
     roof = None

@@ -788,6 +788,26 @@ __device__ inline int lds_union(int* P, const int* SZ, int a, int b) {
     }
 }
 
+// Measurement build only (-DDOFS_KRT_TIMING): thread 0 of each KRT workgroup adds the wall-clock time
+// (100 MHz counter) of each phase to g_kt[i] (read by dofs_debug_krt_timing; tools/krt_timing.py).
+#ifdef DOFS_KRT_TIMING
+__device__ unsigned long long g_kt[16];
+#define KT_DECL unsigned long long kt_last = wall_clock64();
+#define KT(i)                                                  \
+    do {                                                       \
+        if (threadIdx.x == 0) {                                \
+            const unsigned long long kt_now = wall_clock64();  \
+            atomicAdd(&g_kt[i], kt_now - kt_last);             \
+            kt_last = kt_now;                                  \
+        }                                                      \
+    } while (0)
+#else
+#define KT_DECL
+#define KT(i) \
+    do {      \
+    } while (0)
+#endif
+
 struct DeepShared {
     int hkey[kDeepHT];    // global label in the slot (-1 empty)
     short hval[kDeepHT];  // compact local id of the slot
@@ -843,6 +863,7 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
         sh.P[x] = x;
         sh.CS[x] = 0;
         sh.MX[x] = -1;
+        if (x >= kDeepK) sh.SZ[x] = -1;  // the block's new nodes: written once, at the end
     }
     __syncthreads();
     for (int t = tid; t < cnt; t += kDeepT) {
@@ -850,6 +871,7 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
         sh.lv[t] = sh.hval[sh.lv[t]];
     }
     __syncthreads();
+    KT_DECL
     for (int S = kDeepS; S >= 2; S >>= 1) {
         const int half = S >> 1;
         // union (L edges of sub-blocks whose R half exists)
@@ -884,9 +906,7 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
                     continue;
                 }
                 sh.lrr[t] = (short)r;
-                const int sz = sh.CS[r] + sh.SZ[r];
-                sh.SZ[kDeepK + t] = sz;
-                w.SZ[lb + d.N + s0 + t] = sz;
+                sh.SZ[kDeepK + t] = sh.CS[r] + sh.SZ[r];  // to global at the end (no store drain per depth)
             } else {
                 for (int side = 0; side < 2; ++side) {
                     short* lp = side ? sh.lv : sh.lu;
@@ -909,6 +929,7 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
             }
         }
         __syncthreads();
+        KT(S >= 256 ? 9 : 10);  // the upper depths (S >= 256) and the lower ones
     }
     // final labels (the edge's KRT children) as global ids: a local id below kDeepK was never
     // relabeled, so it is still the edge's own input label
@@ -916,6 +937,8 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
         const int a = sh.lu[t], b = sh.lv[t];
         if (a >= kDeepK) w.lu[eb + s0 + t] = (int)(d.N + s0 + (a - kDeepK));
         if (b >= kDeepK) w.lv[eb + s0 + t] = (int)(d.N + s0 + (b - kDeepK));
+        const int z = sh.SZ[kDeepK + t];
+        if (z >= 0) w.SZ[lb + d.N + s0 + t] = z;
     }
 }
 
@@ -1036,6 +1059,7 @@ __device__ void top_level(const Ws& w, TopShared& sh, int f, int64_t s0, int cnt
 struct ParentShared {
     int lp[kDeepTop];    // local parent (index in the block) of a block merge, -1: parent outside
     int loff[kDeepTop];  // offset to it
+    int lp2[kDeepTop], loff2[kDeepTop];  // the other buffer of the jumping rounds
 };
 __device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, int cnt) {
     const Dims& d = w.d;
@@ -1069,35 +1093,39 @@ __device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, in
     }
     __syncthreads();
     // pointer jumping to the block-top ancestor (a node whose parent is outside the block keeps
-    // lp = -1 and its word is written by the block of its parent)
+    // lp = -1 and its word is written by the block of its parent): double-buffered, one barrier per
+    // round, stopping at the first round in which no word advanced
+    int *lpa = sh.lp, *ofa = sh.loff, *lpb = sh.lp2, *ofb = sh.loff2;
     for (int it = 0; (1 << it) < cnt; ++it) {
-        int na[kDeepTop / kDeepT], ns[kDeepTop / kDeepT];
+        int moved = 0;
 #pragma unroll
         for (int k = 0; k < kDeepTop / kDeepT; ++k) {
             const int t = tid + k * kDeepT;
-            na[k] = -1;
             if (t >= cnt) continue;
-            const int p = sh.lp[t];
-            na[k] = p;
-            ns[k] = sh.loff[t];
-            if (p >= 0 && sh.lp[p] >= 0) {
-                na[k] = sh.lp[p];
-                ns[k] += sh.loff[p];
+            int p = lpa[t], o = ofa[t];
+            if (p >= 0) {
+                const int pp = lpa[p];
+                if (pp >= 0) {
+                    o += ofa[p];
+                    p = pp;
+                    moved = 1;
+                }
             }
+            lpb[t] = p;
+            ofb[t] = o;
         }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < kDeepTop / kDeepT; ++k) {
-            const int t = tid + k * kDeepT;
-            if (t >= cnt) continue;
-            sh.lp[t] = na[k];
-            sh.loff[t] = ns[k];
-        }
-        __syncthreads();
+        const int any = __syncthreads_or(moved);
+        int* x = lpa;
+        lpa = lpb;
+        lpb = x;
+        x = ofa;
+        ofa = ofb;
+        ofb = x;
+        if (!any) break;
     }
     for (int t = tid; t < cnt; t += kDeepT) {
-        const int p = sh.lp[t];
-        if (p >= 0) w.J[lb + x0 + t] = jump_pack((int)(x0 + p), sh.loff[t]);
+        const int p = lpa[t];
+        if (p >= 0) w.J[lb + x0 + t] = jump_pack((int)(x0 + p), ofa[t]);
     }
 }
 static_assert(kDeepTop % kDeepT == 0, "parent epilogue shape");
@@ -1108,12 +1136,18 @@ constexpr size_t kDeepSmem = kDeepSmem0 > sizeof(ParentShared) ? kDeepSmem0 : si
 __device__ void deep_item(const Ws& w, char* smem, int f, int64_t s0) {
     const Dims& d = w.d;
     const int cnt = (int)((d.M - s0) < kDeepTop ? (d.M - s0) : kDeepTop);
+    KT_DECL
     if (cnt > kDeepS) top_level(w, *reinterpret_cast<TopShared*>(smem), f, s0, cnt);
+    KT(5);
     deep_block(w, *reinterpret_cast<DeepShared*>(smem), f, s0, cnt < kDeepS ? cnt : kDeepS);
     __syncthreads();
+    KT(6);
     if (cnt > kDeepS) deep_block(w, *reinterpret_cast<DeepShared*>(smem), f, s0 + kDeepS, cnt - kDeepS);
     __syncthreads();
+    KT(7);
     deep_parent(w, *reinterpret_cast<ParentShared*>(smem), f, s0, cnt);
+    __syncthreads();
+    KT(8);
 }
 __global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
     __shared__ __attribute__((aligned(16))) char smem[kDeepSmem];
@@ -1138,31 +1172,10 @@ constexpr int kTileX = 32, kTileY = 8, kMinHT = 512;  // 512 > 256 pixels + 82 h
 // leaving the component has an end in it), reduced per wave and per tile before one global atomic.
 // Pass 1 then only compares each pixel's kept weight with its component's minimum and reduces the
 // kept indices of the equal ones — no weights recomputed, no neighbour reads.
-// Pass 0 stages each tile's labels and blurred flows with a one-pixel halo in LDS (coalesced row loads,
-// each word once), and every pixel reads its eight neighbours from there.
-// Tile order: a block walks a contiguous run of tiles in raster order (a row segment's left / right halo
-// lines were just loaded by the same CU), and blocks that share an XCD (blockIdx.x % 8 when the grid
-// width is a multiple of 8) take contiguous bands of the frame, so the halo rows shared with the tiles
-// above and below are read through one L2 (MI355X_MICROARCH.md §Workgroup dispatch, XCD placement).
-constexpr int kHaloX = kTileX + 2, kHalo = kHaloX * (kTileY + 2);
-__device__ __forceinline__ void tile_run(int tiles, int& t0, int& t1) {
-    const int gx = gridDim.x, x = blockIdx.x;
-    if (gx % 8 == 0 && gx >= 64) {
-        const int g = x % 8, j = x / 8, G = gx / 8;
-        const int b0 = (int)((int64_t)g * tiles / 8), n = (int)((int64_t)(g + 1) * tiles / 8) - b0;
-        t0 = b0 + (int)((int64_t)j * n / G);
-        t1 = b0 + (int)((int64_t)(j + 1) * n / G);
-    } else {
-        t0 = (int)((int64_t)x * tiles / gx);
-        t1 = (int)((int64_t)(x + 1) * tiles / gx);
-    }
-}
 __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass, unsigned char* tdone,
-                                                     unsigned long long* candw, unsigned* candi, int runs) {
+                                                     unsigned long long* candw, unsigned* candi) {
     __shared__ int hk[kMinHT];
     __shared__ unsigned long long hv[kMinHT];
-    __shared__ int sl[kHalo];
-    __shared__ F2 sf[kHalo];
     __shared__ int any, tany;
     const Dims& d = w.d;
     const int f = blockIdx.y;
@@ -1194,54 +1207,34 @@ __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass, unsi
         }
         atomicMin(hv + slot, v);
     };
-    int t0 = blockIdx.x, t1 = tiles, ts = gridDim.x;  // strided over the frame's tiles (balanced)
-    if (runs) {  // contiguous XCD-banded runs (DOFS_BMIN_RUNS=1)
-        tile_run(tiles, t0, t1);
-        ts = 1;
-    }
-    for (int t = t0; t < t1; t += ts) {
+    for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
         if (td[t]) continue;  // block-uniform
-        const int tx0 = (t % tiles_x) * kTileX, ty0 = (t / tiles_x) * kTileY;
-        if (pass == 0) {  // the tile and its one-pixel halo into LDS, row by row (out-of-frame cells unused)
-            for (int e = tid; e < kHalo; e += 256) {
-                const int gx = tx0 - 1 + e % kHaloX, gy = ty0 - 1 + e / kHaloX;
-                if (gx >= 0 && gx < d.W && gy >= 0 && gy < d.H) {
-                    const int64_t q = (int64_t)gy * d.W + gx;
-                    sl[e] = comp[q];
-                    sf[e] = b[q];
-                }
-            }
-            __syncthreads();
-        }
-        const int x = tx0 + (tid % kTileX), y = ty0 + tid / kTileX;
+        const int x = (t % tiles_x) * kTileX + (tid % kTileX), y = (t / tiles_x) * kTileY + tid / kTileX;
         int cp = -1;
         unsigned long long own = ~0ull;  // pass 0: the pixel's minimum weight; pass 1: its index
         if (x < d.W && y < d.H) {
             const int64_t p = (int64_t)y * d.W + x;
             if (pass == 0) {
-                // Slots 0-3: the edges p emits (left, up, up-left, down-left); 4-7: the edges its right,
-                // lower, lower-right and upper-right neighbours emit towards it. An absent neighbour
-                // reads the pixel itself and is masked below.
+                // all loads first, from in-frame addresses (an absent neighbour reads the pixel
+                // itself and is masked below), so the wave waits on memory once per tile instead of
+                // once per edge. Slots 0-3: the edges p emits (left, up, up-left, down-left); 4-7:
+                // the edges its right, lower, lower-right and upper-right neighbours emit towards it.
                 const int64_t W = d.W;
                 const bool xl = x > 0, xr = x + 1 < d.W, yu = y > 0, yd = y + 1 < d.H;
                 const bool ok[8] = {xl, yu, d.nbr8 && xl && yu, d.nbr8 && xl && yd,
                                     xr, yd, d.nbr8 && xr && yd, d.nbr8 && xr && yu};
                 const int64_t nb[8] = {p - 1, p - W, p - W - 1, p + W - 1, p + 1, p + W, p + W + 1, p - W + 1};
-                const int e0 = (tid / kTileX + 1) * kHaloX + tid % kTileX + 1;
-                const int ne[8] = {e0 - 1, e0 - kHaloX, e0 - kHaloX - 1, e0 + kHaloX - 1,
-                                   e0 + 1, e0 + kHaloX, e0 + kHaloX + 1, e0 - kHaloX + 1};
                 int64_t q[8];
                 int cq[8];
                 F2 bq[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) q[j] = ok[j] ? nb[j] : p;
-                cp = sl[e0];
-                const F2 bp = sf[e0];
+                cp = comp[p];
+                const F2 bp = b[p];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const int ej = ok[j] ? ne[j] : e0;
-                    cq[j] = sl[ej];
-                    bq[j] = sf[ej];
+                    cq[j] = comp[q[j]];
+                    bq[j] = b[q[j]];
                 }
                 unsigned allow_bits = 0xff;  // bit j: slot j's edge may be in the MST
                 if (w.allow) {               // launch-uniform
@@ -1526,8 +1519,12 @@ __device__ __forceinline__ void rec_find(SeqRec* rec, int (&x)[K], bool (&pend)[
 __device__ __forceinline__ constexpr bool seq_compress() { return DOFS_SEQ_COMPRESS != 0; }
 // Per block of kSeqB merges (four barrier-separated phases):
 //   A  endpoint roots at the block start -> labels (lu, lv)
-//   B  the block's unions: one CAS per merge (parents always point to lower hash priority, so a
-//      root may be hooked onto any node of lower priority without forming a cycle)
+//   B  the block's unions: one CAS per merge. A root is hooked under the other root by the key
+//      (size at the block start, hash priority), which no write of the block changes, so parents
+//      only ever point to a larger key and a root may be hooked onto a node that was hooked
+//      meanwhile without forming a cycle. Union by size keeps a frame's large components' roots
+//      stable (a pixel joining the largest cluster hangs one hop below its root), so the finds of
+//      later blocks are short; linking by hash priority alone moved the root O(log n) times.
 //   C  each merge's resulting root R, aggregated per R in LDS: max rank in the block, sizes of the
 //      roots hooked into it, R's old size; the endpoints are compressed onto R
 //   D  per R: its new label and size (one 8-byte store) and the KRT node size SZ
@@ -1558,6 +1555,7 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
         hsz[x] = 0;
     }
     __syncthreads();
+    KT_DECL
     for (int64_t s = 0; s < d.M; s += kSeqB) {
         const int cnt = (int)((d.M - s) < kSeqB ? (d.M - s) : kSeqB);
         // ---- A
@@ -1596,6 +1594,7 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
         if (progress && tid == 0)
             __hip_atomic_store(progress + (int64_t)f * kCounters, (int)(s / kSeqB) + 1, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+        KT(0);
         // ---- B
         int hooked_sz[K];
         {
@@ -1619,11 +1618,14 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     if (!todo[k]) continue;
+                    // union by size at the block start (roots' sizes change only in phase D, so the
+                    // key (size, hash priority) is static during the block), ties by hash priority
                     int a = x[2 * k], b = x[2 * k + 1], sa = r2s[2 * k];
-                    if (!uf_above(a, b)) {
+                    const int sb = r2s[2 * k + 1];
+                    if (!(sa != sb ? sa < sb : uf_above(a, b))) {
                         a = x[2 * k + 1];
                         b = x[2 * k];
-                        sa = r2s[2 * k + 1];
+                        sa = sb;
                     }
                     if (wg_cas(&rec[a].par, a, b) == a) {
                         hooked_sz[k] = sa;
@@ -1638,6 +1640,7 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
             }
         }
         __syncthreads();
+        KT(1);
         // ---- C
         {
             int R[K];
@@ -1670,6 +1673,7 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
             }
         }
         __syncthreads();
+        KT(2);
         // ---- D
 #pragma unroll
         for (int q = 0; q < KS; ++q) {
@@ -1689,6 +1693,7 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
             hsz[x] = 0;
         }
         __syncthreads();
+        KT(3);
     }
 }
 
@@ -1869,6 +1874,7 @@ __global__ __launch_bounds__(kDeepT) void k_krt_fused(Ws w, int* progress) {
         if (it >= nblk * B) break;
         const int f = it % B;
         const int64_t k = it / B;
+        KT_DECL
         if (tid == 0) {
             while (__hip_atomic_load(progress + f * kCounters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k + 1)
                 __builtin_amdgcn_s_sleep(8);
@@ -1876,6 +1882,7 @@ __global__ __launch_bounds__(kDeepT) void k_krt_fused(Ws w, int* progress) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
+        KT(11);
         deep_item(w, smem, f, k * kDeepTop);
         __syncthreads();
     }
@@ -2254,12 +2261,7 @@ struct HipBackend {
     }
     void boruvka_min(const Ws& w, int r, int pass) {
         const int64_t tiles = (int64_t)((w.d.W + kTileX - 1) / kTileX) * ((w.d.H + kTileY - 1) / kTileY);
-        int64_t gx = std::min<int64_t>(tiles, std::max<int64_t>(1, grid_cap() / w.d.B));
-        static const int runs = [] {
-            const char* e = getenv("DOFS_BMIN_RUNS");
-            return e ? atoi(e) : 0;
-        }();
-        if (runs && gx >= 64) gx &= ~(int64_t)7;  // a multiple of 8: XCD-banded tile runs (tile_run)
+        const int64_t gx = std::min<int64_t>(tiles, std::max<int64_t>(1, grid_cap() / w.d.B));
         unsigned char* tdone = w.hlB;  // free during the MST (KDncParent fills it after the KRT)
         static_assert(sizeof(*w.hlB) == 1, "tile flags are bytes");
         if (r == 1 && pass == 0) memset(tdone, 0, (size_t)tiles * w.d.B);  // tiles <= M per frame
@@ -2267,8 +2269,7 @@ struct HipBackend {
             // kept candidates: the row-blur temporary (8 B per pixel, dead after the blur) and the
             // MST-count words (written only after the MST)
             hipLaunchKernelGGL(k_boruvka_min, dim3((unsigned)gx, (unsigned)w.d.B), dim3(256), 0, stream, w, r, pass,
-                               tdone, reinterpret_cast<unsigned long long*>(w.tmp), reinterpret_cast<unsigned*>(w.cnt),
-                               runs);
+                               tdone, reinterpret_cast<unsigned long long*>(w.tmp), reinterpret_cast<unsigned*>(w.cnt));
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_boruvka_min launch");
     }
@@ -2432,6 +2433,18 @@ struct HipBackend {
 };
 
 }  // namespace dofs
+
+#ifdef DOFS_KRT_TIMING
+// Measurement build only: the KRT phase times accumulated since the last call (microseconds), then reset.
+extern "C" int dofs_debug_krt_timing(double* out_us, int n) {
+    unsigned long long v[16] = {0};
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(dofs::g_kt), sizeof(v)) != hipSuccess) return -1;
+    const unsigned long long z[16] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(dofs::g_kt), z, sizeof(z));
+    for (int i = 0; i < n && i < 16; ++i) out_us[i] = (double)v[i] / 100.0;  // 100 MHz wall clock
+    return 16;
+}
+#endif
 
 using DofsBackend = dofs::HipBackend;
 #include "dofs_cabi.inc.h"

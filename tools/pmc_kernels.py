@@ -1,6 +1,8 @@
 """Per-kernel PMC summary of a bench run (rocprofv3 --pmc passes, one counter group per pass).
 
-usage: python tools/pmc_kernels.py OUT_DIR CALIB_JSON K1,K2,... > summary.json
+usage: python tools/pmc_kernels.py OUT_DIR CALIB_JSON K1,K2,... [BATCH] > summary.json
+
+Output: {"batch", "height", "width", "kernels": {name: ...}} — bench.py --pmc reads it (roofline traffic).
 
 OUT_DIR holds the pass directories pmc_fetch/ (FETCH_SIZE), pmc_write/ (WRITE_SIZE), pmc_sq/ (SQ
 issue/wait counters) and pmc_tcc/ (L2 hits / misses). For each kernel (functor or kernel name, e.g.
@@ -93,7 +95,8 @@ def main():
             if h is not None and m is not None and h + m > 0:
                 e["l2_hit_rate"] = h / (h + m)
         res[k] = e
-    print(json.dumps(res, indent=1))
+    batch = int(sys.argv[4]) if len(sys.argv) > 4 else 96
+    print(json.dumps({"batch": batch, "height": 1080, "width": 1920, "kernels": res}, indent=1))
 
 
 if __name__ == "__main__":

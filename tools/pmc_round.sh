@@ -22,5 +22,5 @@ run pmc_fetch rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format 
 run pmc_write rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python $BENCH
 run pmc_sq rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS -d $O/pmc_sq -o run --output-format csv -- python $BENCH
 run pmc_tcc rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d $O/pmc_tcc -o run --output-format csv -- python $BENCH
-python tools/pmc_kernels.py $O $O/fetch_calib.json $KS > $O/pmc_kernels.json || exit 1
+python tools/pmc_kernels.py $O $O/fetch_calib.json $KS $B > $O/pmc_kernels.json || exit 1
 cat $O/pmc_kernels.json
