@@ -855,7 +855,8 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
         for (int x = beg; x < end; ++x)
             if (sh.hkey[x] != -1) {
                 sh.hval[x] = (short)base;
-                sh.SZ[base] = w.SZ[lb + sh.hkey[x]];
+                const int g = sh.hkey[x];
+                sh.SZ[base] = g < d.N ? 1 : w.SZ[lb + g];  // a pixel label is a leaf (size 1): no load
                 ++base;
             }
     }
@@ -1002,7 +1003,8 @@ __device__ void top_level(const Ws& w, TopShared& sh, int f, int64_t s0, int cnt
         for (int x = beg; x < end; ++x)
             if (sh.hkey[x] != -1) {
                 sh.hval[x] = (short)base;
-                sh.SZ[base] = w.SZ[lb + sh.hkey[x]];
+                const int g = sh.hkey[x];
+                sh.SZ[base] = g < d.N ? 1 : w.SZ[lb + g];  // a pixel label is a leaf (size 1): no load
                 ++base;
             }
     }
@@ -1060,35 +1062,43 @@ struct ParentShared {
     int lp[kDeepTop];    // local parent (index in the block) of a block merge, -1: parent outside
     int loff[kDeepTop];  // offset to it
     int lp2[kDeepTop], loff2[kDeepTop];  // the other buffer of the jumping rounds
+    unsigned char lit[kDeepTop];         // path-top flag of a block merge whose parent is in the block
 };
 __device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, int cnt) {
     const Dims& d = w.d;
     const int64_t lb = f * d.NL, eb = f * d.M;
     const int tid = threadIdx.x;
     const int64_t x0 = d.N + s0;  // node id of the block's first merge
-    for (int t = tid; t < cnt; t += kDeepT) sh.lp[t] = -1;
+    for (int t = tid; t < cnt; t += kDeepT) {
+        sh.lp[t] = -1;
+        sh.lit[t] = 0xFF;
+    }
     __syncthreads();
     for (int t = tid; t < cnt; t += kDeepT) {
         const int a = w.lu[eb + s0 + t], b = w.lv[eb + s0 + t];
-        const int sa = w.SZ[lb + a], sb = w.SZ[lb + b];
+        const int sa = a < d.N ? 1 : w.SZ[lb + a], sb = b < d.N ? 1 : w.SZ[lb + b];  // leaves: no load
         const bool lightB = sa >= sb;
         const int h = lightB ? a : b, l = lightB ? b : a;
         const int offl = 2 * (lightB ? sa : sb);
         const int x = (int)(x0 + t);
         w.hlB[eb + s0 + t] = lightB ? 1 : 0;
-        w.lite[lb + h] = 0;
-        w.lite[lb + l] = 1;
+        // path-top flags: read by KPathInit for merge nodes only (a leaf needs none); a child merge of
+        // this block gets its flag in LDS (stored with the block's flags at the end, coalesced)
         if (h >= x0 && h < x0 + cnt) {
             sh.lp[h - x0] = t;
             sh.loff[h - x0] = 1;
+            sh.lit[h - x0] = 0;
         } else {
             w.J[lb + h] = jump_pack(x, 1);
+            if (h >= d.N) w.lite[lb + h] = 0;
         }
         if (l >= x0 && l < x0 + cnt) {
             sh.lp[l - x0] = t;
             sh.loff[l - x0] = offl;
+            sh.lit[l - x0] = 1;
         } else {
             w.J[lb + l] = jump_pack(x, offl);
+            if (l >= d.N) w.lite[lb + l] = 1;
         }
     }
     __syncthreads();
@@ -1126,6 +1136,8 @@ __device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, in
     for (int t = tid; t < cnt; t += kDeepT) {
         const int p = lpa[t];
         if (p >= 0) w.J[lb + x0 + t] = jump_pack((int)(x0 + p), ofa[t]);
+        const unsigned char v = sh.lit[t];
+        if (v != 0xFF) w.lite[lb + x0 + t] = v;
     }
 }
 static_assert(kDeepTop % kDeepT == 0, "parent epilogue shape");
@@ -1474,8 +1486,10 @@ __device__ __forceinline__ void rec_set_par(SeqRec* p, int v) { wg_st(&p->par, v
 // on return x[k] is the root and lab[k] / sz[k] its label and size (only the fields a caller needs
 // stay live, to keep the sweep within 128 VGPRs)
 template <int K>
-__device__ __forceinline__ void rec_find(SeqRec* rec, int (&x)[K], bool (&pend)[K], int (&lab)[K], int (&sz)[K]) {
+__device__ __forceinline__ void rec_find(SeqRec* rec, int (&x)[K], bool (&pend)[K], int (&lab)[K], int (&sz)[K],
+                                         int* rounds = nullptr) {
     for (;;) {
+        if (rounds) ++*rounds;
         int pp[K], pl[K], ps[K];
         bool any = false;
 #pragma unroll
@@ -1574,7 +1588,24 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
             c[k] = e[k];
             pend[k] = act2[k];
         }
+#ifdef DOFS_KRT_TIMING
+        {  // the slowest thread's find rounds (two dependent loads each) in phase A
+            int rounds = 0;
+            rec_find<K2>(rec, c, pend, rtl, rts, &rounds);
+            if (tid == 0) hmx[0] = 0;
+            __syncthreads();
+            atomicMax(hmx, rounds);
+            __syncthreads();
+            if (tid == 0) {
+                atomicAdd(&g_kt[12], (unsigned long long)hmx[0]);
+                atomicAdd(&g_kt[13], 1ull);
+                hmx[0] = -1;
+            }
+            __syncthreads();
+        }
+#else
         rec_find<K2>(rec, c, pend, rtl, rts);
+#endif
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             if (!act2[2 * k]) continue;

@@ -1096,7 +1096,7 @@ struct KPathInit {  // one lane per merge node x = N + k; path ids and lists thr
             int lt, lB;
             const int h = heavy_child(w, f, (int)x, &lt, &lB);
             StepIn in;
-            in.fs = (float)w.SZ[lb + h];
+            in.fs = h < d.N ? 1.f : (float)w.SZ[lb + h];  // a leaf has size 1 (no load)
             in.r = 1. / (double)w.SZ[lb + x];
             in.meta = (lB ? kStepB : 0) | (top ? kStepTop : 0);
             if (lt < d.N) {

@@ -1,0 +1,204 @@
+// san_driver.cpp — TEST INFRASTRUCTURE ONLY. The CPU oracle (oracle/*.cpp) and the test-only host emulator
+// of the product pipeline (tests/emu/dofs_emu.cpp: the product's kernel bodies and orchestration from
+// denseopticalflowsegmentation3d_amd/csrc, run sequentially) linked into one executable built with
+// -fsanitize=address,undefined (tests/sanitize/Makefile). It drives both on small inputs —
+// get_segmented_array (fast and faithful oracle modes), build_graph, segment_graph on shuffled / partial
+// lists, lifting, Farneback, overlay — and checks that the emulator equals the oracle, so every index the
+// product's kernel bodies compute is bounds-checked on the host. Exit 0 = clean and equal.
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <random>
+#include <vector>
+
+#include "../../include/dofs.h"
+
+extern "C" {
+void oracle_default_params(dofs_params* p);
+void oracle_calib(float persp[9], float inv[9], float inv_upper[27]);
+void oracle_synth_flow(float* out, int32_t H, int32_t W, uint64_t seed);
+void oracle_blur(const float* in, int32_t H, int32_t W, double sigma, float* out);
+int64_t oracle_build_graph(const float* flow, int32_t H, int32_t W, int32_t neighbor, int32_t* start, int32_t* end,
+                           double* weight, int64_t cap);
+int32_t oracle_segment(const float* flow_uv, int32_t H, int32_t W, const float persp[9], const float inv[9],
+                       const float inv_upper[27], const dofs_params* params, int32_t mode, dofs_result* out,
+                       dofs_event* events);
+int32_t oracle_segment_graph(const float* flow_uv, int32_t H, int32_t W, const int32_t* start, const int32_t* end,
+                             const double* weight, int64_t E, const float persp[9], const float inv[9],
+                             const float inv_upper[27], const dofs_params* params, int32_t mode, dofs_result* out,
+                             dofs_event* events);
+void oracle_lift(const float dir[2], const int32_t box[4], const float mat[9], const float inv[9],
+                 const float inv_upper[9], int32_t cls, dofs_solution* out);
+int32_t oracle_farneback(const uint8_t* prev, const uint8_t* next, int32_t rows, int32_t cols, double pyr_scale,
+                         int32_t levels, int32_t winsize, int32_t iterations, int32_t poly_n, double poly_sigma,
+                         int32_t flags, float* flow0);
+void oracle_overlay(const uint8_t* frame, int32_t H, int32_t W, const dofs_snapshot* snaps, int32_t n,
+                    const int32_t* leaf_order, double min_score, uint8_t* out);
+}
+
+static int fails = 0;
+#define CHECK(c, ...)                                         \
+    do {                                                      \
+        if (!(c)) {                                           \
+            fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+            fprintf(stderr, __VA_ARGS__);                     \
+            fprintf(stderr, "\n");                            \
+            ++fails;                                          \
+        }                                                     \
+    } while (0)
+
+struct Res {
+    std::vector<dofs_snapshot> snaps;
+    std::vector<int32_t> labels, leaf;
+    std::vector<float> blurred;
+    dofs_result r{};
+    explicit Res(int N) : snaps((size_t)std::max(N, 1)), labels((size_t)N), leaf((size_t)N), blurred((size_t)2 * N) {
+        r.snapshots = snaps.data();
+        r.snapshot_capacity = (int32_t)snaps.size();
+        r.labels = labels.data();
+        r.leaf_order = leaf.data();
+        r.blurred = blurred.data();
+    }
+};
+
+static std::vector<int> members(const Res& x, const dofs_snapshot& s) {
+    std::vector<int> m(x.leaf.begin() + s.seg_begin, x.leaf.begin() + s.seg_begin + s.size);
+    std::sort(m.begin(), m.end());
+    return m;
+}
+
+static void compare(const char* what, const Res& o, const Res& g, const std::vector<dofs_event>& eo,
+                    const std::vector<dofs_event>& eg, int64_t merges) {
+    CHECK(o.r.n_snapshots == g.r.n_snapshots, "%s: snapshots %d vs %d", what, o.r.n_snapshots, g.r.n_snapshots);
+    CHECK(o.labels == g.labels, "%s: labels", what);
+    CHECK(o.r.stats.n_merges == g.r.stats.n_merges && o.r.stats.n_candidates == g.r.stats.n_candidates,
+          "%s: stats", what);
+    for (int k = 0; k < std::min(o.r.n_snapshots, g.r.n_snapshots); ++k) {
+        const dofs_snapshot &a = o.snaps[k], &b = g.snaps[k];
+        CHECK(a.slot == b.slot && a.event == b.event && a.size == b.size && a.score == b.score, "%s: snapshot %d",
+              what, k);
+        CHECK(members(o, a) == members(g, b), "%s: members of snapshot %d", what, k);
+    }
+    for (int64_t i = 0; i < merges; ++i) {
+        const dofs_event &a = eo[i], &b = eg[i];
+        if (a.start != b.start || a.end != b.end || a.root != b.root || a.size != b.size || a.rank != b.rank ||
+            memcmp(a.mean, b.mean, sizeof(a.mean)) != 0 || memcmp(a.bbox, b.bbox, sizeof(a.bbox)) != 0) {
+            CHECK(false, "%s: event %lld", what, (long long)i);
+            break;
+        }
+    }
+}
+
+int main() {
+    float persp[9], inv[9], up[27];
+    oracle_calib(persp, inv, up);
+    dofs_params prm;
+    oracle_default_params(&prm);
+    dofs_ctx* ctx = dofs_create(0);  // the host emulator: always available
+    CHECK(ctx != nullptr, "emulator context");
+    if (!ctx) return 1;
+    struct Case {
+        int H, W;
+        uint64_t seed;
+        int min_size, nbr;
+    } cases[] = {{1, 1, 0, 1, 8}, {1, 6, 0, 1, 8}, {5, 1, 0, 1, 4}, {7, 9, 3, 2, 8}, {24, 32, 1, 20, 8},
+                 {30, 40, 5, 30, 4}, {64, 48, 7, 50, 8}, {90, 160, 0, 500, 8}, {120, 200, 2, 300, 8}};
+    std::mt19937 rng(7);
+    for (const Case& c : cases) {
+        const int N = c.H * c.W;
+        std::vector<float> flow((size_t)2 * N);
+        oracle_synth_flow(flow.data(), c.H, c.W, c.seed);
+        if (c.seed == 5)
+            for (auto& v : flow) v = roundf(v * 2.f) * 0.5f;  // massive exact ties
+        dofs_params p = prm;
+        p.min_size = c.min_size;
+        p.neighbor = c.nbr;
+        char name[64];
+        snprintf(name, sizeof(name), "%dx%d seed %llu", c.H, c.W, (unsigned long long)c.seed);
+        // get_segmented_array: oracle fast + faithful-with-self-check vs the emulated product path
+        Res o(N), of(N), g(N);
+        std::vector<dofs_event> eo((size_t)std::max(N - 1, 1)), eg(eo.size());
+        CHECK(oracle_segment(flow.data(), c.H, c.W, persp, inv, up, &p, 0, &o.r, eo.data()) == DOFS_OK, "%s", name);
+        CHECK(oracle_segment(flow.data(), c.H, c.W, persp, inv, up, &p, 2, &of.r, nullptr) == DOFS_OK,
+              "%s faithful self-check", name);
+        CHECK(dofs_segment(ctx, flow.data(), c.H, c.W, 0, persp, inv, up, &p, &g.r) == DOFS_OK, "%s emu", name);
+        CHECK(dofs_events(ctx, 0, eg.data(), (int64_t)eg.size()) == DOFS_OK, "%s events", name);
+        compare(name, o, g, eo, eg, N - 1);
+        CHECK(o.labels == of.labels && o.r.n_snapshots == of.r.n_snapshots, "%s fast vs faithful", name);
+        // build_graph on the blurred field, then segment_graph on shuffled and partial lists
+        std::vector<float> bl((size_t)2 * N);
+        oracle_blur(flow.data(), c.H, c.W, p.blur_sigma, bl.data());
+        const int64_t cap = 4 * (int64_t)N + 4;
+        std::vector<int32_t> s((size_t)cap), e((size_t)cap);
+        std::vector<double> wgt((size_t)cap);
+        const int64_t E = oracle_build_graph(bl.data(), c.H, c.W, c.nbr, s.data(), e.data(), wgt.data(), cap);
+        std::vector<dofs_edge> ge((size_t)std::max<int64_t>(cap, 1));
+        int64_t gE = 0;
+        CHECK(dofs_build_graph(ctx, bl.data(), c.H, c.W, 0, c.nbr == 8, ge.data(), cap, &gE) == DOFS_OK, "%s bg", name);
+        CHECK(gE == E, "%s edge count", name);
+        for (int64_t i = 0; i < std::min(E, gE); ++i)
+            if (ge[i].start != s[i] || ge[i].end != e[i] || memcmp(&ge[i].weight, &wgt[i], 8) != 0) {
+                CHECK(false, "%s edge %lld", name, (long long)i);
+                break;
+            }
+        for (int variant = 0; variant < 3; ++variant) {
+            std::vector<int64_t> idx((size_t)E);
+            for (int64_t i = 0; i < E; ++i) idx[i] = i;
+            if (variant == 1) std::shuffle(idx.begin(), idx.end(), rng);
+            if (variant == 2) idx.resize((size_t)(E / 2));
+            std::vector<int32_t> ss, ee;
+            std::vector<double> ww;
+            std::vector<dofs_edge> de;
+            for (int64_t i : idx) {
+                ss.push_back(s[i]);
+                ee.push_back(e[i]);
+                ww.push_back(wgt[i]);
+                de.push_back(dofs_edge{s[i], e[i], wgt[i]});
+            }
+            Res o2(N), g2(N);
+            std::vector<dofs_event> e2o(eo.size()), e2g(eo.size());
+            CHECK(oracle_segment_graph(bl.data(), c.H, c.W, ss.data(), ee.data(), ww.data(), (int64_t)ss.size(), persp,
+                                       inv, up, &p, 0, &o2.r, e2o.data()) == DOFS_OK, "%s sg oracle", name);
+            CHECK(dofs_segment_graph(ctx, bl.data(), c.H, c.W, 0, de.data(), (int64_t)de.size(), persp, inv, up, &p,
+                                     &g2.r) == DOFS_OK, "%s sg emu", name);
+            CHECK(dofs_events(ctx, 0, e2g.data(), (int64_t)e2g.size()) == DOFS_OK, "%s sg events", name);
+            compare(name, o2, g2, e2o, e2g, o2.r.stats.n_merges);
+        }
+        // overlay of the emulated result on a synthetic frame (the oracle's restatement) — bounds only
+        std::vector<uint8_t> frame((size_t)3 * N), out((size_t)3 * N);
+        for (size_t i = 0; i < frame.size(); ++i) frame[i] = (uint8_t)(i * 37);
+        oracle_overlay(frame.data(), c.H, c.W, o.snaps.data(), o.r.n_snapshots, o.leaf.data(), 0.7, out.data());
+    }
+    // lifting on random boxes (oracle and emulated device code share nothing but the inputs)
+    for (int i = 0; i < 200; ++i) {
+        const float dir[2] = {(float)(rng() % 600) / 100.f - 3.f, (float)(rng() % 600) / 100.f - 3.f};
+        const int x0 = (int)(rng() % 500), y0 = (int)(rng() % 300);
+        const int32_t box[4] = {x0, y0, x0 + 1 + (int)(rng() % 120), y0 + 1 + (int)(rng() % 60)};
+        const int cls = (int)(rng() % 3);
+        dofs_solution a{}, b{};
+        oracle_lift(dir, box, persp, inv, up + 9 * cls, cls, &a);
+        CHECK(dofs_lift(ctx, dir, box, persp, inv, up + 9 * cls, cls, &b) == DOFS_OK, "lift %d", i);
+        CHECK(a.valid == b.valid && a.cls == b.cls, "lift %d validity", i);
+    }
+    // Farneback on a small textured pair
+    {
+        const int H = 48, W = 64;
+        std::vector<uint8_t> g1((size_t)H * W), g2((size_t)H * W);
+        for (int y = 0; y < H; ++y)
+            for (int x = 0; x < W; ++x) {
+                g1[(size_t)y * W + x] = (uint8_t)((x * 7 + y * 13 + (x * y) % 29) & 0xFF);
+                g2[(size_t)y * W + x] = (uint8_t)(((x + 2) * 7 + (y + 1) * 13 + ((x + 2) * (y + 1)) % 29) & 0xFF);
+            }
+        std::vector<float> fl((size_t)2 * H * W);
+        CHECK(oracle_farneback(g1.data(), g2.data(), H, W, 0.5, 3, 15, 3, 5, 1.2, 0, fl.data()) > 0, "farneback");  // levels run
+    }
+    dofs_destroy(ctx);
+    if (fails) {
+        fprintf(stderr, "%d failure(s)\n", fails);
+        return 1;
+    }
+    printf("sanitized oracle + emulator: clean and equal\n");
+    return 0;
+}

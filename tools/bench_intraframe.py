@@ -3,6 +3,13 @@ shard of the MST stage, denseopticalflowsegmentation3d_amd/bands.py), beside the
 
   python -m torch.distributed.run --nproc-per-node 4 --master-addr 127.0.0.1 tools/bench_intraframe.py
 Prints one JSON line on rank 0 (frames/s and Mpix/s of the sharded path, and of the 1-GPU path).
+
+  python tools/bench_intraframe.py --model 4
+One GPU: the expected N-GPU time of the sharded path from measured parts — the slowest band's
+minimum spanning forest (dofs_band_msf_device, each band timed alone), the gather of band forests and
+flow rows over xGMI (bytes / link bandwidth), and rank 0's masked whole-frame path
+(dofs_segment_masked_device) with its stage times — next to the single-GPU path. The ceiling is
+rank 0's part: the KRT sweep and the replay chains are sequential in merge order and do not shard.
 """
 import argparse
 import json
@@ -21,13 +28,80 @@ from denseopticalflowsegmentation3d_amd.abi import default_params  # noqa: E402
 from denseopticalflowsegmentation3d_amd.bands import IntraFrame, band_bounds  # noqa: E402
 
 
+def model(a):
+    """Projected N-GPU time of the row-band path from single-GPU measurements of its parts."""
+    from denseopticalflowsegmentation3d_amd.bands import add_cut_edges, blur_radius, halo_bounds
+    H, W, n = a.height, a.width, a.model
+    ctx = runtime.Dofs(0)
+    persp, inv, up = runtime.calib()
+    prm = default_params()
+    sh = torch.cuda.current_stream().cuda_stream
+    full = torch.empty((1, H, W, 2), dtype=torch.float32, device="cuda")
+    runtime.synth_flow_device(full.data_ptr(), 1, H, W, seed0=0, stream=sh)
+    R = blur_radius(prm)
+    bounds = [band_bounds(H, n, r) for r in range(n)]
+    masks = [torch.zeros((b1 - b0, W), dtype=torch.uint8, device="cuda") for b0, b1 in bounds]
+
+    def timeit(fn, reps):
+        for _ in range(a.warmup):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps
+
+    band_ms = []
+    for (b0, b1), m in zip(bounds, masks):
+        h0, h1 = halo_bounds(H, b0, b1, R)
+        rows = full[0, h0:h1].contiguous()
+        band_ms.append(1e3 * timeit(lambda: ctx.band_msf_device(rows.data_ptr(), h0, h1 - h0, H, W, b0, b1,
+                                                               m.data_ptr(), params=prm, stream=sh), a.steps))
+    allowed = torch.cat(masks)
+    add_cut_edges(allowed, bounds, prm.neighbor == 8)
+    rec = torch.empty(4 + 64 * 88, dtype=torch.uint8, device="cuda")
+
+    def masked():
+        ctx.segment_masked_device(full.data_ptr(), H, W, allowed.data_ptr(), persp, inv, up, params=prm, stream=sh)
+        ctx.records_copy(rec.data_ptr(), 64, stream=sh)
+
+    def one():
+        ctx.segment_batch_device(full.data_ptr(), 1, H, W, persp, inv, up, params=prm, stream=sh)
+        ctx.records_copy(rec.data_ptr(), 64, stream=sh)
+
+    t_masked = 1e3 * timeit(masked, a.steps)
+    t_one = 1e3 * timeit(one, a.steps)
+    ctx.profile(True)
+    masked()
+    torch.cuda.synchronize()
+    ms, nb = ctx.profile_read()
+    ctx.profile(False)
+    per_band = max(b1 - b0 for b0, b1 in bounds)
+    gather_bytes = (n - 1) * per_band * W * (1 + 8)  # edge-bit mask + flow rows of every other band
+    t_gather = 1e3 * gather_bytes / (a.xgmi_gbs * 1e9)
+    t_n = max(band_ms) + t_gather + t_masked
+    print(json.dumps({"config": f"{W}x{H} synthetic, {n} row bands, projected from one GPU",
+                      "band_msf_ms": [round(x, 3) for x in band_ms], "gather_ms_est": round(t_gather, 3),
+                      "gather_bytes": gather_bytes, "xgmi_gbs_assumed": a.xgmi_gbs,
+                      "rank0_masked_ms": round(t_masked, 3),
+                      "rank0_stage_ms": {k: round(v / max(nb, 1), 3) for k, v in ms.items()},
+                      "projected_ms_per_frame": round(t_n, 3), "one_gpu_ms_per_frame": round(t_one, 3),
+                      "projected_speedup": round(t_one / t_n, 3)}), flush=True)
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", type=int, default=0, help="one GPU: project the N-band sharded time (N = value)")
+    ap.add_argument("--xgmi-gbs", type=float, default=64.0, help="assumed gather bandwidth to rank 0 (GB/s)")
     a = ap.parse_args()
+    if a.model:
+        return model(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -37,4 +37,5 @@ names = ["sweep A finds", "sweep B unions", "sweep C roots+hash", "sweep D store
          "LDS worker wait"]
 res = {n: {"total_ms": round(out[i] / 1e3, 2), "us_per_block": round(out[i] / blocks, 2)}
        for i, n in enumerate(names) if n != "-"}
-print(json.dumps({"B": B, "batches": NB, "blocks": blocks, "phases": res}, indent=1))
+hops = {"phase A find rounds (slowest thread) per sweep block": round(out[12] * 100 / max(out[13] * 100, 1), 2)}
+print(json.dumps({"B": B, "batches": NB, "blocks": blocks, "phases": res, "sweep": hops}, indent=1))
