@@ -438,11 +438,23 @@ int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity
     const int64_t fo = (int64_t)frame * d.NL;
     be.d2h(eu.data(), w.EU + (int64_t)frame * d.M, 4 * (size_t)d.M);
     be.d2h(evv.data(), w.EV + (int64_t)frame * d.M, 4 * (size_t)d.M);
-    be.d2h(key.data(), w.key_out + (int64_t)frame * d.M, 8 * (size_t)d.M);
+    const bool keys = cx->pipe(slot).keys_by_frame;
+    std::vector<F2> bl(keys ? 0 : (size_t)d.N);
+    if (keys)
+        be.d2h(key.data(), w.key_out + (int64_t)frame * d.M, 8 * (size_t)d.M);
+    else  // the batch-wide sort left the weights in global order: recompute them from the blurred field
+        be.d2h(bl.data(), w.blur + (int64_t)frame * d.N, sizeof(F2) * (size_t)d.N);
     be.d2h(pre.data(), cx->pipe(slot).pre + fo + d.N, 4 * (size_t)d.M);
     be.d2h(rv.data(), w.Rv + fo, sizeof(RepVal) * (size_t)d.NL);
     be.d2h(sz.data(), w.SZ + fo + d.N, 4 * (size_t)d.M);
     be.sync();
+    if (!keys)
+        for (int64_t i = 0; i < M; ++i) {  // KMstEmit's edge_weight: float differences, double squares
+            const F2 a = bl[(size_t)eu[i]], b = bl[(size_t)evv[i]];
+            const double dx = a.x - b.x, dy = a.y - b.y;
+            const double wt = sqrt(dx * dx + dy * dy);
+            memcpy(&key[i], &wt, sizeof(double));
+        }
     for (int64_t i = 0; i < M; ++i) {
         dofs_event& e = ev[i];
         const int q = pre[i];

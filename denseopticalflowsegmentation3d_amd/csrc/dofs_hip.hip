@@ -2407,49 +2407,9 @@ struct HipBackend {
             launch_on(stream, nf, n, KFrameRebase{out, start, n});
         }
     }
-    // stable LSD radix sort of (key, value) pairs by the 64-bit key, per frame. All frames at once
-    // when the frame id fits above the value bits: sort every pair by key, then stably by frame id
-    // (held in the value's top bits, with the key riding along as the value), then unpack.
-    struct KPackFrame {
-        unsigned* v;
-        int64_t n;
-        int ib;
-        __device__ void operator()(int f, int64_t i) const { v[f * n + i] |= (unsigned)f << ib; }
-    };
-    struct KUnpackFrame {
-        const unsigned* vin;
-        unsigned* vout;
-        const unsigned long long* kin;
-        unsigned long long* kout;
-        int64_t n;
-        unsigned mask;
-        __device__ void operator()(int f, int64_t i) const {
-            const int64_t o = f * n + i;
-            vout[o] = vin[o] & mask;
-            kout[o] = kin[o];
-        }
-    };
+    // stable LSD radix sort of (key, value) pairs by the 64-bit key, per frame (build_graph's edge list)
     void sort_pairs(unsigned long long* kin, unsigned long long* kout, unsigned* vin, unsigned* vout, int64_t n,
-                    int nf, int value_bits) {
-        int fb = 0;
-        while ((1 << fb) < nf) ++fb;
-        const int64_t tot = n * nf;
-        if (nf > 1 && value_bits + fb <= 32 && tot < ((int64_t)1 << 31)) {
-            launch_on(stream, nf, n, KPackFrame{vin, n, value_bits});
-            size_t b1 = 0, b2 = 0;
-            note(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, kin, kout, vin, vout, (int)tot, 0, 64, stream),
-                 "sort size");
-            note(hipcub::DeviceRadixSort::SortPairs(nullptr, b2, vout, vin, kout, kin, (int)tot, value_bits,
-                                                    value_bits + fb, stream),
-                 "sort size");
-            void* t = temp(std::max(b1, b2));
-            note(hipcub::DeviceRadixSort::SortPairs(t, b1, kin, kout, vin, vout, (int)tot, 0, 64, stream), "sort");
-            note(hipcub::DeviceRadixSort::SortPairs(t, b2, vout, vin, kout, kin, (int)tot, value_bits,
-                                                    value_bits + fb, stream),
-                 "sort frames");
-            launch_on(stream, nf, n, KUnpackFrame{vin, vout, kin, kout, n, (1u << value_bits) - 1u});
-            return;
-        }
+                    int nf, int) {
         for (int f = 0; f < nf; ++f) {
             size_t bytes = 0;
             note(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kin + f * n, kout + f * n, vin + f * n, vout + f * n,
@@ -2460,6 +2420,37 @@ struct HipBackend {
                                                     (int)n, 0, 64, stream),
                  "sort");
         }
+    }
+    static int frame_bits(int nf) {
+        int fb = 0;
+        while ((1 << fb) < nf) ++fb;
+        return fb;
+    }
+    // The whole batch's MST edges in one sort when the frame id fits above the value_bits index bits
+    // (KMstEmit then writes it there): pairs by the 64-bit weight key, then the values alone, stably,
+    // by the frame bits — a 4-byte keys-only pass; the weights stay in global key order.
+    static bool mst_packed(int64_t n, int nf, int value_bits) {
+        return nf > 1 && value_bits + frame_bits(nf) <= 32 && n * nf < ((int64_t)1 << 31);
+    }
+    // Kruskal order of each frame's MST edges into w.val_out (values of frame f at [f n, (f + 1) n)).
+    // Packed: w.EU (written later by KEdgeInit) is the scratch between the two passes.
+    void sort_mst(Ws& w, int64_t n, int nf, int value_bits, bool packed) {
+        if (!packed) {
+            sort_pairs(w.key_in, w.key_out, w.val_in, w.val_out, n, nf, value_bits);
+            return;
+        }
+        const int fb = frame_bits(nf);
+        const int tot = (int)(n * nf);
+        unsigned* vmid = reinterpret_cast<unsigned*>(w.EU);
+        size_t b1 = 0, b2 = 0;
+        note(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, w.key_in, w.key_out, w.val_in, vmid, tot, 0, 64, stream),
+             "sort size");
+        note(hipcub::DeviceRadixSort::SortKeys(nullptr, b2, vmid, w.val_out, tot, value_bits, value_bits + fb, stream),
+             "sort size");
+        void* t = temp(std::max(b1, b2));
+        note(hipcub::DeviceRadixSort::SortPairs(t, b1, w.key_in, w.key_out, w.val_in, vmid, tot, 0, 64, stream), "sort");
+        note(hipcub::DeviceRadixSort::SortKeys(t, b2, vmid, w.val_out, tot, value_bits, value_bits + fb, stream),
+             "sort frames");
     }
 };
 

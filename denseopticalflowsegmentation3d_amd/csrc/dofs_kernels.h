@@ -538,6 +538,7 @@ struct KMstCount {
 
 struct KMstEmit {
     Ws w;
+    int fshift;  // > 0: the frame id rides above the emission index (one batch-wide frame sort, HIP)
     DOFS_HD void operator()(int f, int64_t p) const {
         const Dims& d = w.d;
         const int bits = (int)mst_bits(w.mstbits[f * d.N + p]);
@@ -555,7 +556,7 @@ struct KMstEmit {
             if (j < d.M) {
                 const double dx = bp.x - bq[k].x, dy = bp.y - bq[k].y;  // edge_weight(b, p, q)
                 w.key_in[f * d.M + j] = dbits(sqrt(dx * dx + dy * dy));
-                w.val_in[f * d.M + j] = (unsigned)(4 * p + k);
+                w.val_in[f * d.M + j] = (unsigned)(4 * p + k) | (fshift ? (unsigned)f << fshift : 0u);
             }
             ++j;
         }
@@ -566,7 +567,8 @@ struct KMstEmit {
 struct KEdgeInit {  // endpoints by rank; labels = the endpoints (global-kernel KRT only: `labels`)
     Ws w;
     bool labels;
-    bool given = false;  // EU / EV already hold the merges (segment_graph on a caller's edge list)
+    bool given = false;   // EU / EV already hold the merges (segment_graph on a caller's edge list)
+    unsigned vmask = ~0u;  // the emission index bits of val_out (a frame id may sit above them)
     DOFS_HD void operator()(int f, int64_t i) const {
         const Dims& d = w.d;
         const int64_t o = f * d.M + i;
@@ -575,7 +577,7 @@ struct KEdgeInit {  // endpoints by rank; labels = the endpoints (global-kernel 
             p = w.EU[o];
             q = w.EV[o];
         } else {
-            const unsigned idx = w.val_out[o];
+            const unsigned idx = w.val_out[o] & vmask;
             p = idx >> 2;
             q = edge_end(d, p, idx & 3);
             w.EU[o] = (int)p;

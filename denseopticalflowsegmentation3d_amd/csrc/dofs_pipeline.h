@@ -56,8 +56,10 @@ struct Pipeline {
     int64_t snap_cap = 4096;
     bool preorder_in_b = false;
     bool krt_dnc = false;  // DOFS_KRT_DNC=1: block-start labels by the top-down global depths
-    int skip_mask = 0;
-    int long_path = kLongPath;  // measurement only (DOFS_SKIPMASK): 1 short replay, 2 long replay, 4 lift  // pipeline split: K4 at the end of phase A (default) or start of B
+    int skip_mask = 0;          // measurement only (DOFS_SKIPMASK): 1 short replay, 2 long replay, 4 lift
+    bool keys_by_frame = true;  // key_out holds each frame's sorted weights (else: recomputed for events)
+    unsigned vmask = ~0u;       // emission index bits of val_out
+    int long_path = kLongPath;
 
     explicit Pipeline(Backend& b) : be(b) { memset(&w, 0, sizeof(w)); }
     ~Pipeline() {
@@ -244,8 +246,14 @@ struct Pipeline {
         be.mark(2);
         be.launch(B, N, KMstCount{w});
         be.scan_excl(w.cnt, w.off, N, B);
-        be.launch(B, N, KMstEmit{w});
-        be.sort_pairs(w.key_in, w.key_out, w.val_in, w.val_out, M, B, ceil_log2(4 * N));  // Kruskal order
+        // Kruskal order: val_out holds each frame's MST edges by (weight, index); when the backend sorts
+        // the whole batch at once the frame id rides above the index bits and key_out is not per frame
+        const int vb = ceil_log2(4 * N);
+        const bool packed = be.mst_packed(M, B, vb);
+        be.launch(B, N, KMstEmit{w, packed ? vb : 0});
+        be.sort_mst(w, M, B, vb, packed);
+        keys_by_frame = !packed;
+        vmask = vb >= 32 ? ~0u : (1u << vb) - 1u;
         krt(false);
     }
 
@@ -288,6 +296,7 @@ struct Pipeline {
             be.launch(1, E, KElEmit{w, edges, acc, off});
         }
         w.mreal = m;
+        keys_by_frame = true;
         if (m < M) {  // a forest: chain its roots after the caller's merges
             be.launch(1, N, KElRootFlag{w});
             be.scan_excl(w.cnt, w.off, N, 1);
@@ -308,6 +317,7 @@ struct Pipeline {
         be.mark(3);
         KEdgeInit ei{w, krt_dnc};
         ei.given = given;
+        ei.vmask = vmask;
         if (!given || krt_dnc) be.launch(B, M, ei);
         const bool words = krt_dnc || Backend::kKrtLabelWords;  // the global-kernel KRT reads them
         be.launch(B, words ? NL : N, KLabelInit{w, words});

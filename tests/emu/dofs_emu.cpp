@@ -229,6 +229,10 @@ struct HostBackend {
             }
         }
     }
+    static bool mst_packed(int64_t, int, int) { return false; }
+    void sort_mst(Ws& w, int64_t n, int nf, int value_bits, bool) {
+        sort_pairs(w.key_in, w.key_out, w.val_in, w.val_out, n, nf, value_bits);
+    }
     void sort_pairs(const unsigned long long* kin, unsigned long long* kout, const unsigned* vin, unsigned* vout,
                     int64_t n, int nf, int) {
         std::vector<int64_t> ix((size_t)n);

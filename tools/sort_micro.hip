@@ -1,0 +1,110 @@
+// sort_micro.hip — radix-sort configurations for the Kruskal-order sort of the MST edges (stage A):
+// n = 96 frames x (1920*1080 - 1) (u64 weight bits, u32 index) pairs, weight-like keys (30 % exact
+// zeros, the rest sqrt of small uniforms). Times (hipEvents, median of 5):
+//   hip64   hipcub SortPairs over 64 bits (the default onesweep, 8 bits per pass)
+//   ros<R>  rocprim onesweep with R bits per pass over 64 bits
+//   fpair   the frame pass as it was: SortPairs(u32 frame|index -> u64 key) over 7 bits
+//   fkeys   the frame pass keys-only: SortKeys(u32 frame|index) over 7 bits
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <rocprim/rocprim.hpp>
+#include <stdio.h>
+
+#include <algorithm>
+#include <vector>
+
+#define CK(x)                                                                      \
+    do {                                                                           \
+        hipError_t e = (x);                                                        \
+        if (e != hipSuccess) {                                                     \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+            exit(1);                                                               \
+        }                                                                          \
+    } while (0)
+
+__device__ inline unsigned long long mix(unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ void k_fill(unsigned long long* k, unsigned* v, long n, long per, int vb) {
+    const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long h = mix((unsigned long long)i);
+    double w = 0.0;
+    if ((h & 3) != 0) w = sqrt((double)((h >> 11) & 0xFFFFF) * (0.05 / 1048576.0));
+    unsigned long long b;
+    memcpy(&b, &w, 8);
+    k[i] = b;
+    const long f = i / per;
+    v[i] = (unsigned)(i % per) | ((unsigned)f << vb);
+}
+
+template <unsigned R>
+using OsCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                         rocprim::radix_sort_onesweep_config<rocprim::kernel_config<512, 16>,
+                                                                             rocprim::kernel_config<512, 16>, R,
+                                                                             rocprim::block_radix_rank_algorithm::match>>;
+
+int main() {
+    const long per = 1920L * 1080 - 1, F = 96, n = per * F;
+    const int vb = 23;
+    unsigned long long *k0, *k1;
+    unsigned *v0, *v1;
+    CK(hipMalloc(&k0, 8 * n));
+    CK(hipMalloc(&k1, 8 * n));
+    CK(hipMalloc(&v0, 4 * n));
+    CK(hipMalloc(&v1, 4 * n));
+    void* tmp = nullptr;
+    size_t tb = 0;
+    auto need = [&](size_t b) {
+        if (b > tb) {
+            if (tmp) CK(hipFree(tmp));
+            CK(hipMalloc(&tmp, b));
+            tb = b;
+        }
+    };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto timeit = [&](const char* name, auto&& fn) {
+        std::vector<float> t;
+        for (int it = 0; it < 6; ++it) {
+            k_fill<<<(unsigned)((n + 255) / 256), 256>>>(k0, v0, n, per, vb);
+            CK(hipEventRecord(e0));
+            fn();
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (it) t.push_back(ms);
+        }
+        std::sort(t.begin(), t.end());
+        printf("{\"sort\": \"%s\", \"n\": %ld, \"ms_median\": %.3f, \"ms_min\": %.3f}\n", name, n, t[t.size() / 2], t[0]);
+        fflush(stdout);
+    };
+    size_t b = 0;
+    CK(hipcub::DeviceRadixSort::SortPairs(nullptr, b, k0, k1, v0, v1, (int)n, 0, 64));
+    need(b);
+    timeit("hip64", [&] { CK(hipcub::DeviceRadixSort::SortPairs(tmp, b, k0, k1, v0, v1, (int)n, 0, 64)); });
+#define ROS(R)                                                                                               \
+    {                                                                                                        \
+        size_t bb = 0;                                                                                       \
+        CK(rocprim::radix_sort_pairs<OsCfg<R>>(nullptr, bb, k0, k1, v0, v1, (size_t)n, 0, 64));              \
+        need(bb);                                                                                            \
+        timeit("ros" #R, [&] { CK(rocprim::radix_sort_pairs<OsCfg<R>>(tmp, bb, k0, k1, v0, v1, (size_t)n, 0, 64)); }); \
+    }
+    ROS(8)
+    ROS(10)
+    ROS(9)
+    b = 0;
+    CK(hipcub::DeviceRadixSort::SortPairs(nullptr, b, v0, v1, k0, k1, (int)n, vb, vb + 7));
+    need(b);
+    timeit("fpair", [&] { CK(hipcub::DeviceRadixSort::SortPairs(tmp, b, v0, v1, k0, k1, (int)n, vb, vb + 7)); });
+    b = 0;
+    CK(hipcub::DeviceRadixSort::SortKeys(nullptr, b, v0, v1, (int)n, vb, vb + 7));
+    need(b);
+    timeit("fkeys", [&] { CK(hipcub::DeviceRadixSort::SortKeys(tmp, b, v0, v1, (int)n, vb, vb + 7)); });
+    return 0;
+}
