@@ -38,18 +38,22 @@ ROUND_FLAG = 16        # counters: C_ACT + r = Borůvka round r found a cross-co
 C_LONGM = 57           # counters: merges on long heavy paths
 
 # Algorithmic (compulsory) bytes of the probed kernels, per unit:
-#   k_boruvka_min — unit: a pixel of a tile the launch processes (tiles found done are skipped;
-#     dofs_batch_tile_pixels says which): pass 0 reads its component label (4 B) and blurred flow (8 B)
-#     and writes its kept incident-minimum candidate (weight 8 B + index 4 B) = 24 B; pass 1 reads its
-#     label and kept candidate = 16 B. Neighbours' words are other pixels' own reads.
+#   k_boruvka_min4 — Borůvka pass 0 (frames of width % 4 == 0). Units: a pixel of a tile the launch
+#     processes (tiles found done are skipped; dofs_batch_tile_pixels says which) reads its component
+#     label (4 B) and blurred flow (8 B) = 12 B; a (tile, component) record it writes (weight 8 B,
+#     index 4 B, component 4 B) = 16 B (dofs_batch_records). Neighbours' words are other pixels' reads.
+#   k_boruvka_pick4 — pass 1: a record read (16 B); the component minimum it compares with is a
+#     cached gather, not counted.
+#   k_boruvka_min — the pixel-candidate form (other widths): pass 0 24 B, pass 1 16 B per pixel.
 #   k_krt_fused — unit: a merge: its endpoints in (8 B), its node size out (4 B), two child seed words
 #     of the preorder's pointer jumping out (16 B), heavy/light and path-top flags out (3 B), and one
 #     16-B union-find record of the sweep read = 47 B.
 #   k_replay_long — unit: a merge on a long heavy path: its step inputs (StepIn, 32 B) in and its
 #     replay record (RepVal, 32 B) out = 64 B (a light merge child's 32-B record read is not counted).
-BYTES = {"k_boruvka_min": (24, 16), "k_krt_fused": 47, "k_replay_long": 64}
-PROBES = ("k_boruvka_min", "k_krt_fused", "k_replay_long")
-ROOF_KERNEL = "k_boruvka_min"
+BYTES = {"k_boruvka_min4": (12, 16), "k_boruvka_pick4": 16, "k_boruvka_min": (24, 16), "k_krt_fused": 47,
+         "k_replay_long": 64}
+PROBES = ("k_boruvka_min4", "k_boruvka_pick4", "k_krt_fused", "k_replay_long")
+ROOF_KERNEL = "k_boruvka_min4"
 
 
 def ceil_log2(n):
@@ -323,6 +327,7 @@ def main(argv=None):
     # (every batch of the bench is the same workload shape)
     counters = ctx.batch_counters(chunks[-1][1])
     tiles = ctx.tile_pixels(chunks[-1][1])
+    recs = ctx.records(chunks[-1][1])
     pmc = {}
     if a.pmc and os.path.exists(a.pmc):
         pj = json.load(open(a.pmc))
@@ -337,7 +342,18 @@ def main(argv=None):
                  "avg_launch_us": round(ms / launches * 1e3, 2),
                  "share_of_step": round(ms / a.steps / (elapsed * 1e3 / a.steps), 4)}
         alg = None
-        if name == "k_boruvka_min" and len(chunks) == 1:
+        if name == "k_boruvka_min4" and len(chunks) == 1:
+            p0, _, _ = boruvka_min_units(tiles, counters, N)
+            nrec = int(recs.sum())
+            alg = (p0 * BYTES[name][0] + nrec * BYTES[name][1]) * batches
+            entry["alg_bytes_per_unit"] = "12 per pixel of a processed tile + 16 per record written"
+            entry["units_per_batch"] = {"pass0_px": p0, "records": nrec}
+        elif name == "k_boruvka_pick4" and len(chunks) == 1:
+            nrec = int(recs.sum())
+            alg = nrec * BYTES[name] * batches
+            entry["alg_bytes_per_unit"] = "16 per record read"
+            entry["units_per_batch"] = {"records": nrec}
+        elif name == "k_boruvka_min" and len(chunks) == 1:
             p0, p1, lpb = boruvka_min_units(tiles, counters, N)
             assert launches == lpb * batches, (launches, lpb, batches)
             alg = (p0 * BYTES[name][0] + p1 * BYTES[name][1]) * batches

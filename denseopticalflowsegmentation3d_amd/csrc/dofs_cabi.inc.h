@@ -199,6 +199,18 @@ int32_t dofs_batch_tile_pixels(dofs_ctx* ctx, int32_t* out, int64_t capacity) {
     return ctx->check();
 }
 
+int32_t dofs_batch_records(dofs_ctx* ctx, int32_t* out, int64_t capacity) {
+    if (!ctx || !out || !ctx->have_batch()) return DOFS_ERR_INVALID_ARG;
+    const int slot = ctx->last_slot();
+    const int64_t n = (int64_t)ctx->meta[slot].B * dofs::kRoundsMax;
+    if (capacity < n) return DOFS_ERR_CAPACITY;
+    ctx->be.use_own();
+    ctx->join(ctx->nbatch - 1);
+    ctx->be.d2h(out, ctx->pipe(slot).w.trec, sizeof(int32_t) * (size_t)n);
+    ctx->be.sync();
+    return ctx->check();
+}
+
 int32_t dofs_lift(dofs_ctx* ctx, const float dir[2], const int32_t box[4], const float mat[9], const float inv[9],
                   const float inv_upper[9], int32_t cls, dofs_solution* out) {
     if (!ctx || cls < 0 || cls > 2 || !inv_upper) return DOFS_ERR_INVALID_ARG;

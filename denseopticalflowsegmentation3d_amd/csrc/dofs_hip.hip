@@ -758,6 +758,8 @@ constexpr int kDeepHT = kDeepK + kDeepK / 2;    // hash slots (load factor <= 2/
 constexpr int kDeepT = kDeepS >= 2048 ? 1024 : 512;  // threads per block
 static_assert(kDeepL < 32768 && kDeepHT < 32768, "local ids are int16");
 
+// LDS operations of one wave complete in order: waiting for them makes them visible to its other lanes
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ inline int lds_ld(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ inline void lds_st(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ inline int lds_find(int* P, int x) {
@@ -873,6 +875,16 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
     }
     __syncthreads();
     KT_DECL
+    // a sub-block of S <= 64 merges lies in one wave (thread tid handles merges tid and tid + kDeepT,
+    // 64 consecutive merges per wave) and its labels are no other sub-block's (a component current at
+    // the sub-block's start was not merged by an earlier sub-block of the depth), so those depths
+    // synchronise the wave only
+    auto depth_sync = [&](int S) {
+        if (S > 64)
+            __syncthreads();
+        else
+            lds_wait();
+    };
     for (int S = kDeepS; S >= 2; S >>= 1) {
         const int half = S >> 1;
         // union (L edges of sub-blocks whose R half exists)
@@ -880,7 +892,7 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
             const bool isL = (t & (S - 1)) < half && s0 + (t & ~(S - 1)) + half < d.M;
             if (isL) sh.own[t] = (short)lds_union(sh.P, sh.SZ, sh.lu[t], sh.lv[t]);
         }
-        __syncthreads();
+        depth_sync(S);
         for (int t = tid; t < cnt; t += kDeepT) {  // compress + aggregate
             const bool isL = (t & (S - 1)) < half && s0 + (t & ~(S - 1)) + half < d.M;
             if (!isL) continue;
@@ -895,7 +907,7 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
             atomicAdd(sh.CS + r, sh.SZ[h]);
             atomicMax(sh.MX + r, t);
         }
-        __syncthreads();
+        depth_sync(S);
         // L-roots: sizes of the new components; R edges: relabel (both only read P, MX, CS)
         for (int t = tid; t < cnt; t += kDeepT) {
             if ((t & (S - 1)) < half) {
@@ -918,7 +930,7 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
                 }
             }
         }
-        __syncthreads();
+        depth_sync(S);
         for (int t = tid; t < cnt; t += kDeepT) {  // cleanup
             const bool isL = (t & (S - 1)) < half && s0 + (t & ~(S - 1)) + half < d.M;
             if (!isL) continue;
@@ -929,7 +941,7 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
                 sh.CS[r] = 0;
             }
         }
-        __syncthreads();
+        depth_sync(S);
         KT(S >= 256 ? 9 : 10);  // the upper depths (S >= 256) and the lower ones
     }
     // final labels (the edge's KRT children) as global ids: a local id below kDeepK was never
@@ -1341,6 +1353,297 @@ __global__ __launch_bounds__(256) void k_tile_hist(Ws w, const unsigned char* td
     __syncthreads();
     for (int k = threadIdx.x; k < kRoundsMax; k += blockDim.x)
         if (bins[k]) atomicAdd(w.tpx + (int64_t)f * kRoundsMax + k, bins[k]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2 Borůvka rounds >= 1 on frames of width % 4 == 0 without an edge mask (the hot path; other
+// frames use k_boruvka_min): one wave per 32x8 tile, four pixels per lane (lane row = lane / 8,
+// pixels 4 (lane % 8) .. + 3), no workgroup barrier.
+//   k_boruvka_min4 (pass 0): each lane loads its three rows' labels as one 16-B load and flows as
+//     two 16-B loads (+ the two halo columns), every pixel takes its lexicographic minimum over its
+//     cross-component incident edges, and the wave reduces them per component in a wave-private
+//     LDS hash to one (weight, index) record per (tile, component): the weight goes to the
+//     component's global minimum, the record to the tile's k-th pixel slot of three pixel-strided
+//     arrays. A tile with no record is done for good (as in k_boruvka_min).
+//   k_boruvka_pick4 (pass 1): per record, the index goes to its component's minimum if its weight
+//     is the component's minimum weight — records, not pixels.
+//   k_boruvka_hookr: the record equal to its component's (weight, index) minimum hooks the component
+//     along its edge and clears the minima (one winner per component: a cross edge has exactly one
+//     end in it, so no two records of a component share an edge) — records, not a scan for roots.
+// ---------------------------------------------------------------------------------------------
+constexpr int kRecHT = 256;  // >= pixels of a tile, so the probing always finds a slot
+struct RecHash {
+    unsigned long long w[kRecHT];
+    int k[kRecHT];
+    unsigned i[kRecHT];
+};
+__device__ __forceinline__ int rec_slot(RecHash& h, int key) {
+    int s = (int)(uf_prio(key) & (kRecHT - 1));
+    for (;;) {
+        int old = -1;
+        __hip_atomic_compare_exchange_strong(h.k + s, &old, key, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (old == -1 || old == key) return s;
+        s = (s + 1) & (kRecHT - 1);
+    }
+}
+// pixel of tile t's record slot k (k < the tile's in-frame pixels, which bound its components)
+__device__ __forceinline__ int64_t rec_px(const Dims& d, int tiles_x, int t, int k) {
+    const int x0 = (t % tiles_x) * kTileX, y0 = (t / tiles_x) * kTileY;
+    const int tw = min(kTileX, d.W - x0);
+    return (int64_t)(y0 + k / tw) * d.W + x0 + k % tw;
+}
+struct RecBufs {  // the records: pixel-strided arrays free during the MST
+    unsigned long long* rw;  // weight bits (the row-blur temporary)
+    unsigned* ri;            // edge index (the MST count words)
+    int* rk;                 // component (the MST emission offsets)
+    unsigned char* td;       // per frame and tile: round that found it done (0: active)
+    unsigned short* tc;      // per frame and tile: records of the last pass 0
+};
+__device__ __forceinline__ bool lexless(unsigned long long wa, unsigned ia, unsigned long long wb, unsigned ib) {
+    return wa < wb || (wa == wb && ia < ib);
+}
+__global__ __launch_bounds__(256) void k_boruvka_min4(Ws w, int r, RecBufs rb) {
+    __shared__ RecHash sh[4];
+    const Dims& d = w.d;
+    const int f = blockIdx.y;
+    if (r > 0 && !w.C(f)[C_ACT + r - 1]) return;
+    const int lane = __lane_id(), wv = threadIdx.x >> 6;
+    RecHash& H = sh[wv];
+    for (int k = lane; k < kRecHT; k += 64) {
+        H.k[k] = -1;
+        H.w[k] = ~0ull;
+        H.i[k] = kNoEdge;
+    }
+    lds_wait();
+    const int tiles_x = (d.W + kTileX - 1) / kTileX;
+    const int tiles = tiles_x * ((d.H + kTileY - 1) / kTileY);
+    const int* comp = w.comp + f * d.N;
+    const F2* b = w.blur + f * d.N;
+    unsigned long long* bw = w.bw + f * d.N;
+    unsigned long long* rw = rb.rw + f * d.N;
+    unsigned* ri = rb.ri + f * d.N;
+    int* rk = rb.rk + f * d.N;
+    unsigned char* td = rb.td + (int64_t)f * tiles;
+    unsigned short* tc = rb.tc + (int64_t)f * tiles;
+    const int W = d.W, Hh = d.H;
+    int nrec = 0;
+    for (int t = blockIdx.x * 4 + wv; t < tiles; t += gridDim.x * 4) {
+        if (td[t]) continue;  // wave-uniform
+        const int x0 = (t % tiles_x) * kTileX + (lane & 7) * 4, y = (t / tiles_x) * kTileY + (lane >> 3);
+        const bool valid = x0 < W && y < Hh;  // W % 4 == 0: the lane's four pixels are all in or all out
+        const int yc = min(y, Hh - 1), xc = min(x0, W - 4);
+        const int ry[3] = {max(yc - 1, 0), yc, min(yc + 1, Hh - 1)};
+        const int xl = max(xc - 1, 0), xr = min(xc + 4, W - 1);
+        // column j + 1 of the lane's row data holds pixel column xc + j (j = -1 .. 4)
+        int C[3][6];
+        F2 Fl[3][6];
+#pragma unroll
+        for (int R = 0; R < 3; ++R) {
+            const int64_t o = (int64_t)ry[R] * W;
+            const int4 c4 = *reinterpret_cast<const int4*>(comp + o + xc);
+            const float4 fa = *reinterpret_cast<const float4*>(b + o + xc);
+            const float4 fb = *reinterpret_cast<const float4*>(b + o + xc + 2);
+            C[R][0] = comp[o + xl];
+            C[R][1] = c4.x;
+            C[R][2] = c4.y;
+            C[R][3] = c4.z;
+            C[R][4] = c4.w;
+            C[R][5] = comp[o + xr];
+            Fl[R][0] = b[o + xl];
+            Fl[R][1] = F2{fa.x, fa.y};
+            Fl[R][2] = F2{fa.z, fa.w};
+            Fl[R][3] = F2{fb.x, fb.y};
+            Fl[R][4] = F2{fb.z, fb.w};
+            Fl[R][5] = b[o + xr];
+        }
+        // each pixel's lexicographic minimum (weight, index) over its cross-component incident edges
+        bool has[4];
+        int cp[4];
+        unsigned long long mw[4];
+        unsigned mi[4];
+        const bool yu = y > 0, yd = y + 1 < Hh;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int x = xc + i;
+            const int64_t p = (int64_t)y * W + x;
+            const bool xlo = x > 0, xhi = x + 1 < W;
+            const bool ok[8] = {xlo, yu, d.nbr8 && xlo && yu, d.nbr8 && xlo && yd,
+                                xhi, yd, d.nbr8 && xhi && yd, d.nbr8 && xhi && yu};
+            const int cq[8] = {C[1][i], C[0][i + 1], C[0][i], C[2][i], C[1][i + 2], C[2][i + 1], C[2][i + 2], C[0][i + 2]};
+            const F2 fq[8] = {Fl[1][i], Fl[0][i + 1], Fl[0][i], Fl[2][i], Fl[1][i + 2], Fl[2][i + 1], Fl[2][i + 2], Fl[0][i + 2]};
+            const int64_t nb[8] = {p - 1, p - W, p - W - 1, p + W - 1, p + 1, p + W, p + W + 1, p - W + 1};
+            const int c0 = C[1][i + 1];
+            const F2 f0 = Fl[1][i + 1];
+            // edge_weight(b, s, e) = sqrt(sq) with s the emitting pixel (float differences, double
+            // squares): sqrt is monotone and correctly rounded, so the minimum weight is sqrt of the
+            // minimum sq, and an edge can tie with it only if its sq lies within 2^-48 (relative) of
+            // the minimum — only those take a sqrt (the rounding interval of a weight is 2^-52 wide)
+            unsigned long long sqb[8];
+            unsigned long long msq = ~0ull;  // bits of non-negative doubles order like the values
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const F2 bs = j < 4 ? f0 : fq[j], be = j < 4 ? fq[j] : f0;
+                const double dx = bs.x - be.x, dy = bs.y - be.y;
+                sqb[j] = (ok[j] && cq[j] != c0) ? dbits(dx * dx + dy * dy) : ~0ull;
+                msq = sqb[j] < msq ? sqb[j] : msq;
+            }
+            unsigned long long best = ~0ull;
+            unsigned bidx = kNoEdge;
+            if (msq != ~0ull) {
+                double mv;
+                memcpy(&mv, &msq, 8);
+                best = dbits(sqrt(mv));
+                const unsigned long long thr = dbits(mv * 1.0000000000000036);  // (1 + 2^-48) mv
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if (sqb[j] > thr) continue;  // also the non-candidates (~0)
+                    bool tie = sqb[j] == msq;
+                    if (!tie) {
+                        double v;
+                        memcpy(&v, &sqb[j], 8);
+                        tie = dbits(sqrt(v)) == best;
+                    }
+                    const unsigned idx = (unsigned)(4 * (j < 4 ? p : nb[j]) + (j & 3));
+                    if (tie && idx < bidx) bidx = idx;
+                }
+            }
+            has[i] = valid && bidx != kNoEdge;
+            cp[i] = c0;
+            mw[i] = best;
+            mi[i] = bidx;
+        }
+        // a lane's pixels mostly share their component: fold equal ones into the first
+#pragma unroll
+        for (int i = 1; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < i; ++j)
+                if (has[i] && has[j] && cp[i] == cp[j]) {
+                    if (lexless(mw[i], mi[i], mw[j], mi[j])) {
+                        mw[j] = mw[i];
+                        mi[j] = mi[i];
+                    }
+                    has[i] = false;
+                }
+        const bool lany = has[0] || has[1] || has[2] || has[3];
+        const unsigned long long on = __ballot(lany);
+        if (on) {  // wave-uniform
+            // the first such lane's first component, reduced across the wave by shuffles; the rest
+            // through the wave's LDS hash (weight minimum, then the index among the equal weights)
+            const int leader = __ffsll((long long)on) - 1;
+            const int mycf = has[0] ? cp[0] : has[1] ? cp[1] : has[2] ? cp[2] : cp[3];
+            const int cl = __shfl(mycf, leader, 64);
+            unsigned long long lw = ~0ull;
+            unsigned li = kNoEdge;
+            int slot[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                slot[i] = -1;
+                if (!has[i]) continue;
+                if (cp[i] == cl) {
+                    lw = mw[i];  // at most one pixel entry of the lane per component after the fold
+                    li = mi[i];
+                } else {
+                    slot[i] = rec_slot(H, cp[i]);
+                    atomicMin(H.w + slot[i], mw[i]);
+                }
+            }
+            unsigned long long m = lw;
+            for (int o = 32; o >= 1; o >>= 1) {
+                const unsigned long long v = __shfl_xor(m, o, 64);
+                m = v < m ? v : m;
+            }
+            unsigned mi2 = lw == m ? li : kNoEdge;
+            for (int o = 32; o >= 1; o >>= 1) {
+                const unsigned v = __shfl_xor(mi2, o, 64);
+                mi2 = v < mi2 ? v : mi2;
+            }
+            int sl = -1;
+            if (lane == leader) {
+                sl = rec_slot(H, cl);
+                atomicMin(H.w + sl, m);
+            }
+            lds_wait();
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (slot[i] >= 0 && H.w[slot[i]] == mw[i]) atomicMin(H.i + slot[i], mi[i]);
+            if (sl >= 0 && H.w[sl] == m) atomicMin(H.i + sl, mi2);
+            lds_wait();
+        }
+        // flush: per occupied slot the component's global minimum weight and the tile's record
+        int cnt = 0;
+#pragma unroll
+        for (int s = 0; s < kRecHT / 64; ++s) {
+            const int k = lane + 64 * s;
+            const int key = H.k[k];
+            const bool occ = key >= 0;
+            const unsigned long long ob = __ballot(occ);
+            if (occ) {
+                const int pos = cnt + __popcll(ob & ((1ull << lane) - 1));
+                const unsigned long long hw = H.w[k];
+                const unsigned hi = H.i[k];
+                atomicMin(bw + key, hw);  // no return value: no wait
+                const int64_t px = rec_px(d, tiles_x, t, pos);
+                rw[px] = hw;
+                ri[px] = hi;
+                rk[px] = key;
+                H.k[k] = -1;
+                H.w[k] = ~0ull;
+                H.i[k] = kNoEdge;
+            }
+            cnt += __popcll(ob);
+        }
+        lds_wait();
+        if (lane == 0) {
+            tc[t] = (unsigned short)cnt;
+            if (!cnt) td[t] = (unsigned char)r;  // r >= 1: the last round that processed the tile
+        }
+        nrec += cnt;
+    }
+    if (lane == 0 && nrec) {
+        w.C(f)[C_ACT + r] = 1;
+        atomicAdd(w.trec + (int64_t)f * kRoundsMax + r, nrec);
+    }
+}
+// pass 1 / hook over a frame's records (one wave per tile, lanes over its records)
+template <bool kHook>
+__global__ __launch_bounds__(256) void k_boruvka_recs(Ws w, int r, RecBufs rb) {
+    const Dims& d = w.d;
+    const int f = blockIdx.y;
+    if (!w.C(f)[C_ACT + r]) return;
+    const int lane = __lane_id(), wv = threadIdx.x >> 6;
+    const int tiles_x = (d.W + kTileX - 1) / kTileX;
+    const int tiles = tiles_x * ((d.H + kTileY - 1) / kTileY);
+    unsigned long long* bw = w.bw + f * d.N;
+    unsigned* bi = w.bi + f * d.N;
+    const unsigned long long* rw = rb.rw + f * d.N;
+    const unsigned* ri = rb.ri + f * d.N;
+    const int* rk = rb.rk + f * d.N;
+    const unsigned char* td = rb.td + (int64_t)f * tiles;
+    const unsigned short* tc = rb.tc + (int64_t)f * tiles;
+    for (int t = blockIdx.x * 4 + wv; t < tiles; t += gridDim.x * 4) {
+        if (td[t]) continue;
+        const int cnt = tc[t];
+        for (int k = lane; k < cnt; k += 64) {
+            const int64_t px = rec_px(d, tiles_x, t, k);
+            const int key = rk[px];
+            const unsigned long long wb = rw[px];
+            const unsigned ix = ri[px];
+            if (wb != bw[key]) continue;
+            if (!kHook) {
+                if (ix < bi[key]) atomicMin(bi + key, ix);
+            } else if (ix == bi[key]) {  // the component's minimum edge: hook along it (boruvka_hook_root)
+                bw[key] = ~0ull;
+                bi[key] = kNoEdge;
+                const int64_t p = ix >> 2;
+                const int e = ix & 3;
+                const int64_t q = edge_end(d, p, e);
+                reinterpret_cast<unsigned char*>(w.mstbits + f * d.N + p)[e] = 1;
+                const int* comp = w.comp + f * d.N;
+                uf_union(w.uf + f * d.N, comp[p], comp[q]);
+            }
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1771,6 +2074,18 @@ __global__ __launch_bounds__(256) void k_boruvka_hook4(Ws w, int r) {
         if (comp[c] == (int)c) boruvka_hook_root(w, f, c);
     }
 }
+// uf_find with plain (L1-cacheable) loads: no union runs during a relabel, so a root's word is final
+// and any word read — stale or not — points to an ancestor; path halving stores stay as they are
+__device__ __forceinline__ int uf_find_ro_halve(int* P, int x) {
+    for (;;) {
+        const int p = P[x];
+        if (p == x) return x;
+        const int gp = P[p];
+        if (gp == p) return p;
+        P[x] = gp;
+        x = gp;
+    }
+}
 __global__ __launch_bounds__(256) void k_boruvka_relabel4(Ws w, int r) {
     const int f = blockIdx.y;
     if (!w.C(f)[C_ACT + r]) return;
@@ -1784,16 +2099,16 @@ __global__ __launch_bounds__(256) void k_boruvka_relabel4(Ws w, int r) {
         int4* p4 = reinterpret_cast<int4*>(comp + sp.head + 4 * i);
         const int4 v = *p4;
         int4 o;
-        o.x = uf_find(uf, v.x);
-        o.y = v.y == v.x ? o.x : uf_find(uf, v.y);
-        o.z = v.z == v.y ? o.y : uf_find(uf, v.z);
-        o.w = v.w == v.z ? o.z : uf_find(uf, v.w);
+        o.x = uf_find_ro_halve(uf, v.x);
+        o.y = v.y == v.x ? o.x : uf_find_ro_halve(uf, v.y);
+        o.z = v.z == v.y ? o.y : uf_find_ro_halve(uf, v.z);
+        o.w = v.w == v.z ? o.z : uf_find_ro_halve(uf, v.w);
         if (o.x != v.x || o.y != v.y || o.z != v.z || o.w != v.w) *p4 = o;
     }
     if (i0 < sp.head + (N - sp.tail)) {
         const int64_t p = i0 < sp.head ? i0 : sp.tail + (i0 - sp.head);
         const int c = comp[p];
-        const int root = uf_find(uf, c);
+        const int root = uf_find_ro_halve(uf, c);
         if (root != c) comp[p] = root;
     }
 }
@@ -2279,7 +2594,13 @@ struct HipBackend {
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_dnc_deep launch");
     }
-    void boruvka_hook(const Ws& w, int r) { pixel4(w, r, k_boruvka_hook4, "KBoruvkaHook"); }
+    void boruvka_hook(const Ws& w, int r) {
+        if (rec_path(w)) {
+            rec_launch(w, r, k_boruvka_recs<true>, "k_boruvka_hookr");
+            return;
+        }
+        pixel4(w, r, k_boruvka_hook4, "KBoruvkaHook");
+    }
     void boruvka_relabel(const Ws& w, int r) { pixel4(w, r, k_boruvka_relabel4, "KBoruvkaRelabelFind"); }
     void pixel4(const Ws& w, int r, void (*k)(Ws, int), const char* name) {
         const int64_t n4 = (w.d.N + 3) / 4;
@@ -2290,12 +2611,48 @@ struct HipBackend {
         timed(name, [&] { hipLaunchKernelGGL(k, dim3((unsigned)gx, (unsigned)w.d.B), dim3(256), 0, stream, w, r); });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, name);
     }
+    static int64_t tile_count(const Dims& d) {
+        return (int64_t)((d.W + kTileX - 1) / kTileX) * ((d.H + kTileY - 1) / kTileY);
+    }
+    // the record-based rounds (k_boruvka_min4, ...): 16-byte label loads need W % 4 == 0; the tile
+    // counts (u16) sit after the tile flags in the heavy/light bytes, which hold 3 bytes per tile
+    static bool rec_path(const Ws& w) {
+        static const bool off = [] {
+            const char* e = getenv("DOFS_BORUVKA_REC");
+            return e && atoi(e) == 0;
+        }();
+        return !off && !w.allow && w.d.W % 4 == 0 && w.d.N >= 1024 && 3 * tile_count(w.d) + 2 <= w.d.M;
+    }
+    RecBufs rec_bufs(const Ws& w) {
+        const int64_t tiles = tile_count(w.d);
+        RecBufs rb;
+        rb.rw = reinterpret_cast<unsigned long long*>(w.tmp);  // dead after the blur
+        rb.ri = reinterpret_cast<unsigned*>(w.cnt);            // written only after the MST
+        rb.rk = w.off;                                         // written only after the MST
+        rb.td = w.hlB;                                         // filled by KDncParent after the KRT
+        rb.tc = reinterpret_cast<unsigned short*>(w.hlB + ((tiles * w.d.B + 1) & ~(int64_t)1));
+        return rb;
+    }
+    void rec_launch(const Ws& w, int r, void (*k)(Ws, int, RecBufs), const char* name) {
+        const int64_t gx = std::min<int64_t>((tile_count(w.d) + 3) / 4, std::max<int64_t>(1, grid_cap() / w.d.B));
+        const RecBufs rb = rec_bufs(w);
+        timed(name, [&] { hipLaunchKernelGGL(k, dim3((unsigned)gx, (unsigned)w.d.B), dim3(256), 0, stream, w, r, rb); });
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, name);
+    }
     void boruvka_min(const Ws& w, int r, int pass) {
-        const int64_t tiles = (int64_t)((w.d.W + kTileX - 1) / kTileX) * ((w.d.H + kTileY - 1) / kTileY);
+        const int64_t tiles = tile_count(w.d);
         const int64_t gx = std::min<int64_t>(tiles, std::max<int64_t>(1, grid_cap() / w.d.B));
         unsigned char* tdone = w.hlB;  // free during the MST (KDncParent fills it after the KRT)
         static_assert(sizeof(*w.hlB) == 1, "tile flags are bytes");
-        if (r == 1 && pass == 0) memset(tdone, 0, (size_t)tiles * w.d.B);  // tiles <= M per frame
+        if (r == 1 && pass == 0) {
+            memset(tdone, 0, (size_t)tiles * w.d.B);  // tiles <= M per frame
+            memset(w.trec, 0, sizeof(int) * kRoundsMax * (size_t)w.d.B);
+        }
+        if (rec_path(w)) {
+            rec_launch(w, r, pass == 0 ? k_boruvka_min4 : k_boruvka_recs<false>,
+                       pass == 0 ? "k_boruvka_min4" : "k_boruvka_pick4");
+            return;
+        }
         timed("k_boruvka_min", [&] {
             // kept candidates: the row-blur temporary (8 B per pixel, dead after the blur) and the
             // MST-count words (written only after the MST)

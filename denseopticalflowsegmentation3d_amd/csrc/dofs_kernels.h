@@ -112,6 +112,8 @@ struct Ws {
     int* ctr;
     // pixels of the Borůvka tiles by the round that found them done (stride kRoundsMax; 0: never)
     int* tpx;
+    // records written by round r's k_boruvka_min4 (stride kRoundsMax; HIP record path only)
+    int* trec;
     // parameters
     LiftMats L;
     int min_size;

@@ -155,6 +155,7 @@ struct Pipeline {
         w.recs = (dofs_box_record*)take(sizeof(dofs_box_record) * B * snap_cap);
         w.ctr = (int*)take(4 * B * kCounters);
         w.tpx = (int*)take(4 * B * kRoundsMax);
+        w.trec = (int*)take(4 * B * kRoundsMax);
         w.snap_cap = (int)snap_cap;
         return off + 256;
     }

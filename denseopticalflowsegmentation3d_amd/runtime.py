@@ -98,6 +98,8 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_probe_read_n.restype = C.c_int32
     L.dofs_batch_tile_pixels.argtypes = [C.c_void_p, _ip, C.c_int64]
     L.dofs_batch_tile_pixels.restype = C.c_int32
+    L.dofs_batch_records.argtypes = [C.c_void_p, _ip, C.c_int64]
+    L.dofs_batch_records.restype = C.c_int32
     L.dofs_lift.argtypes = [C.c_void_p, _fp, _ip, _fp, _fp, _fp, C.c_int32, C.POINTER(DofsSolution)]
     L.dofs_lift.restype = C.c_int32
     L.dofs_lift_batch.argtypes = [C.c_void_p, C.c_int32, _fp, _ip, _ip, _fp, _fp, _fp, C.POINTER(DofsSolution)]
@@ -382,6 +384,12 @@ class Dofs:
         """The last batch's Borůvka tile census (B x 40 int32, see include/dofs.h)."""
         out = np.zeros((B, 40), np.int32)
         self._err(self.lib.dofs_batch_tile_pixels(self.ctx, _p(out, C.c_int32), out.size), "dofs_batch_tile_pixels")
+        return out
+
+    def records(self, B: int) -> np.ndarray:
+        """The last batch's Borůvka record census (B x 40 int32, see include/dofs.h)."""
+        out = np.zeros((B, 40), np.int32)
+        self._err(self.lib.dofs_batch_records(self.ctx, _p(out, C.c_int32), out.size), "dofs_batch_records")
         return out
 
     def lift(self, direction, box, mat, inv, inv_upper, cls: int) -> dict:

@@ -277,6 +277,11 @@ int32_t dofs_probe_read_n(dofs_ctx* ctx, int32_t n, double* ms, int64_t* launche
  * pass 0 of rounds 1..m and pass 1 of rounds 1..m-1 (bench.py's roofline unit count). */
 int32_t dofs_batch_tile_pixels(dofs_ctx* ctx, int32_t* out, int64_t capacity);
 
+/* The last batch's Borůvka record census (B x 40 int32): entry [f][r] = (tile, component) records
+ * that round r's k_boruvka_min4 wrote for frame f (0 where the frame took the pixel-candidate kernel
+ * k_boruvka_min). With the tile census it gives the record kernels' roofline units (bench.py). */
+int32_t dofs_batch_records(dofs_ctx* ctx, int32_t* out, int64_t capacity);
+
 /* get_bottom_variants on the GPU (one candidate, or n candidates with per-candidate class). */
 int32_t dofs_lift(dofs_ctx* ctx, const float dir[2], const int32_t box[4], const float mat[9],
                   const float inv[9], const float inv_upper[9], int32_t cls, dofs_solution* out);

@@ -156,7 +156,10 @@ struct HostBackend {
         else
             launch(w.d.B, w.d.N, KBoruvkaMinI{w, r});
     }
-    void boruvka_tiles(const Ws& w) { ::memset(w.tpx, 0, sizeof(int) * kRoundsMax * (size_t)w.d.B); }  // no tiles here
+    void boruvka_tiles(const Ws& w) {  // no tiles or records here
+        ::memset(w.tpx, 0, sizeof(int) * kRoundsMax * (size_t)w.d.B);
+        ::memset(w.trec, 0, sizeof(int) * kRoundsMax * (size_t)w.d.B);
+    }
     void dnc_compress(const Ws& w, int64_t S, int ep) { launch(w.d.B, w.d.M, KDncCompress{w, S, ep}); }
     void replay_long(const Ws& w, int r) {
         launch_counted(w.d.B, w.d.N, KReplay{w, 2 * r + 1, w.list_long, C_LONG, nullptr, 0}, C_LONG);
