@@ -1055,11 +1055,13 @@ struct KJumpLeaf {  // a pixel (leaf) hangs off a merge: one jump once the merge
     }
 };
 
-struct KOrd {
+struct KOrd {  // preorder positions; a leaf (x < N) takes its last jump here (KJumpLeaf's, not stored)
     Ws w;
     DOFS_HD void operator()(int f, int64_t x) const {
         const Dims& d = w.d;
-        const int q = jump_sum(w.J[f * d.NL + x]);
+        const unsigned long long v = w.J[f * d.NL + x];
+        const int a = jump_anc(v);
+        const int q = jump_sum(v) + (x < d.N && a >= 0 ? jump_sum(w.J[f * d.NL + a]) : 0);
         w.pre[f * d.NL + x] = q;
         w.ord[f * d.NL + q] = (int)x;  // leaf ranks: scan of (ord < N)
     }
@@ -1310,7 +1312,9 @@ struct KFilter {  // appends candidates through the backend's list taker (called
     DOFS_HD void operator()(int f, int64_t i, bool valid, T& t) const {
         const Dims& d = w.d;
         bool c = false;
-        if (valid && i < w.mreal) {
+        // the size test first (a coalesced read): most merges are small, and only the others read
+        // their replay record (a random 32-B gather by preorder position)
+        if (valid && i < w.mreal && w.SZ[f * d.NL + d.N + i] >= w.min_size) {
             const NodeVal v = node_val(w, pre, f, d.N + i);
             const int y = v.root / d.W;
             c = v.size >= w.min_size && y >= d.H / 10 && !(vec_norm(v.mx, v.my) < 3 * (y + 1) / (double)d.H);

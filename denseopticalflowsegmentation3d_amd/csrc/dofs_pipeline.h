@@ -352,7 +352,6 @@ struct Pipeline {
         const int64_t chain = std::min<int64_t>(d.M, Backend::jump_chain_bound(d.M));
         for (int64_t span = 1; span < chain; span *= 3) ++launches;
         for (int t = 0; t < launches; ++t) be.launch(B, d.M, KJump{w.J, NL, 2, N});
-        be.launch(B, N, KJumpLeaf{w.J, NL});
         pre = w.pre;
         be.launch(B, NL, KOrd{w});
         be.scan_excl_leaf(w.ord, w.lscan, NL, B, N);
