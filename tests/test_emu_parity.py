@@ -28,3 +28,26 @@ def test_emu_adversarial(emu, calib, kind):
             "ints": np.round(rng.normal(size=(H, W, 2)) * 4) + 2.0}[kind].astype(np.float32)
     o, g, ev = run_both(emu, flow, calib, params(50, 8))
     check_exact(o, g, ev, lift_exact=True)
+
+
+# heavy-path lists: tiny paths (<= kTinyPath merges) are listed from the back of the
+# short-path buffer and the others from its front; fields dominated by tiny paths (all-tie and
+# striped fields at small N) must stay exact and every path must land in exactly one list
+C_PATHS, C_SHORT, C_LONG, C_TINY = 0, 6, 7, 15
+
+
+@pytest.mark.parametrize("kind,H,W", [("zeros", 3, 5), ("zeros", 16, 16), ("stripes", 12, 20),
+                                      ("checker", 9, 11), ("normal", 40, 64)])
+def test_emu_path_lists(emu, calib, kind, H, W):
+    rng = np.random.default_rng(7)
+    yy, xx = np.mgrid[0:H, 0:W]
+    flow = {"zeros": np.zeros((H, W, 2)),
+            "stripes": np.stack([(xx % 3).astype(float), np.zeros((H, W))], -1),
+            "checker": np.stack([((xx + yy) % 2) * 2.0, ((xx // 2 + yy) % 3) * 1.0], -1),
+            "normal": rng.normal(size=(H, W, 2))}[kind].astype(np.float32)
+    o, g, ev = run_both(emu, flow, calib, params(2, 8))
+    check_exact(o, g, ev, lift_exact=True)
+    c = emu.batch_counters(1)[0]
+    assert c[C_TINY] + c[C_SHORT] + c[C_LONG] == c[C_PATHS], c[:16]
+    if H * W > 1:
+        assert c[C_PATHS] > 0
