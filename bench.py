@@ -103,7 +103,7 @@ def parse(argv=None):
     ap.add_argument("--no-stages", action="store_true", help="skip the per-stage event timing pass")
     ap.add_argument("--no-h2d", action="store_true", help="skip the with-H2D (host input) pass")
     ap.add_argument("--probe", default=",".join(PROBES), help="kernels timed with device events (comma list)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02", "pmc_summary.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02", "pmc_kernels.json"),
                     help="PMC summary JSON (tools/pmc_kernels.py via tools/pmc_round.sh) for the roofline traffic")
     ap.add_argument("--cpu-worker", nargs=4, metavar=("OPT", "H", "W", "SEED"), help=argparse.SUPPRESS)
     return ap.parse_args(argv)
@@ -381,7 +381,10 @@ def main(argv=None):
     main_k = next((e for e in kern if e["kernel"] == ROOF_KERNEL and "achieved" in e), None)
     if main_k:
         roof = {"bound": "hbm", "achieved": main_k["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": main_k["frac"], "traffic": main_k.get("traffic"), "kernel": ROOF_KERNEL,
+                "frac": main_k["frac"], "traffic": main_k.get("traffic"),
+                "traffic_source": (os.path.relpath(a.pmc, ROOT) + " (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, "
+                                   "tools/pmc_round.sh)") if main_k.get("traffic") else None,
+                "kernel": ROOF_KERNEL,
                 "launches": main_k["launches"], "avg_launch_us": main_k["avg_launch_us"],
                 "alg_bytes_per_launch": main_k["alg_bytes_per_launch"],
                 "alg_bytes_per_unit": main_k["alg_bytes_per_unit"],

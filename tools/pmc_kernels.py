@@ -23,7 +23,11 @@ import sys
 
 # dominant access pattern of each kernel's reads (see the docstring)
 PATTERN = {
-    "k_boruvka_min": "stream",   # tile label / flow rows (LDS-staged), candidate words per pixel
+    "k_boruvka_min": "stream",   # tile label / flow rows, candidate words per pixel
+    "k_boruvka_min4": "stream",  # tile label / flow rows (16-B loads), records per tile
+    "k_boruvka_recs<false>": "stream",  # records by tile (k_boruvka_pick4)
+    "k_boruvka_recs<true>": "stream",   # records by tile (k_boruvka_hookr)
+    "KOrd": "stream",            # jump words by node; the ord[] scatter is random 4-B stores
     "k_krt_fused": "random",     # union-find records, label / seed stores
     "k_replay_long1": "stream",  # StepIn / RepVal records by preorder position (64-step chunks)
     "KJump": "random",
@@ -41,7 +45,8 @@ def rows(d):
 
 
 def match(name, k):
-    return f"dofs::{k}(" in name or f"dofs::{k}>" in name or f"::{k}(" in name
+    return (f"dofs::{k}(" in name or f"dofs::{k}>" in name or f"::{k}(" in name
+            or (k.endswith(">") and f"dofs::{k}(" in name.replace("void ", "")))
 
 
 def per_dispatch(rs, k):
