@@ -1713,8 +1713,8 @@ __global__ __launch_bounds__(kAggT) void k_dnc_compress(Ws w, int64_t S, int ep)
 // its new label, size and the KRT node size. The frames' sweeps are latency-bound and use one CU
 // each; the rest of the chip runs the other stream's replay stage meanwhile.
 // ---------------------------------------------------------------------------------------------
-constexpr int kSeqT = 1024, kSeqHT = 8192, kSeqB = kDeepTop, kSeqK = kSeqB / kSeqT;
-static_assert(2 * kSeqB <= kSeqHT && kSeqK * kSeqT == kSeqB, "sweep shape");
+constexpr int kSeqT = 1024, kSeqB = kDeepTop, kSeqK = kSeqB / kSeqT;
+static_assert(kSeqK * kSeqT == kSeqB, "sweep shape");
 
 // One workgroup owns a frame's union-find: workgroup-scope accesses (plain loads and stores that
 // may stay in the CU's L1 / the XCD's L2; the kernel boundary publishes them to the next kernels)
@@ -1830,34 +1830,62 @@ __device__ __forceinline__ void rec_find(SeqRec* rec, int (&x)[K], bool (&pend)[
     }
 }
 
-#ifndef DOFS_SEQ_COMPRESS
-#define DOFS_SEQ_COMPRESS 0  // measured: the two endpoint stores cost more than the hops they save
-#endif
-__device__ __forceinline__ constexpr bool seq_compress() { return DOFS_SEQ_COMPRESS != 0; }
-// Per block of kSeqB merges (four barrier-separated phases):
-//   A  endpoint roots at the block start -> labels (lu, lv)
-//   B  the block's unions: one CAS per merge. A root is hooked under the other root by the key
-//      (size at the block start, hash priority), which no write of the block changes, so parents
-//      only ever point to a larger key and a root may be hooked onto a node that was hooked
-//      meanwhile without forming a cycle. Union by size keeps a frame's large components' roots
-//      stable (a pixel joining the largest cluster hangs one hop below its root), so the finds of
-//      later blocks are short; linking by hash priority alone moved the root O(log n) times.
-//   C  each merge's resulting root R, aggregated per R in LDS: max rank in the block, sizes of the
-//      roots hooked into it, R's old size; the endpoints are compressed onto R
-//   D  per R: its new label and size (one 8-byte store) and the KRT node size SZ
+// Per block of kSeqB merges:
+//   A  endpoint roots at the block start -> labels (lu, lv): the only global finds of the block
+//   B  the block-start roots into an LDS hash (the slot is the root's local id; the first inserter
+//      keeps the root's block-start size)
+//   C  the block's unions over slots, in LDS (lock-free, union by (block-start size, slot priority):
+//      the key never changes during the block, so a component's LDS root is its largest root —
+//      union by size keeps a frame's large components' roots stable, and the finds of later blocks
+//      short); then per LDS root the max rank in the block (one LDS atomicMax per merge) and the
+//      component's total size (every other slot adds its block-start size)
+//   D  per slot, one global store: a hooked root's parent (directly its component's root), or at
+//      the component's root its new label and size (8 bytes), plus the KRT node size SZ
+// The global forest only gains the hooks of D, each root one hop below its component's root.
+constexpr int kSeqHT = 12288;  // >= 2 kSeqB distinct roots at load <= 2/3
+static_assert(kSeqHT >= 3 * kSeqB && kSeqHT < 65536 && kSeqB < 32767, "sweep hash shape");
 struct SweepShared {
-    int hk[kSeqHT], hmx[kSeqHT], hsz[kSeqHT], hold[kSeqHT];
+    int key[kSeqHT];  // global root in the slot (-1 empty)
+    int sz[kSeqHT];   // its size at the block start; at an LDS root after C, the component's total
+    int pm[kSeqHT];   // LDS parent slot (low 16 bits); at an LDS root after C, (max rank + 1) << 16
 };
+// finds in the slot forest (path halving; a non-root's high bits stay 0)
+__device__ inline int swp_find(int* pm, int x) {
+    for (;;) {
+        const int p = lds_ld(pm + x) & 0xFFFF;
+        if (p == x) return x;
+        const int gp = lds_ld(pm + p) & 0xFFFF;
+        if (gp == p) return p;
+        lds_st(pm + x, gp);
+        x = gp;
+    }
+}
+__device__ inline void swp_union(int* pm, const int* sz, int a, int b) {
+    for (;;) {
+        a = swp_find(pm, a);
+        b = swp_find(pm, b);
+        if (a == b) return;
+        const int sa = sz[a], sb = sz[b];
+        if (!(sa != sb ? sa < sb : uf_above(a, b))) {
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        int old = a;
+        __hip_atomic_compare_exchange_strong(pm + a, &old, b, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (old == a) return;
+    }
+}
 // The sweep of frame f by one workgroup. progress (optional, stride kCounters per frame): after
 // phase A of block b, the frame's word is set to b + 1 — the block's labels and every label size it refers to are then
 // published (stored write-through, drained, one agent-scope flag store) for k_krt_fused's LDS-KRT
 // workers.
 __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
-    constexpr int K = kSeqK, K2 = 2 * kSeqK, KS = kSeqHT / kSeqT;
-    int* hk = sh.hk;
-    int* hmx = sh.hmx;
-    int* hsz = sh.hsz;
-    int* hold = sh.hold;
+    constexpr int K = kSeqK, K2 = 2 * kSeqK;
+    int* key = sh.key;
+    int* hsz = sh.sz;
+    int* pm = sh.pm;
     const Dims& d = w.d;
     const int tid = threadIdx.x;
     SeqRec* rec = reinterpret_cast<SeqRec*>(w.In + f * d.NL);
@@ -1866,11 +1894,7 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
     int* lu = w.lu + f * d.M;
     int* lv = w.lv + f * d.M;
     int* SZ = w.SZ + f * d.NL + d.N;
-    for (int x = tid; x < kSeqHT; x += kSeqT) {
-        hk[x] = -1;
-        hmx[x] = -1;
-        hsz[x] = 0;
-    }
+    for (int x = tid; x < kSeqHT; x += kSeqT) key[x] = -1;
     __syncthreads();
     KT_DECL
     for (int64_t s = 0; s < d.M; s += kSeqB) {
@@ -1895,14 +1919,13 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
         {  // the slowest thread's find rounds (two dependent loads each) in phase A
             int rounds = 0;
             rec_find<K2>(rec, c, pend, rtl, rts, &rounds);
-            if (tid == 0) hmx[0] = 0;
+            if (tid == 0) pm[0] = 0;
             __syncthreads();
-            atomicMax(hmx, rounds);
+            atomicMax(pm, rounds);
             __syncthreads();
             if (tid == 0) {
-                atomicAdd(&g_kt[12], (unsigned long long)hmx[0]);
+                atomicAdd(&g_kt[12], (unsigned long long)pm[0]);
                 atomicAdd(&g_kt[13], 1ull);
-                hmx[0] = -1;
             }
             __syncthreads();
         }
@@ -1930,103 +1953,66 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
                                __HIP_MEMORY_SCOPE_AGENT);
         KT(0);
         // ---- B
-        int hooked_sz[K];
-        {
-            int x[K2];
-            bool pu[K2], todo[K];
+        int sl[K2];
 #pragma unroll
-            for (int k = 0; k < K2; ++k) {
-                x[k] = c[k];
-                pu[k] = false;
-            }
-            int r2l[K2], r2s[K2];
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                todo[k] = act2[2 * k];
-                hooked_sz[k] = 0;
-                r2s[2 * k] = rts[2 * k];
-                r2s[2 * k + 1] = rts[2 * k + 1];
-            }
+        for (int k = 0; k < K2; ++k) {
+            sl[k] = 0;
+            if (!act2[k]) continue;
+            int h = (int)(uf_prio(c[k]) % (unsigned)kSeqHT);
             for (;;) {
-                bool any = false;
-#pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    if (!todo[k]) continue;
-                    // union by size at the block start (roots' sizes change only in phase D, so the
-                    // key (size, hash priority) is static during the block), ties by hash priority
-                    int a = x[2 * k], b = x[2 * k + 1], sa = r2s[2 * k];
-                    const int sb = r2s[2 * k + 1];
-                    if (!(sa != sb ? sa < sb : uf_above(a, b))) {
-                        a = x[2 * k + 1];
-                        b = x[2 * k];
-                        sa = sb;
-                    }
-                    if (wg_cas(&rec[a].par, a, b) == a) {
-                        hooked_sz[k] = sa;
-                        todo[k] = false;
-                    } else {  // a was hooked meanwhile: find both roots again
-                        pu[2 * k] = pu[2 * k + 1] = true;
-                        any = true;
-                    }
+                int old = -1;
+                __hip_atomic_compare_exchange_strong(key + h, &old, c[k], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (old == -1) {  // first inserter: the root's block-start size, a singleton slot
+                    hsz[h] = rts[k];
+                    pm[h] = h;
+                    break;
                 }
-                if (!any) break;
-                rec_find<K2>(rec, x, pu, r2l, r2s);
+                if (old == c[k]) break;
+                h = h + 1 == kSeqHT ? 0 : h + 1;
             }
+            sl[k] = h;
         }
         __syncthreads();
         KT(1);
         // ---- C
-        {
-            int R[K];
-            bool pr[K];
-            int rrl[K], rrs[K];
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                R[k] = c[2 * k];
-                pr[k] = act2[2 * k];
-            }
-            rec_find<K>(rec, R, pr, rrl, rrs);
+        for (int k = 0; k < K; ++k)
+            if (act2[2 * k]) swp_union(pm, hsz, sl[2 * k], sl[2 * k + 1]);
+        __syncthreads();
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                if (!act2[2 * k]) continue;
-                int slot = (int)(uf_prio(R[k]) & (kSeqHT - 1));
-                for (;;) {
-                    int o = -1;
-                    __hip_atomic_compare_exchange_strong(hk + slot, &o, R[k], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (o == -1 || o == R[k]) break;
-                    slot = (slot + 1) & (kSeqHT - 1);
-                }
-                atomicMax(hmx + slot, tid + k * kSeqT);
-                atomicAdd(hsz + slot, hooked_sz[k]);
-                hold[slot] = rrs[k];  // R's size at the block start (same value from every inserter)
-                if (seq_compress()) {
-                    if (e[2 * k] != R[k]) rec_set_par(rec + e[2 * k], R[k]);
-                    if (e[2 * k + 1] != R[k]) rec_set_par(rec + e[2 * k + 1], R[k]);
-                }
+        for (int k = 0; k < K; ++k)
+            if (act2[2 * k]) {
+                const int r = swp_find(pm, sl[2 * k]);
+                atomicMax(pm + r, r | ((tid + k * kSeqT + 1) << 16));
             }
+        for (int x = tid; x < kSeqHT; x += kSeqT) {
+            if (key[x] < 0) continue;
+            const int r = swp_find(pm, x);
+            if (r != x) atomicAdd(hsz + r, hsz[x]);
         }
         __syncthreads();
         KT(2);
         // ---- D
-#pragma unroll
-        for (int q = 0; q < KS; ++q) {
-            const int x = tid + q * kSeqT;
-            const int R = hk[x];
-            if (R < 0) continue;
-            const int sz = hold[x] + hsz[x];
-            const int j = (int)(s + hmx[x]);
-            int2* lz = reinterpret_cast<int2*>(&rec[R].lab);
+        for (int x = tid; x < kSeqHT; x += kSeqT) {
+            const int g = key[x];
+            if (g < 0) continue;
+            const int r = swp_find(pm, x);
+            if (r != x) {
+                rec_set_par(rec + g, key[r]);
+                continue;
+            }
+            const int sz = hsz[x];
+            const int j = (int)(s + (pm[x] >> 16) - 1);
+            int2* lz = reinterpret_cast<int2*>(&rec[g].lab);
             *lz = make_int2(j, sz);
             if (progress)
                 __hip_atomic_store(SZ + j, sz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else
                 SZ[j] = sz;
-            hk[x] = -1;
-            hmx[x] = -1;
-            hsz[x] = 0;
         }
         __syncthreads();
+        for (int x = tid; x < kSeqHT; x += kSeqT) key[x] = -1;  // next used after phase A's barrier
         KT(3);
     }
 }
