@@ -2099,6 +2099,42 @@ __global__ __launch_bounds__(256) void k_boruvka_relabel4(Ws w, int r) {
     }
 }
 
+// KBoruvkaRelabelFind of rounds >= 1 on the record path, one wave per 32x8 tile (four pixels per lane):
+// a tile is relabelled only while it or one of its eight neighbours is active. Pass 0 reads a tile's
+// labels only for the tile itself or as the halo of a neighbour, the hook resolves the labels it
+// reads by finds, and nothing reads them after the MST — so a done tile among done tiles keeps its
+// stale labels (tile flags: the round that found the tile done, written by this round's pass 0).
+__global__ __launch_bounds__(256) void k_boruvka_relabel_t(Ws w, int r, RecBufs rb) {
+    const Dims& d = w.d;
+    const int f = blockIdx.y;
+    if (!w.C(f)[C_ACT + r]) return;
+    const int lane = __lane_id(), wv = threadIdx.x >> 6;
+    const int tiles_x = (d.W + kTileX - 1) / kTileX, tiles_y = (d.H + kTileY - 1) / kTileY;
+    const int tiles = tiles_x * tiles_y;
+    const unsigned char* td = rb.td + (int64_t)f * tiles;
+    int* comp = w.comp + f * d.N;
+    int* uf = w.uf + f * d.N;
+    for (int t = blockIdx.x * 4 + wv; t < tiles; t += gridDim.x * 4) {
+        const int tx = t % tiles_x, ty = t / tiles_x;
+        bool act = false;
+        if (lane < 9) {
+            const int nx = tx + lane % 3 - 1, ny = ty + lane / 3 - 1;
+            act = nx >= 0 && nx < tiles_x && ny >= 0 && ny < tiles_y && td[ny * tiles_x + nx] == 0;
+        }
+        if (!__ballot(act)) continue;  // wave-uniform
+        const int x0 = tx * kTileX + (lane & 7) * 4, y = ty * kTileY + (lane >> 3);
+        if (x0 >= d.W || y >= d.H) continue;  // W % 4 == 0: a lane's four pixels are all in or all out
+        int4* p4 = reinterpret_cast<int4*>(comp + (int64_t)y * d.W + x0);
+        const int4 v = *p4;
+        int4 o;
+        o.x = uf_find_ro_halve(uf, v.x);
+        o.y = v.y == v.x ? o.x : uf_find_ro_halve(uf, v.y);
+        o.z = v.z == v.y ? o.y : uf_find_ro_halve(uf, v.z);
+        o.w = v.w == v.z ? o.z : uf_find_ro_halve(uf, v.w);
+        if (o.x != v.x || o.y != v.y || o.z != v.z || o.w != v.w) *p4 = o;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // K1 blur, LDS-tiled (KBlurRow / KBlurCol of dofs_kernels.h, same float operations in the same
 // order): a row segment of 256 outputs (+ reflect-101 halo) or a 64 x 64 column tile (+ halo rows)
@@ -2587,7 +2623,20 @@ struct HipBackend {
         }
         pixel4(w, r, k_boruvka_hook4, "KBoruvkaHook");
     }
-    void boruvka_relabel(const Ws& w, int r) { pixel4(w, r, k_boruvka_relabel4, "KBoruvkaRelabelFind"); }
+    void boruvka_relabel(const Ws& w, int r) {
+        if (r >= 1 && rec_path(w) && relabel_tiles()) {  // round 0 runs before the tile flags exist
+            rec_launch(w, r, k_boruvka_relabel_t, "k_boruvka_relabelt");
+            return;
+        }
+        pixel4(w, r, k_boruvka_relabel4, "KBoruvkaRelabelFind");
+    }
+    static bool relabel_tiles() {  // DOFS_RELABEL_TILES=0: every pixel every round (k_boruvka_relabel4)
+        static const bool on = [] {
+            const char* e = getenv("DOFS_RELABEL_TILES");
+            return !(e && atoi(e) == 0);
+        }();
+        return on;
+    }
     void pixel4(const Ws& w, int r, void (*k)(Ws, int), const char* name) {
         const int64_t n4 = (w.d.N + 3) / 4;
         int64_t gx = (n4 + 255) / 256;
