@@ -2256,6 +2256,80 @@ __global__ __launch_bounds__(kDeepT) void k_krt_fused(Ws w, int* progress) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// K4 preorder positions of the merge nodes by one top-down sweep per frame over the KRT blocks (in
+// place of the global pointer jumping, KJump): a merge's parent has a higher rank, and after the LDS
+// KRT's epilogue every merge's jump word points either out of its block — to a node of a later
+// block, whose position the sweep already knows — or to its block-top ancestor, whose word points
+// out of the block. So the frame's blocks, last to first, each take one round of gathers of resolved
+// words and one LDS lookup; every merge's word ends converged (-1, position), and its pre / ord
+// entries are written here (KOrd then runs over the leaves only). One workgroup per frame: latency-
+// bound, it leaves the other CUs to the replay stage.
+// ---------------------------------------------------------------------------------------------
+constexpr int kPreT = 1024, kPreK = kDeepTop / kPreT;
+static_assert(kPreK * kPreT == kDeepTop, "preorder sweep shape");
+__global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w) {
+    __shared__ int lpos[kDeepTop];
+    const Dims& d = w.d;
+    const int f = blockIdx.x;
+    const int64_t lb = f * d.NL;
+    unsigned long long* J = w.J + lb;
+    int* pre = w.pre + lb;
+    int* ord = w.ord + lb;
+    const int tid = threadIdx.x;
+    const int64_t nblk = (d.M + kDeepTop - 1) / kDeepTop;
+    unsigned long long v[kPreK];
+    auto load = [&](int64_t b, unsigned long long (&o)[kPreK]) {  // the block's words (final until swept)
+        const int64_t x0 = d.N + b * kDeepTop;
+        const int cnt = (int)((d.M - b * kDeepTop) < kDeepTop ? (d.M - b * kDeepTop) : kDeepTop);
+#pragma unroll
+        for (int k = 0; k < kPreK; ++k) {
+            const int t = tid + k * kPreT;
+            o[k] = t < cnt ? J[x0 + t] : 0ull;
+        }
+    };
+    if (nblk > 0) load(nblk - 1, v);
+    for (int64_t b = nblk - 1; b >= 0; --b) {
+        const int64_t x0 = d.N + b * kDeepTop;
+        const int cnt = (int)((d.M - b * kDeepTop) < kDeepTop ? (d.M - b * kDeepTop) : kDeepTop);
+        const int64_t x1 = x0 + cnt;
+        unsigned long long nv[kPreK];
+        if (b > 0) load(b - 1, nv);  // prefetch: the next block's words
+        unsigned long long g[kPreK];
+        int pos[kPreK];
+        bool in[kPreK];
+#pragma unroll
+        for (int k = 0; k < kPreK; ++k) {  // all gathers first (ancestors in later blocks: resolved)
+            const int t = tid + k * kPreT;
+            const int a = jump_anc(v[k]);
+            in[k] = t < cnt && a >= x0 && a < x1;
+            g[k] = (t < cnt && a >= x1) ? J[a] : 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < kPreK; ++k) {
+            const int t = tid + k * kPreT;
+            if (t >= cnt || in[k]) continue;
+            pos[k] = jump_sum(v[k]) + jump_sum(g[k]);  // g = 0 at the root (a = -1)
+            lpos[t] = pos[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kPreK; ++k) {
+            const int t = tid + k * kPreT;
+            if (t >= cnt) continue;
+            if (in[k]) pos[k] = jump_sum(v[k]) + lpos[jump_anc(v[k]) - x0];  // the block-top's position
+            J[x0 + t] = jump_pack(-1, pos[k]);
+            pre[x0 + t] = pos[k];
+            ord[pos[k]] = (int)(x0 + t);
+        }
+        __syncthreads();  // this block's words are read by the gathers of the blocks below it
+        if (b > 0) {
+#pragma unroll
+            for (int k = 0; k < kPreK; ++k) v[k] = nv[k];
+        }
+    }
+}
+
 struct HipBackend {
     int device = 0;
     hipStream_t own = nullptr;
@@ -2622,6 +2696,17 @@ struct HipBackend {
             return;
         }
         pixel4(w, r, k_boruvka_hook4, "KBoruvkaHook");
+    }
+    // K4 merge positions by the top-down sweep (k_pre_sweep) instead of KJump; DOFS_PRE_SWEEP=0: KJump
+    bool pre_sweep(const Ws& w) {
+        static const bool on = [] {
+            const char* e = getenv("DOFS_PRE_SWEEP");
+            return !(e && atoi(e) == 0);
+        }();
+        if (!on) return false;
+        timed("k_pre_sweep", [&] { hipLaunchKernelGGL(k_pre_sweep, dim3((unsigned)w.d.B), dim3(kPreT), 0, stream, w); });
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_pre_sweep launch");
+        return true;
     }
     void boruvka_relabel(const Ws& w, int r) {
         if (r >= 1 && rec_path(w) && relabel_tiles()) {  // round 0 runs before the tile flags exist

@@ -348,12 +348,17 @@ struct Pipeline {
         // merge nodes only (the leaves hang off them): two hops per launch at least triple every
         // node's jump distance (the second hop may read an ancestor word not yet advanced in this
         // launch), so 3^launches >= M reaches every root
-        int launches = 0;
-        const int64_t chain = std::min<int64_t>(d.M, Backend::jump_chain_bound(d.M));
-        for (int64_t span = 1; span < chain; span *= 3) ++launches;
-        for (int t = 0; t < launches; ++t) be.launch(B, d.M, KJump{w.J, NL, 2, N});
+        // (the HIP backend instead sweeps each frame's KRT blocks top-down once, k_pre_sweep, and
+        // writes the merges' positions itself)
+        const bool swept = be.pre_sweep(w);
+        if (!swept) {
+            int launches = 0;
+            const int64_t chain = std::min<int64_t>(d.M, Backend::jump_chain_bound(d.M));
+            for (int64_t span = 1; span < chain; span *= 3) ++launches;
+            for (int t = 0; t < launches; ++t) be.launch(B, d.M, KJump{w.J, NL, 2, N});
+        }
         pre = w.pre;
-        be.launch(B, NL, KOrd{w});
+        be.launch(B, swept ? N : NL, KOrd{w});  // swept: the leaves only
         be.scan_excl_leaf(w.ord, w.lscan, NL, B, N);
         be.launch(B, N, KLeafOrder{w, pre});
         be.launch(B, d.M, KPathInit{w, pre});
