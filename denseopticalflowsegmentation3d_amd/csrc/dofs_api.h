@@ -224,7 +224,7 @@ struct Context {
         const char* kd = getenv("DOFS_KRT_DNC");
         p0.krt_dnc = p1.krt_dnc = p2.krt_dnc = kd && kd[0] == '1';
         const char* sp = getenv("DOFS_SPLIT");
-        p0.preorder_in_b = p1.preorder_in_b = p2.preorder_in_b = sp && sp[0] == '1';
+        p0.preorder_in_b = p1.preorder_in_b = p2.preorder_in_b = sp && (sp[0] == '1' || sp[0] == '2') ? sp[0] - '0' : 0;
         // stream priorities: DOFS_PRIO=2 (default) replay stage urgent — its workgroups are dispatched
         // first when a CU frees up, since the replay rounds are the pipeline's critical chain;
         // 1 = graph stage urgent, replay stage least (experiment); 0 = equal

@@ -1071,18 +1071,24 @@ __device__ void top_level(const Ws& w, TopShared& sh, int f, int64_t s0, int cnt
 // block, the sum of the offsets up to it), found by pointer jumping in LDS — so every global jump
 // leaves a block, and the global pointer jumping needs ~log3(2 x blocks) launches, not log3(M).
 struct ParentShared {
-    int lp[kDeepTop];    // local parent (index in the block) of a block merge, -1: parent outside
-    int loff[kDeepTop];  // offset to it
-    int lp2[kDeepTop], loff2[kDeepTop];  // the other buffer of the jumping rounds
-    unsigned char lit[kDeepTop];         // path-top flag of a block merge whose parent is in the block
+    // per block merge: (local parent index in the block, -1: parent outside) | offset sum << 32 —
+    // one 64-bit word, so the jumping runs in place (every snapshot of an ancestor's word is valid)
+    unsigned long long lw[kDeepTop];
+    unsigned char lit[kDeepTop];  // path-top flag of a block merge whose parent is in the block
 };
+__device__ __forceinline__ unsigned long long lds_ld64(unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st64(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, int cnt) {
     const Dims& d = w.d;
     const int64_t lb = f * d.NL, eb = f * d.M;
     const int tid = threadIdx.x;
     const int64_t x0 = d.N + s0;  // node id of the block's first merge
     for (int t = tid; t < cnt; t += kDeepT) {
-        sh.lp[t] = -1;
+        sh.lw[t] = jump_pack(-1, 0);
         sh.lit[t] = 0xFF;
     }
     __syncthreads();
@@ -1097,16 +1103,14 @@ __device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, in
         // path-top flags: read by KPathInit for merge nodes only (a leaf needs none); a child merge of
         // this block gets its flag in LDS (stored with the block's flags at the end, coalesced)
         if (h >= x0 && h < x0 + cnt) {
-            sh.lp[h - x0] = t;
-            sh.loff[h - x0] = 1;
+            sh.lw[h - x0] = jump_pack(t, 1);
             sh.lit[h - x0] = 0;
         } else {
             w.J[lb + h] = jump_pack(x, 1);
             if (h >= d.N) w.lite[lb + h] = 0;
         }
         if (l >= x0 && l < x0 + cnt) {
-            sh.lp[l - x0] = t;
-            sh.loff[l - x0] = offl;
+            sh.lw[l - x0] = jump_pack(t, offl);
             sh.lit[l - x0] = 1;
         } else {
             w.J[lb + l] = jump_pack(x, offl);
@@ -1114,42 +1118,39 @@ __device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, in
         }
     }
     __syncthreads();
-    // pointer jumping to the block-top ancestor (a node whose parent is outside the block keeps
-    // lp = -1 and its word is written by the block of its parent): double-buffered, one barrier per
-    // round, stopping at the first round in which no word advanced
-    int *lpa = sh.lp, *ofa = sh.loff, *lpb = sh.lp2, *ofb = sh.loff2;
-    for (int it = 0; (1 << it) < cnt; ++it) {
+    // pointer jumping to the block-top ancestor (a node whose parent is outside the block keeps -1 and
+    // its word is written by the block of its parent): in place, two hops per round on the freshest
+    // words, one barrier per round, until a round in which no word advanced
+    for (;;) {
         int moved = 0;
 #pragma unroll
         for (int k = 0; k < kDeepTop / kDeepT; ++k) {
             const int t = tid + k * kDeepT;
             if (t >= cnt) continue;
-            int p = lpa[t], o = ofa[t];
-            if (p >= 0) {
-                const int pp = lpa[p];
-                if (pp >= 0) {
-                    o += ofa[p];
-                    p = pp;
-                    moved = 1;
-                }
+            unsigned long long v = lds_ld64(sh.lw + t);
+            bool mv = false;
+#pragma unroll
+            for (int hop = 0; hop < 2; ++hop) {
+                const int p = jump_anc(v);
+                if (p < 0) break;
+                const unsigned long long u = lds_ld64(sh.lw + p);
+                if (jump_anc(u) < 0) break;  // p is the block top
+                v = jump_pack(jump_anc(u), jump_sum(v) + jump_sum(u));
+                mv = true;
             }
-            lpb[t] = p;
-            ofb[t] = o;
+            if (mv) {
+                lds_st64(sh.lw + t, v);
+                moved = 1;
+            }
         }
-        const int any = __syncthreads_or(moved);
-        int* x = lpa;
-        lpa = lpb;
-        lpb = x;
-        x = ofa;
-        ofa = ofb;
-        ofb = x;
-        if (!any) break;
+        if (!__syncthreads_or(moved)) break;
     }
     for (int t = tid; t < cnt; t += kDeepT) {
-        const int p = lpa[t];
-        if (p >= 0) w.J[lb + x0 + t] = jump_pack((int)(x0 + p), ofa[t]);
-        const unsigned char v = sh.lit[t];
-        if (v != 0xFF) w.lite[lb + x0 + t] = v;
+        const unsigned long long v = sh.lw[t];
+        const int p = jump_anc(v);
+        if (p >= 0) w.J[lb + x0 + t] = jump_pack((int)(x0 + p), jump_sum(v));
+        const unsigned char c = sh.lit[t];
+        if (c != 0xFF) w.lite[lb + x0 + t] = c;
     }
 }
 static_assert(kDeepTop % kDeepT == 0, "parent epilogue shape");

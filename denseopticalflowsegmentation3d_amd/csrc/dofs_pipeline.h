@@ -54,7 +54,7 @@ struct Pipeline {
     Dims cap{};  // allocated shape
     int* pre = nullptr;
     int64_t snap_cap = 4096;
-    bool preorder_in_b = false;
+    int preorder_in_b = 0;  // 0: the preorder in phase A; 1: in phase B; 2: the path inputs (KPathInit) in B
     bool krt_dnc = false;  // DOFS_KRT_DNC=1: block-start labels by the top-down global depths
     int skip_mask = 0;          // measurement only (DOFS_SKIPMASK): 1 short replay, 2 long replay, 4 lift
     bool keys_by_frame = true;  // key_out holds each frame's sorted weights (else: recomputed for events)
@@ -336,11 +336,16 @@ struct Pipeline {
         be.dnc_deep(w);
         be.dnc_parent(w);  // KDncParent (HIP: k_dnc_deep's epilogue)
 
-        if (!preorder_in_b) preorder();
+        if (preorder_in_b == 0) preorder();
+        if (preorder_in_b == 2) preorder_pos();
     }
 
     // K4 heavy-first preorder (pointer jumping) and the replay's per-position inputs
     void preorder() {
+        preorder_pos();
+        path_init();
+    }
+    void preorder_pos() {
         const Dims& d = w.d;
         const int B = d.B;
         const int64_t N = d.N, NL = d.NL;
@@ -361,8 +366,8 @@ struct Pipeline {
         be.launch(B, swept ? N : NL, KOrd{w});  // swept: the leaves only
         be.scan_excl_leaf(w.ord, w.lscan, NL, B, N);
         be.launch(B, N, KLeafOrder{w, pre});
-        be.launch(B, d.M, KPathInit{w, pre});
     }
+    void path_init() { be.launch(w.d.B, w.d.M, KPathInit{w, w.pre}); }
 
     // Phase B (replay + scoring): the order-dependent replay is latency-bound (a few waves per
     // frame), so the HIP backend overlaps it with the next batch's phase A on a second stream.
@@ -371,7 +376,11 @@ struct Pipeline {
         const int B = d.B;
         const int64_t N = d.N, M = d.M;
         if (M <= 0) return;
-        if (preorder_in_b) preorder();
+        if (preorder_in_b == 1) preorder();
+        if (preorder_in_b == 2) {
+            pre = w.pre;
+            path_init();
+        }
         be.mark(5);
         // K5 bottom-up replay of Forest::merge along heavy paths
         const int RR = ceil_log2(N) + 2;
