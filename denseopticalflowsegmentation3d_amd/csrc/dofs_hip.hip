@@ -1157,12 +1157,13 @@ static_assert(kDeepTop % kDeepT == 0, "parent epilogue shape");
 
 constexpr size_t kDeepSmem0 = sizeof(DeepShared) > sizeof(TopShared) ? sizeof(DeepShared) : sizeof(TopShared);
 constexpr size_t kDeepSmem = kDeepSmem0 > sizeof(ParentShared) ? kDeepSmem0 : sizeof(ParentShared);
-// all depths of one kDeepTop-merge block of frame f in LDS, then its parents (block-uniform call)
-__device__ void deep_item(const Ws& w, char* smem, int f, int64_t s0) {
+// all depths of one kDeepTop-merge block of frame f in LDS, then its parents (block-uniform call);
+// top: the block's first depth too (else the sweep did it: its labels are the two halves' starts)
+__device__ void deep_item(const Ws& w, char* smem, int f, int64_t s0, bool top) {
     const Dims& d = w.d;
     const int cnt = (int)((d.M - s0) < kDeepTop ? (d.M - s0) : kDeepTop);
     KT_DECL
-    if (cnt > kDeepS) top_level(w, *reinterpret_cast<TopShared*>(smem), f, s0, cnt);
+    if (top && cnt > kDeepS) top_level(w, *reinterpret_cast<TopShared*>(smem), f, s0, cnt);
     KT(5);
     deep_block(w, *reinterpret_cast<DeepShared*>(smem), f, s0, cnt < kDeepS ? cnt : kDeepS);
     __syncthreads();
@@ -1174,11 +1175,11 @@ __device__ void deep_item(const Ws& w, char* smem, int f, int64_t s0) {
     __syncthreads();
     KT(8);
 }
-__global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w) {
+__global__ __launch_bounds__(kDeepT) void k_dnc_deep(Ws w, int top) {
     __shared__ __attribute__((aligned(16))) char smem[kDeepSmem];
     const int64_t s0 = (int64_t)blockIdx.x * kDeepTop;
     if (s0 >= w.d.M) return;
-    deep_item(w, smem, blockIdx.y, s0);
+    deep_item(w, smem, blockIdx.y, s0, top != 0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1839,16 +1840,22 @@ __device__ __forceinline__ void rec_find(SeqRec* rec, int (&x)[K], bool (&pend)[
 //      the key never changes during the block, so a component's LDS root is its largest root —
 //      union by size keeps a frame's large components' roots stable, and the finds of later blocks
 //      short); then per LDS root the max rank in the block (one LDS atomicMax per merge) and the
-//      component's total size (every other slot adds its block-start size)
+//      component's total size (every other slot adds its block-start size). The unions run in two
+//      halves, which also does the LDS KRT's top level (the block's first depth): after the L half
+//      (the first kDeepS merges) an R-half endpoint whose component holds an L merge is relabelled
+//      to N + the component's max L rank, and the L-half component of the L half's last merge gets
+//      its size (the only L-half node size the LDS blocks do not write themselves); the block's
+//      labels are published after that, so each LDS-KRT block starts at its two halves' depths.
 //   D  per slot, one global store: a hooked root's parent (directly its component's root), or at
 //      the component's root its new label and size (8 bytes), plus the KRT node size SZ
 // The global forest only gains the hooks of D, each root one hop below its component's root.
 constexpr int kSeqHT = 12288;  // >= 2 kSeqB distinct roots at load <= 2/3
-static_assert(kSeqHT >= 3 * kSeqB && kSeqHT < 65536 && kSeqB < 32767, "sweep hash shape");
+static_assert(kSeqHT >= 3 * kSeqB && kSeqHT < 65536 && kSeqB < 32767 && kSeqB == 2 * kDeepS, "sweep hash shape");
 struct SweepShared {
     int key[kSeqHT];  // global root in the slot (-1 empty)
     int sz[kSeqHT];   // its size at the block start; at an LDS root after C, the component's total
     int pm[kSeqHT];   // LDS parent slot (low 16 bits); at an LDS root after C, (max rank + 1) << 16
+    int rlast, zlast;  // the L half's last merge: its LDS root, its component's size
 };
 // finds in the slot forest (path halving; a non-root's high bits stay 0)
 __device__ inline int swp_find(int* pm, int x) {
@@ -1872,10 +1879,12 @@ __device__ inline void swp_union(int* pm, const int* sz, int a, int b) {
             a = b;
             b = t;
         }
-        int old = a;
+        int old = lds_ld(pm + a);  // a root's word may carry its L-half max rank in the high bits
+        if ((old & 0xFFFF) != a) continue;
+        const int seen = old;
         __hip_atomic_compare_exchange_strong(pm + a, &old, b, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (old == a) return;
+        if (old == seen) return;
     }
 }
 // The sweep of frame f by one workgroup. progress (optional, stride kCounters per frame): after
@@ -1947,11 +1956,6 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
                 lv[s + t] = lb;
             }
         }
-        if (progress) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
-        __syncthreads();
-        if (progress && tid == 0)
-            __hip_atomic_store(progress + (int64_t)f * kCounters, (int)(s / kSeqB) + 1, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
         KT(0);
         // ---- B
         int sl[K2];
@@ -1976,17 +1980,72 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
         }
         __syncthreads();
         KT(1);
-        // ---- C
+        // ---- C, L half (the merges t < kDeepS): unions, then per LDS root the max L rank
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            if (act2[2 * k]) swp_union(pm, hsz, sl[2 * k], sl[2 * k + 1]);
+            if (act2[2 * k] && tid + k * kSeqT < kDeepS) swp_union(pm, hsz, sl[2 * k], sl[2 * k + 1]);
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-            if (act2[2 * k]) {
+        for (int k = 0; k < K; ++k) {
+            const int t = tid + k * kSeqT;
+            if (act2[2 * k] && t < kDeepS) {
                 const int r = swp_find(pm, sl[2 * k]);
-                atomicMax(pm + r, r | ((tid + k * kSeqT + 1) << 16));
+                atomicMax(pm + r, r | ((t + 1) << 16));
+                if (t == kDeepS - 1) sh.rlast = r;
             }
+        }
+        if (tid == 0) sh.zlast = 0;
+        __syncthreads();
+        if (cnt > kDeepS) {  // the top level: R-half endpoints relabelled, the last L merge's size
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int t = tid + k * kSeqT;
+                if (!act2[2 * k] || t < kDeepS) continue;
+#pragma unroll
+                for (int side = 0; side < 2; ++side) {
+                    const int m = pm[swp_find(pm, sl[2 * k + side])] >> 16;  // (max L rank + 1), 0: none
+                    if (!m) continue;
+                    int* lp = side ? lv : lu;
+                    const int lab = (int)(d.N + s + m - 1);
+                    if (progress)
+                        __hip_atomic_store(lp + s + t, lab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    else
+                        lp[s + t] = lab;
+                }
+            }
+            const int rl = sh.rlast;
+            int z = 0;
+            for (int x = tid; x < kSeqHT; x += kSeqT)
+                if (key[x] >= 0 && swp_find(pm, x) == rl) z += hsz[x];
+            if (z) atomicAdd(&sh.zlast, z);
+            __syncthreads();
+            if (tid == 0) {
+                const int j = (int)(s + kDeepS - 1);
+                if (progress)
+                    __hip_atomic_store(SZ + j, sh.zlast, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else
+                    SZ[j] = sh.zlast;
+            }
+        }
+        if (progress) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+        __syncthreads();
+        if (progress && tid == 0)
+            __hip_atomic_store(progress + (int64_t)f * kCounters, (int)(s / kSeqB) + 1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        KT(4);
+        // ---- C, R half: unions, max rank per LDS root (an L-only component keeps its L max), sizes
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (act2[2 * k] && tid + k * kSeqT >= kDeepS) swp_union(pm, hsz, sl[2 * k], sl[2 * k + 1]);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int t = tid + k * kSeqT;
+            if (act2[2 * k] && t >= kDeepS) {
+                const int r = swp_find(pm, sl[2 * k]);
+                atomicMax(pm + r, r | ((t + 1) << 16));
+            }
+        }
         for (int x = tid; x < kSeqHT; x += kSeqT) {
             if (key[x] < 0) continue;
             const int r = swp_find(pm, x);
@@ -2252,7 +2311,7 @@ __global__ __launch_bounds__(kDeepT) void k_krt_fused(Ws w, int* progress) {
         }
         __syncthreads();
         KT(11);
-        deep_item(w, smem, f, k * kDeepTop);
+        deep_item(w, smem, f, k * kDeepTop, false);
         __syncthreads();
     }
 }
@@ -2673,6 +2732,7 @@ struct HipBackend {
             fused_done = true;
             return;
         }
+        swept_top = true;
         launch(w.d.B, w.d.N, KSeqInitRec{reinterpret_cast<SeqRec*>(w.In), 2 * w.d.NL});
         timed("k_krt_seq", [&] {
             hipLaunchKernelGGL(k_krt_seq, dim3((unsigned)w.d.B), dim3(kSeqT), 0, stream, w);
@@ -2680,14 +2740,17 @@ struct HipBackend {
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_krt_seq launch");
     }
     bool fused_done = false;  // the last krt_seq already ran the LDS KRT
+    bool swept_top = false;   // the last krt_seq (unfused) did the blocks' top level
     void dnc_deep(const Ws& w) {
         if (fused_done) {
             fused_done = false;
             return;
         }
         const unsigned nb = (unsigned)((w.d.M + kDeepTop - 1) / kDeepTop);
+        const int top = swept_top ? 0 : 1;  // DOFS_KRT_DNC: the global depths stop above the block
+        swept_top = false;
         timed("k_dnc_deep", [&] {
-            hipLaunchKernelGGL(k_dnc_deep, dim3(nb, (unsigned)w.d.B), dim3(kDeepT), 0, stream, w);
+            hipLaunchKernelGGL(k_dnc_deep, dim3(nb, (unsigned)w.d.B), dim3(kDeepT), 0, stream, w, top);
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_dnc_deep launch");
     }

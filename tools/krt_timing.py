@@ -32,10 +32,10 @@ torch.cuda.synchronize()
 ctx.records_device()
 L.dofs_debug_krt_timing(out, 16)
 blocks = NB * B * ((H * W - 1 + 4095) // 4096)
-names = ["sweep A finds", "sweep B unions", "sweep C roots+hash", "sweep D stores", "-", "top level",
+names = ["sweep A finds", "sweep B unions", "sweep C roots+hash", "sweep D stores", "sweep top level (L half, R relabel)", "top level",
          "deep block 1", "deep block 2", "parent epilogue", "deep depths S>=256", "deep depths S<256",
          "LDS worker wait"]
 res = {n: {"total_ms": round(out[i] / 1e3, 2), "us_per_block": round(out[i] / blocks, 2)}
-       for i, n in enumerate(names) if n != "-"}
+       for i, n in enumerate(names)}
 hops = {"phase A find rounds (slowest thread) per sweep block": round(out[12] * 100 / max(out[13] * 100, 1), 2)}
 print(json.dumps({"B": B, "batches": NB, "blocks": blocks, "phases": res, "sweep": hops}, indent=1))
