@@ -760,6 +760,8 @@ static_assert(kDeepL < 32768 && kDeepHT < 32768, "local ids are int16");
 
 // LDS operations of one wave complete in order: waiting for them makes them visible to its other lanes
 __device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// a workgroup barrier that orders LDS only: outstanding global loads and stores are not waited for
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ inline int lds_ld(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ inline void lds_st(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ inline int lds_find(int* P, int x) {
@@ -1957,7 +1959,8 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
             }
         }
         KT(0);
-        // ---- B
+        // ---- B (after a barrier: the previous block's key clears precede the inserts; LDS only)
+        lds_barrier();
         int sl[K2];
 #pragma unroll
         for (int k = 0; k < K2; ++k) {
@@ -2260,6 +2263,84 @@ __global__ __launch_bounds__(kColT) void k_blur_col(Ws w) {
                 o.x = sx;
                 o.y = sy;
                 w.blur[f * w.d.N + (int64_t)y * W + x] = o;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// K1 in one pass (the blur radius of the reference's sigma = 3: 25 taps): per 64 x 32 output tile the
+// input rows and columns it needs, (32 + 2r) x (64 + 2r) with reflect-101 in both directions, are
+// staged in LDS once; the row filter writes (32 + 2r) x 64 row outputs to LDS (KBlurRow's operations
+// and order), the column filter the tile (KBlurCol's). A lane computes 8 consecutive outputs from a
+// 32-element window. No row-filtered field in HBM: 8 B in (plus halo) and 8 B out per pixel.
+constexpr int kFbW = 64, kFbH = 32, kFbR = 12, kFbT = 256;
+constexpr int kFbIW = kFbW + 2 * kFbR, kFbRH = kFbH + 2 * kFbR, kFbWin = 8 + 2 * kFbR;
+static_assert(kFbW == 64 && kFbH % 8 == 0 && (kFbW / 64) * (kFbH / 8) * 64 == kFbT, "fused blur shape");
+__global__ __launch_bounds__(kFbT) void k_blur_fused(Ws w) {
+    __shared__ F2 in[kFbRH * kFbIW];
+    __shared__ F2 ro[kFbRH * kFbW];
+    const int W = w.d.W, H = w.d.H;
+    const int tx = (W + kFbW - 1) / kFbW, ty = (H + kFbH - 1) / kFbH;
+    const int f = blockIdx.y;
+    const int tid = threadIdx.x;
+    const F2* src = w.flow + f * w.flow_fstride;
+    F2* dst = w.blur + f * w.d.N;
+    float k[2 * kFbR + 1];
+#pragma unroll
+    for (int t = 0; t <= 2 * kFbR; ++t) k[t] = w.bk[t];
+    for (int64_t bi = blockIdx.x; bi < (int64_t)tx * ty; bi += gridDim.x) {
+        const int x0 = (int)(bi % tx) * kFbW, y0 = (int)(bi / tx) * kFbH;
+        for (int e = tid; e < kFbRH * kFbIW; e += kFbT) {
+            const int i = e / kFbIW, c = e % kFbIW;
+            in[e] = src[(int64_t)reflect101(y0 - kFbR + i, H) * W + reflect101(x0 - kFbR + c, W)];
+        }
+        __syncthreads();
+        for (int it = tid; it < kFbRH * (kFbW / 8); it += kFbT) {  // row filter, 8 outputs per item
+            const int i = it / (kFbW / 8), j = it % (kFbW / 8);
+            if (x0 + 8 * j >= W) continue;  // columns beyond the frame feed no output
+            const F2* r = in + i * kFbIW + 8 * j;
+            F2 v[kFbWin];
+#pragma unroll
+            for (int q = 0; q < kFbWin; ++q) v[q] = r[q];
+#pragma unroll
+            for (int o = 0; o < 8; ++o) {
+                float sx = k[0] * v[o].x, sy = k[0] * v[o].y;
+#pragma unroll
+                for (int t = 1; t <= 2 * kFbR; ++t) {
+                    sx += k[t] * v[o + t].x;
+                    sy += k[t] * v[o + t].y;
+                }
+                F2 out;
+                out.x = sx;
+                out.y = sy;
+                ro[i * kFbW + 8 * j + o] = out;
+            }
+        }
+        __syncthreads();
+        {  // column filter: lane = column, 8 rows per lane
+            const int c = tid % kFbW, j = tid / kFbW;
+            const int x = x0 + c;
+            if (x < W) {
+                F2 v[kFbWin];
+#pragma unroll
+                for (int q = 0; q < kFbWin; ++q) v[q] = ro[(8 * j + q) * kFbW + c];
+#pragma unroll
+                for (int o = 0; o < 8; ++o) {
+                    const int y = y0 + 8 * j + o;
+                    const F2 cc = v[o + kFbR];
+                    float sx = k[kFbR] * cc.x + 0.0f, sy = k[kFbR] * cc.y + 0.0f;
+#pragma unroll
+                    for (int jj = 1; jj <= kFbR; ++jj) {
+                        const F2 a = v[o + kFbR + jj], b = v[o + kFbR - jj];
+                        sx += k[kFbR + jj] * (a.x + b.x);
+                        sy += k[kFbR + jj] * (a.y + b.y);
+                    }
+                    F2 out;
+                    out.x = sx;
+                    out.y = sy;
+                    if (y < H) dst[(int64_t)y * W + x] = out;
+                }
             }
         }
         __syncthreads();
@@ -2686,9 +2767,22 @@ struct HipBackend {
     static constexpr int64_t deep_block() { return kDeepTop; }
     void dnc_parent(const Ws&) {}  // done by k_dnc_deep's epilogue
     void blur(const Ws& w) {  // KBlurRow + KBlurCol, LDS-tiled
+        const int64_t cap = std::max<int64_t>(1, grid_cap() / w.d.B);
+        static const bool fused_on = [] {
+            const char* e = getenv("DOFS_BLUR_FUSED");
+            return !(e && e[0] == '0');
+        }();
+        if (fused_on && w.bn == 2 * kFbR + 1) {  // sigma = 3 (the reference's): one pass
+            const int64_t ft = (int64_t)((w.d.W + kFbW - 1) / kFbW) * ((w.d.H + kFbH - 1) / kFbH);
+            timed("k_blur_fused", [&] {
+                hipLaunchKernelGGL(k_blur_fused, dim3((unsigned)std::min(ft, cap), (unsigned)w.d.B), dim3(kFbT), 0,
+                                   stream, w);
+            });
+            if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "blur launch");
+            return;
+        }
         const int64_t segs = (int64_t)((w.d.W + kBlurSeg - 1) / kBlurSeg) * w.d.H;
         const int64_t tiles = (int64_t)((w.d.W + kColW - 1) / kColW) * ((w.d.H + kColH - 1) / kColH);
-        const int64_t cap = std::max<int64_t>(1, grid_cap() / w.d.B);
         timed("k_blur_row", [&] {
             hipLaunchKernelGGL(k_blur_row, dim3((unsigned)std::min(segs, cap), (unsigned)w.d.B), dim3(kBlurSeg), 0,
                                stream, w);
