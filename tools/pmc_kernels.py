@@ -34,6 +34,8 @@ PATTERN = {
     "KPathInit": "random",
     "KLift": "random",
     "KFilter": "random",
+    "k_pre_sweep": "random",     # jump words of later blocks (gathers); the ord[] scatter
+    "k_blur_fused": "stream",    # tile + halo rows of the flow in, the blurred tile out
 }
 
 
