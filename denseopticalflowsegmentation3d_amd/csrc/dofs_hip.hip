@@ -1102,6 +1102,7 @@ __device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, in
         const int offl = 2 * (lightB ? sa : sb);
         const int x = (int)(x0 + t);
         w.hlB[eb + s0 + t] = lightB ? 1 : 0;
+        w.hls[eb + s0 + t] = hl_pack(lightB ? sa : sb, lightB ? sb : sa);
         // path-top flags: read by KPathInit for merge nodes only (a leaf needs none); a child merge of
         // this block gets its flag in LDS (stored with the block's flags at the end, coalesced)
         if (h >= x0 && h < x0 + cnt) {

@@ -102,6 +102,10 @@ struct Ws {
     // per edge (stride M)
     int* cand;
     double* cscore;
+    // per merge (stride M): size of its heavy child | size of its light child << 32, written by the
+    // KRT's parent pass for KPathInit (coalesced instead of gathered); aliases cscore, which KLift
+    // fills only after the replay inputs are built
+    unsigned long long* hls;
     // segment tree (stride 2*P2)
     int* seg;
     // outputs (stride snap_cap)
@@ -982,6 +986,9 @@ struct KDncLRootRelabel {
 // into heavy (larger subtree; ties → A) and light, and seeds the heavy-first preorder's pointer
 // jumping (K4): a heavy child sits right after its parent (offset 1), the light one after the
 // parent's whole heavy subtree (offset 1 + 2*size(heavy) - 1). The light child starts a heavy path.
+DOFS_HD inline unsigned long long hl_pack(int sh, int sl) {
+    return (unsigned long long)(unsigned)sh | ((unsigned long long)(unsigned)sl << 32);
+}
 struct KDncParent {
     Ws w;
     DOFS_HD void operator()(int f, int64_t i) const {
@@ -997,6 +1004,7 @@ struct KDncParent {
         w.lite[lb + h] = 0;
         w.lite[lb + l] = 1;
         w.hlB[o] = lightB ? 1 : 0;
+        w.hls[o] = hl_pack(lightB ? sa : sb, lightB ? sb : sa);
     }
 };
 
@@ -1100,10 +1108,12 @@ struct KPathInit {  // one lane per merge node x = N + k; path ids and lists thr
             q = pre[lb + x];
             top = w.lite[lb + x] != 0;
             int lt, lB;
-            const int h = heavy_child(w, f, (int)x, &lt, &lB);
+            heavy_child(w, f, (int)x, &lt, &lB);
+            const unsigned long long hl = w.hls[f * d.M + k];  // children's sizes (the KRT's parent pass)
+            const int sh = (int)(unsigned)(hl & 0xffffffffu), sl = (int)(unsigned)(hl >> 32);
             StepIn in;
-            in.fs = h < d.N ? 1.f : (float)w.SZ[lb + h];  // a leaf has size 1 (no load)
-            in.r = 1. / (double)w.SZ[lb + x];
+            in.fs = (float)sh;
+            in.r = 1. / (double)(sh + sl);  // size(x)
             in.meta = (lB ? kStepB : 0) | (top ? kStepTop : 0);
             if (lt < d.N) {
                 const F2 v = w.blur[f * d.N + lt];
@@ -1114,8 +1124,8 @@ struct KPathInit {  // one lane per merge node x = N + k; path ids and lists thr
             } else {
                 in.meta |= kStepDyn;
                 in.wbx = in.wby = 0.f;
-                in.la = w.SZ[lb + lt];
-                in.lb = pre[lb + lt];
+                in.la = sl;
+                in.lb = q + 2 * sh;  // heavy-first preorder: the light child follows the heavy subtree
             }
             w.In[lb + q] = in;
             if (top) {  // heavy path [q, bottom): its bottom leaf is the first leaf after q in preorder

@@ -150,6 +150,7 @@ struct Pipeline {
         w.labels = (int*)take(4 * B * N);
         w.cand = (int*)take(4 * B * M);
         w.cscore = (double*)take(8 * B * M);
+        w.hls = reinterpret_cast<unsigned long long*>(w.cscore);  // dead until KLift
         w.seg = (int*)take(4 * B * 2 * d.P2);
         w.snaps = (dofs_snapshot*)take(sizeof(dofs_snapshot) * B * snap_cap);
         w.recs = (dofs_box_record*)take(sizeof(dofs_box_record) * B * snap_cap);
