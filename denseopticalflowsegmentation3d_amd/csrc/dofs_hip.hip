@@ -1787,7 +1787,18 @@ struct KSeqInitRec {
         rec[f * NL2 + x] = r;
     }
 };
-__device__ __forceinline__ SeqRec rec_ld(const SeqRec* p) { return *p; }
+// one 16-byte load (one request per hop: the finds are bounded by the CU's random-access rate); the
+// empty asm keeps the unused pad word live, so the load is not narrowed into two requests
+__device__ __forceinline__ SeqRec rec_ld(const SeqRec* p) {
+    const int4 v = *reinterpret_cast<const int4*>(p);
+    asm volatile("" ::"v"(v.y));
+    SeqRec r;
+    r.par = v.x;
+    r.pad = v.y;
+    r.lab = v.z;
+    r.sz = v.w;
+    return r;
+}
 __device__ __forceinline__ void rec_set_par(SeqRec* p, int v) { wg_st(&p->par, v); }
 
 // finds of K chains at once with path halving: each round issues every pending chain's load first;
