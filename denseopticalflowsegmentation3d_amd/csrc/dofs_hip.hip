@@ -954,6 +954,7 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
         if (b >= kDeepK) w.lv[eb + s0 + t] = (int)(d.N + s0 + (b - kDeepK));
         const int z = sh.SZ[kDeepK + t];
         if (z >= 0) w.SZ[lb + d.N + s0 + t] = z;
+        w.hls[eb + s0 + t] = hl_pack(sh.SZ[a], sh.SZ[b]);  // the children's sizes, for the epilogue
     }
 }
 
@@ -1096,7 +1097,8 @@ __device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, in
     __syncthreads();
     for (int t = tid; t < cnt; t += kDeepT) {
         const int a = w.lu[eb + s0 + t], b = w.lv[eb + s0 + t];
-        const int sa = a < d.N ? 1 : w.SZ[lb + a], sb = b < d.N ? 1 : w.SZ[lb + b];  // leaves: no load
+        const unsigned long long zab = w.hls[eb + s0 + t];  // children's sizes (the deep blocks)
+        const int sa = (int)(unsigned)(zab & 0xffffffffu), sb = (int)(unsigned)(zab >> 32);
         const bool lightB = sa >= sb;
         const int h = lightB ? a : b, l = lightB ? b : a;
         const int offl = 2 * (lightB ? sa : sb);
@@ -1108,16 +1110,14 @@ __device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, in
         if (h >= x0 && h < x0 + cnt) {
             sh.lw[h - x0] = jump_pack(t, 1);
             sh.lit[h - x0] = 0;
-        } else {
+        } else {  // (its path-top flag: k_pre_sweep, from this word's offset)
             w.J[lb + h] = jump_pack(x, 1);
-            if (h >= d.N) w.lite[lb + h] = 0;
         }
         if (l >= x0 && l < x0 + cnt) {
             sh.lw[l - x0] = jump_pack(t, offl);
             sh.lit[l - x0] = 1;
         } else {
             w.J[lb + l] = jump_pack(x, offl);
-            if (l >= d.N) w.lite[lb + l] = 1;
         }
     }
     __syncthreads();
@@ -2474,6 +2474,9 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w) {
             J[x0 + t] = jump_pack(-1, pos[k]);
             pre[x0 + t] = pos[k];
             ord[pos[k]] = (int)(x0 + t);
+            // a block top's word is still (parent, offset): offset 1 = heavy child, else light (a
+            // path top) — its flag, which the parent's block (the epilogue) did not scatter
+            if (!in[k] && jump_anc(v[k]) >= 0) w.lite[lb + x0 + t] = jump_sum(v[k]) != 1 ? 1 : 0;
         }
         __syncthreads();  // this block's words are read by the gathers of the blocks below it
         if (b > 0) {
@@ -2867,13 +2870,9 @@ struct HipBackend {
         }
         pixel4(w, r, k_boruvka_hook4, "KBoruvkaHook");
     }
-    // K4 merge positions by the top-down sweep (k_pre_sweep) instead of KJump; DOFS_PRE_SWEEP=0: KJump
+    // K4 merge positions by the top-down sweep (k_pre_sweep) instead of KJump (which the emulator
+    // keeps): it also writes the block tops' path-top flags, which the LDS KRT's epilogue leaves out
     bool pre_sweep(const Ws& w) {
-        static const bool on = [] {
-            const char* e = getenv("DOFS_PRE_SWEEP");
-            return !(e && atoi(e) == 0);
-        }();
-        if (!on) return false;
         timed("k_pre_sweep", [&] { hipLaunchKernelGGL(k_pre_sweep, dim3((unsigned)w.d.B), dim3(kPreT), 0, stream, w); });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_pre_sweep launch");
         return true;
