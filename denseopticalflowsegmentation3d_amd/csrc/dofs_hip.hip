@@ -1102,7 +1102,6 @@ __device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, in
         const bool lightB = sa >= sb;
         const int h = lightB ? a : b, l = lightB ? b : a;
         const int offl = 2 * (lightB ? sa : sb);
-        const int x = (int)(x0 + t);
         w.hlB[eb + s0 + t] = lightB ? 1 : 0;
         w.hls[eb + s0 + t] = hl_pack(lightB ? sa : sb, lightB ? sb : sa);
         // path-top flags: read by KPathInit for merge nodes only (a leaf needs none); a child merge of
@@ -1110,14 +1109,10 @@ __device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, in
         if (h >= x0 && h < x0 + cnt) {
             sh.lw[h - x0] = jump_pack(t, 1);
             sh.lit[h - x0] = 0;
-        } else {  // (its path-top flag: k_pre_sweep, from this word's offset)
-            w.J[lb + h] = jump_pack(x, 1);
-        }
+        }  // (a child outside the block: k_pre_sweep pushes its position and flag)
         if (l >= x0 && l < x0 + cnt) {
             sh.lw[l - x0] = jump_pack(t, offl);
             sh.lit[l - x0] = 1;
-        } else {
-            w.J[lb + l] = jump_pack(x, offl);
         }
     }
     __syncthreads();
@@ -1151,7 +1146,8 @@ __device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, in
     for (int t = tid; t < cnt; t += kDeepT) {
         const unsigned long long v = sh.lw[t];
         const int p = jump_anc(v);
-        if (p >= 0) w.J[lb + x0 + t] = jump_pack((int)(x0 + p), jump_sum(v));
+        // a block top (parent outside the block) is marked -2: k_pre_sweep reads its pushed position
+        w.J[lb + x0 + t] = p >= 0 ? jump_pack((int)(x0 + p), jump_sum(v)) : jump_pack(-2, 0);
         const unsigned char c = sh.lit[t];
         if (c != 0xFF) w.lite[lb + x0 + t] = c;
     }
@@ -2410,81 +2406,123 @@ __global__ __launch_bounds__(kDeepT) void k_krt_fused(Ws w, int* progress) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// K4 preorder positions of the merge nodes by one top-down sweep per frame over the KRT blocks (in
-// place of the global pointer jumping, KJump): a merge's parent has a higher rank, and after the LDS
-// KRT's epilogue every merge's jump word points either out of its block — to a node of a later
-// block, whose position the sweep already knows — or to its block-top ancestor, whose word points
-// out of the block. So the frame's blocks, last to first, each take one round of gathers of resolved
-// words and one LDS lookup; every merge's word ends converged (-1, position), and its pre / ord
-// entries are written here (KOrd then runs over the leaves only). One workgroup per frame: latency-
-// bound, it leaves the other CUs to the replay stage.
+// K4 preorder positions by one top-down sweep per frame over the KRT blocks (in place of the global
+// pointer jumping, KJump, which the emulator keeps). A merge's parent has a higher rank; after the
+// LDS KRT's epilogue a merge's word is (its block-top ancestor, offset sum) or, at a block top, the
+// mark -2. The frame's blocks are taken last to first: a block top's position was pushed into pre[]
+// by its parent's block (bit 31: it is a light child, a path top), the other merges add their offset
+// sum to their top's position (LDS), and every merge then pushes its merge children outside the
+// block (tops of earlier blocks) their positions (heavy: +1, light: +2 size(heavy)). Per block one
+// coalesced read of pushed positions, no gathers; the merges' pre / ord entries, converged words and
+// the tops' path-top flags come out of this pass, the leaves' from KLeafPos (parallel) after it.
+// One workgroup per frame: latency-bound, it leaves the other CUs to the replay stage.
 // ---------------------------------------------------------------------------------------------
 constexpr int kPreT = 1024, kPreK = kDeepTop / kPreT;
 static_assert(kPreK * kPreT == kDeepTop, "preorder sweep shape");
+constexpr int kPushLight = (int)0x80000000u;
 __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w) {
     __shared__ int lpos[kDeepTop];
     const Dims& d = w.d;
     const int f = blockIdx.x;
-    const int64_t lb = f * d.NL;
+    const int64_t lb = f * d.NL, eb = f * d.M;
     unsigned long long* J = w.J + lb;
     int* pre = w.pre + lb;
     int* ord = w.ord + lb;
     const int tid = threadIdx.x;
     const int64_t nblk = (d.M + kDeepTop - 1) / kDeepTop;
-    unsigned long long v[kPreK];
-    auto load = [&](int64_t b, unsigned long long (&o)[kPreK]) {  // the block's words (final until swept)
-        const int64_t x0 = d.N + b * kDeepTop;
-        const int cnt = (int)((d.M - b * kDeepTop) < kDeepTop ? (d.M - b * kDeepTop) : kDeepTop);
+    const int64_t root = d.N + d.M - 1;
+    struct Node {  // a merge's static inputs (final until swept)
+        unsigned long long v, hl;
+        int a, b;
+        unsigned char lB;
+    };
+    Node nd[kPreK];
+    auto load = [&](int64_t blk, Node (&o)[kPreK]) {
+        const int64_t s0 = blk * kDeepTop;
+        const int cnt = (int)((d.M - s0) < kDeepTop ? (d.M - s0) : kDeepTop);
 #pragma unroll
         for (int k = 0; k < kPreK; ++k) {
             const int t = tid + k * kPreT;
-            o[k] = t < cnt ? J[x0 + t] : 0ull;
+            if (t < cnt) {
+                o[k].v = J[d.N + s0 + t];
+                o[k].hl = w.hls[eb + s0 + t];
+                o[k].a = w.lu[eb + s0 + t];
+                o[k].b = w.lv[eb + s0 + t];
+                o[k].lB = w.hlB[eb + s0 + t];
+            }
         }
     };
-    if (nblk > 0) load(nblk - 1, v);
-    for (int64_t b = nblk - 1; b >= 0; --b) {
-        const int64_t x0 = d.N + b * kDeepTop;
-        const int cnt = (int)((d.M - b * kDeepTop) < kDeepTop ? (d.M - b * kDeepTop) : kDeepTop);
-        const int64_t x1 = x0 + cnt;
-        unsigned long long nv[kPreK];
-        if (b > 0) load(b - 1, nv);  // prefetch: the next block's words
-        unsigned long long g[kPreK];
+    if (nblk > 0) load(nblk - 1, nd);
+    for (int64_t blk = nblk - 1; blk >= 0; --blk) {
+        const int64_t s0 = blk * kDeepTop, x0 = d.N + s0;
+        const int cnt = (int)((d.M - s0) < kDeepTop ? (d.M - s0) : kDeepTop);
         int pos[kPreK];
-        bool in[kPreK];
+        bool top[kPreK];
+        int pushed[kPreK];
 #pragma unroll
-        for (int k = 0; k < kPreK; ++k) {  // all gathers first (ancestors in later blocks: resolved)
+        for (int k = 0; k < kPreK; ++k) {  // the tops' pushed positions (complete: the last barrier)
             const int t = tid + k * kPreT;
-            const int a = jump_anc(v[k]);
-            in[k] = t < cnt && a >= x0 && a < x1;
-            g[k] = (t < cnt && a >= x1) ? J[a] : 0ull;
+            top[k] = t < cnt && jump_anc(nd[k].v) == -2;
+            pushed[k] = top[k] && x0 + t != root ? pre[x0 + t] : 0;
         }
+        Node nx[kPreK];
+        if (blk > 0) load(blk - 1, nx);  // prefetch the next block's inputs
 #pragma unroll
         for (int k = 0; k < kPreK; ++k) {
             const int t = tid + k * kPreT;
-            if (t >= cnt || in[k]) continue;
-            pos[k] = jump_sum(v[k]) + jump_sum(g[k]);  // g = 0 at the root (a = -1)
+            if (!top[k]) continue;
+            pos[k] = pushed[k] & 0x7FFFFFFF;
             lpos[t] = pos[k];
+            // path-top flag of a top: bit 31 of its push (the root: a path top)
+            w.lite[lb + x0 + t] = x0 + t == root || (pushed[k] & kPushLight) ? 1 : 0;
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int k = 0; k < kPreK; ++k) {
             const int t = tid + k * kPreT;
             if (t >= cnt) continue;
-            if (in[k]) pos[k] = jump_sum(v[k]) + lpos[jump_anc(v[k]) - x0];  // the block-top's position
-            J[x0 + t] = jump_pack(-1, pos[k]);
-            pre[x0 + t] = pos[k];
-            ord[pos[k]] = (int)(x0 + t);
-            // a block top's word is still (parent, offset): offset 1 = heavy child, else light (a
-            // path top) — its flag, which the parent's block (the epilogue) did not scatter
-            if (!in[k] && jump_anc(v[k]) >= 0) w.lite[lb + x0 + t] = jump_sum(v[k]) != 1 ? 1 : 0;
+            const int64_t x = x0 + t;
+            if (!top[k]) pos[k] = jump_sum(nd[k].v) + lpos[jump_anc(nd[k].v) - x0];
+            J[x] = jump_pack(-1, pos[k]);
+            pre[x] = pos[k];
+            ord[pos[k]] = (int)x;
+            // push the merge children outside the block (tops of earlier blocks) their positions;
+            // the leaves get theirs from KLeafPos, in parallel after the sweep
+            const int sh = (int)(unsigned)(nd[k].hl & 0xffffffffu);
+            const int h = nd[k].lB ? nd[k].a : nd[k].b, l = nd[k].lB ? nd[k].b : nd[k].a;
+            if (h < x0 && h >= d.N) pre[h] = pos[k] + 1;
+            if (l < x0 && l >= d.N) pre[l] = (pos[k] + 2 * sh) | kPushLight;
         }
-        __syncthreads();  // this block's words are read by the gathers of the blocks below it
-        if (b > 0) {
+        __syncthreads();  // the pushes are read by the blocks below
+        if (blk > 0) {
 #pragma unroll
-            for (int k = 0; k < kPreK; ++k) v[k] = nv[k];
+            for (int k = 0; k < kPreK; ++k) nd[k] = nx[k];
         }
     }
 }
+
+// the leaves' positions from their parents' (after k_pre_sweep): one lane per merge, both children
+struct KLeafPos {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t k) const {
+        const Dims& d = w.d;
+        const int64_t lb = f * d.NL, e = f * d.M + k;
+        const int a = w.lu[e], b = w.lv[e];
+        if (a >= d.N && b >= d.N) return;
+        const int q = w.pre[lb + d.N + k];
+        const int sh = (int)(unsigned)(w.hls[e] & 0xffffffffu);
+        const bool lB = w.hlB[e] != 0;
+        const int h = lB ? a : b, l = lB ? b : a;
+        if (h < d.N) {
+            w.pre[lb + h] = q + 1;
+            w.ord[lb + q + 1] = h;
+        }
+        if (l < d.N) {
+            w.pre[lb + l] = q + 2 * sh;
+            w.ord[lb + q + 2 * sh] = l;
+        }
+    }
+};
 
 struct HipBackend {
     int device = 0;
@@ -2875,6 +2913,7 @@ struct HipBackend {
     bool pre_sweep(const Ws& w) {
         timed("k_pre_sweep", [&] { hipLaunchKernelGGL(k_pre_sweep, dim3((unsigned)w.d.B), dim3(kPreT), 0, stream, w); });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_pre_sweep launch");
+        launch(w.d.B, w.d.M, KLeafPos{w});
         return true;
     }
     void boruvka_relabel(const Ws& w, int r) {

@@ -355,7 +355,7 @@ struct Pipeline {
         // node's jump distance (the second hop may read an ancestor word not yet advanced in this
         // launch), so 3^launches >= M reaches every root
         // (the HIP backend instead sweeps each frame's KRT blocks top-down once, k_pre_sweep, and
-        // writes the merges' positions itself)
+        // writes every node's position itself)
         const bool swept = be.pre_sweep(w);
         if (!swept) {
             int launches = 0;
@@ -364,7 +364,7 @@ struct Pipeline {
             for (int t = 0; t < launches; ++t) be.launch(B, d.M, KJump{w.J, NL, 2, N});
         }
         pre = w.pre;
-        be.launch(B, swept ? N : NL, KOrd{w});  // swept: the leaves only
+        if (!swept) be.launch(B, NL, KOrd{w});  // the sweep writes every position itself
         be.scan_excl_leaf(w.ord, w.lscan, NL, B, N);
         be.launch(B, N, KLeafOrder{w, pre});
     }
