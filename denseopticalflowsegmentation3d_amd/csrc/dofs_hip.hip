@@ -2483,8 +2483,7 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w) {
             if (t >= cnt) continue;
             const int64_t x = x0 + t;
             if (!top[k]) pos[k] = jump_sum(nd[k].v) + lpos[jump_anc(nd[k].v) - x0];
-            J[x] = jump_pack(-1, pos[k]);
-            pre[x] = pos[k];
+            pre[x] = pos[k];  // (the converged word is not needed: nothing reads J after this pass)
             ord[pos[k]] = (int)x;
             // push the merge children outside the block (tops of earlier blocks) their positions;
             // the leaves get theirs from KLeafPos, in parallel after the sweep

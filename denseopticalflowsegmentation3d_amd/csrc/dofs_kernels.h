@@ -1133,7 +1133,7 @@ struct KPathInit {  // one lane per merge node x = N + k; path ids and lists thr
                 qb = pre[lb + leaf];
                 islong = qb - q >= w.long_path;
             }
-            w.ready[lb + q] = islong ? kPendLong : kIntMax;
+            if (top) w.ready[lb + q] = islong ? kPendLong : kIntMax;  // read at path tops only
             if (islong) dofs_aadd(w.C(f) + C_LONGM, qb - q);
         }
         // short paths in two lists by length, so round 0's waves hold paths of like length (a wave
