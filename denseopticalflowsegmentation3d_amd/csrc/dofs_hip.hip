@@ -2500,7 +2500,7 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w) {
     }
 }
 
-// the leaves' positions from their parents' (after k_pre_sweep): one lane per merge, both children
+// the leaves' ord[] entries from their parents' positions (after k_pre_sweep): one lane per merge
 struct KLeafPos {
     Ws w;
     DOFS_HD void operator()(int f, int64_t k) const {
@@ -2512,14 +2512,8 @@ struct KLeafPos {
         const int sh = (int)(unsigned)(w.hls[e] & 0xffffffffu);
         const bool lB = w.hlB[e] != 0;
         const int h = lB ? a : b, l = lB ? b : a;
-        if (h < d.N) {
-            w.pre[lb + h] = q + 1;
-            w.ord[lb + q + 1] = h;
-        }
-        if (l < d.N) {
-            w.pre[lb + l] = q + 2 * sh;
-            w.ord[lb + q + 2 * sh] = l;
-        }
+        if (h < d.N) w.ord[lb + q + 1] = h;  // (a leaf's pre[] is not read: KPathInit uses lposr)
+        if (l < d.N) w.ord[lb + q + 2 * sh] = l;
     }
 };
 

@@ -90,6 +90,8 @@ struct Ws {
     int* ready;
     // per pixel (stride N)
     int* leaf_order;
+    int* lposr;  // per frame (stride N): preorder position of the leaf of each leaf rank (aliases uf,
+                 // dead after the MST); KPathInit's path bottoms
     int* cur;
     int* ptop;
     int* list_short;
@@ -1075,13 +1077,16 @@ struct KOrd {  // preorder positions; a leaf (x < N) takes its last jump here (K
     }
 };
 
-struct KLeafOrder {
-    Ws w;
+struct KLeafOrder {  // one lane per preorder position: leaf ranks rise with the position, so both the
+    Ws w;           // reads (ord, lscan) and the leaves' stores (leaf_order) are coalesced
     const int* pre;
-    DOFS_HD void operator()(int f, int64_t v) const {
+    DOFS_HD void operator()(int f, int64_t q) const {
         const Dims& d = w.d;
-        const int lp = w.lscan[f * d.NL + pre[f * d.NL + v]];
-        w.leaf_order[f * d.N + lp] = (int)v;
+        const int v = w.ord[f * d.NL + q];
+        if (v >= d.N) return;  // a merge
+        const int r = w.lscan[f * d.NL + q];
+        w.leaf_order[f * d.N + r] = v;
+        w.lposr[f * d.N + r] = (int)q;
     }
 };
 
@@ -1129,8 +1134,7 @@ struct KPathInit {  // one lane per merge node x = N + k; path ids and lists thr
             }
             w.In[lb + q] = in;
             if (top) {  // heavy path [q, bottom): its bottom leaf is the first leaf after q in preorder
-                const int leaf = w.leaf_order[f * d.N + w.lscan[lb + q]];
-                qb = pre[lb + leaf];
+                qb = w.lposr[f * d.N + w.lscan[lb + q]];
                 islong = qb - q >= w.long_path;
             }
             if (top) w.ready[lb + q] = islong ? kPendLong : kIntMax;  // read at path tops only

@@ -113,6 +113,7 @@ struct Pipeline {
         w.bw = (unsigned long long*)take(8 * B * N);
         w.bi = (unsigned*)take(4 * B * N);
         w.uf = (int*)take(4 * B * N);
+        w.lposr = w.uf;  // the MST's union-find is dead once the KRT starts
         w.mstbits = (int*)take(4 * B * N);
         w.cnt = (int*)take(4 * B * N);
         w.off = (int*)take(4 * B * N);
@@ -366,7 +367,7 @@ struct Pipeline {
         pre = w.pre;
         if (!swept) be.launch(B, NL, KOrd{w});  // the sweep writes every position itself
         be.scan_excl_leaf(w.ord, w.lscan, NL, B, N);
-        be.launch(B, N, KLeafOrder{w, pre});
+        be.launch(B, NL, KLeafOrder{w, pre});
     }
     void path_init() { be.launch(w.d.B, w.d.M, KPathInit{w, w.pre}); }
 
