@@ -2297,11 +2297,26 @@ __global__ __launch_bounds__(kFbT) void k_blur_fused(Ws w) {
     float k[2 * kFbR + 1];
 #pragma unroll
     for (int t = 0; t <= 2 * kFbR; ++t) k[t] = w.bk[t];
+    constexpr int kLd = (kFbRH * kFbIW + kFbT - 1) / kFbT;  // staged elements per lane
     for (int64_t bi = blockIdx.x; bi < (int64_t)tx * ty; bi += gridDim.x) {
         const int x0 = (int)(bi % tx) * kFbW, y0 = (int)(bi / tx) * kFbH;
-        for (int e = tid; e < kFbRH * kFbIW; e += kFbT) {
+        // every lane's loads issued before any is stored (one memory wait per tile); reflect-101 by
+        // one reflection, branch-free (the launcher keeps frames of W >= 128, H >= 64 here, so no
+        // coordinate of a tile and its halo reflects twice)
+        F2 st[kLd];
+#pragma unroll
+        for (int u = 0; u < kLd; ++u) {
+            const int e = tid + u * kFbT;
             const int i = e / kFbIW, c = e % kFbIW;
-            in[e] = src[(int64_t)reflect101(y0 - kFbR + i, H) * W + reflect101(x0 - kFbR + c, W)];
+            int yy = y0 - kFbR + i, xx = x0 - kFbR + c;
+            yy = yy < 0 ? -yy : (yy >= H ? 2 * H - 2 - yy : yy);
+            xx = xx < 0 ? -xx : (xx >= W ? 2 * W - 2 - xx : xx);
+            if (e < kFbRH * kFbIW) st[u] = src[(int64_t)yy * W + xx];
+        }
+#pragma unroll
+        for (int u = 0; u < kLd; ++u) {
+            const int e = tid + u * kFbT;
+            if (e < kFbRH * kFbIW) in[e] = st[u];
         }
         __syncthreads();
         for (int it = tid; it < kFbRH * (kFbW / 8); it += kFbT) {  // row filter, 8 outputs per item
@@ -2818,7 +2833,7 @@ struct HipBackend {
             const char* e = getenv("DOFS_BLUR_FUSED");
             return !(e && e[0] == '0');
         }();
-        if (fused_on && w.bn == 2 * kFbR + 1) {  // sigma = 3 (the reference's): one pass
+        if (fused_on && w.bn == 2 * kFbR + 1 && w.d.W >= 128 && w.d.H >= 64) {  // sigma = 3: one pass
             const int64_t ft = (int64_t)((w.d.W + kFbW - 1) / kFbW) * ((w.d.H + kFbH - 1) / kFbH);
             timed("k_blur_fused", [&] {
                 hipLaunchKernelGGL(k_blur_fused, dim3((unsigned)std::min(ft, cap), (unsigned)w.d.B), dim3(kFbT), 0,
