@@ -827,9 +827,21 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
     const int tid = threadIdx.x;
     for (int x = tid; x < kDeepHT; x += kDeepT) sh.hkey[x] = -1;
     __syncthreads();
-    for (int t = tid; t < cnt; t += kDeepT) {  // hash the global labels
+    constexpr int kPerT = kDeepS / kDeepT;  // merges per thread
+    static_assert(kPerT * kDeepT == kDeepS, "deep block shape");
+    int gl[2 * kPerT];  // the labels, all loaded before the first insert
+#pragma unroll
+    for (int u = 0; u < kPerT; ++u) {
+        const int t = tid + u * kDeepT;
+        gl[2 * u] = t < cnt ? w.lu[eb + s0 + t] : 0;
+        gl[2 * u + 1] = t < cnt ? w.lv[eb + s0 + t] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kPerT; ++u) {  // hash the global labels
+        const int t = tid + u * kDeepT;
+        if (t >= cnt) continue;
         for (int side = 0; side < 2; ++side) {
-            const int g = side ? w.lv[eb + s0 + t] : w.lu[eb + s0 + t];
+            const int g = gl[2 * u + side];
             int h = (int)(uf_prio(g) % (unsigned)kDeepHT);
             for (;;) {
                 int old = -1;
@@ -856,11 +868,21 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
         __syncthreads();
         int base = incl - c;
         for (int wv = 0; wv < (tid >> 6); ++wv) base += sh.wsum[wv];
-        for (int x = beg; x < end; ++x)
-            if (sh.hkey[x] != -1) {
-                sh.hval[x] = (short)base;
-                const int g = sh.hkey[x];
-                sh.SZ[base] = g < d.N ? 1 : w.SZ[lb + g];  // a pixel label is a leaf (size 1): no load
+        // the merge labels' sizes: every load issued before any is used (a pixel label is a leaf of
+        // size 1 and an empty slot loads nothing useful: both read a valid dummy word)
+        int gk[per], gz[per];
+#pragma unroll
+        for (int u = 0; u < per; ++u) {
+            const int x = beg + u;
+            gk[u] = x < end ? sh.hkey[x] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < per; ++u) gz[u] = w.SZ[lb + (gk[u] >= d.N ? gk[u] : 0)];
+#pragma unroll
+        for (int u = 0; u < per; ++u)
+            if (gk[u] != -1) {
+                sh.hval[beg + u] = (short)base;
+                sh.SZ[base] = gk[u] < d.N ? 1 : gz[u];
                 ++base;
             }
     }
