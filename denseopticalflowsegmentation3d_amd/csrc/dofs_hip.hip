@@ -1426,6 +1426,12 @@ struct RecBufs {  // the records: pixel-strided arrays free during the MST
 __device__ __forceinline__ bool lexless(unsigned long long wa, unsigned ia, unsigned long long wb, unsigned ib) {
     return wa < wb || (wa == wb && ia < ib);
 }
+// The tiles a wave visits in a grid-stride loop (t = first + i * stride) that are still active: 64
+// tiles' flags checked at once, one per lane (a done tile costs no dependent load of its own)
+__device__ __forceinline__ unsigned long long active_tiles(const unsigned char* td, int t0, int stride, int tiles) {
+    const int tl = t0 + __lane_id() * stride;
+    return __ballot(tl < tiles && td[tl] == 0);
+}
 __global__ __launch_bounds__(256) void k_boruvka_min4(Ws w, int r, RecBufs rb) {
     __shared__ RecHash sh[4];
     const Dims& d = w.d;
@@ -1451,8 +1457,9 @@ __global__ __launch_bounds__(256) void k_boruvka_min4(Ws w, int r, RecBufs rb) {
     unsigned short* tc = rb.tc + (int64_t)f * tiles;
     const int W = d.W, Hh = d.H;
     int nrec = 0;
-    for (int t = blockIdx.x * 4 + wv; t < tiles; t += gridDim.x * 4) {
-        if (td[t]) continue;  // wave-uniform
+    for (int t0 = blockIdx.x * 4 + wv; t0 < tiles; t0 += 64 * gridDim.x * 4) {
+        for (unsigned long long tm = active_tiles(td, t0, gridDim.x * 4, tiles); tm; tm &= tm - 1) {
+            const int t = t0 + (__ffsll((long long)tm) - 1) * (gridDim.x * 4);
         const int x0 = (t % tiles_x) * kTileX + (lane & 7) * 4, y = (t / tiles_x) * kTileY + (lane >> 3);
         const bool valid = x0 < W && y < Hh;  // W % 4 == 0: the lane's four pixels are all in or all out
         const int yc = min(y, Hh - 1), xc = min(x0, W - 4);
@@ -1623,6 +1630,7 @@ __global__ __launch_bounds__(256) void k_boruvka_min4(Ws w, int r, RecBufs rb) {
         }
         nrec += cnt;
     }
+    }
     if (lane == 0 && nrec) {
         w.C(f)[C_ACT + r] = 1;
         atomicAdd(w.trec + (int64_t)f * kRoundsMax + r, nrec);
@@ -1644,8 +1652,9 @@ __global__ __launch_bounds__(256) void k_boruvka_recs(Ws w, int r, RecBufs rb) {
     const int* rk = rb.rk + f * d.N;
     const unsigned char* td = rb.td + (int64_t)f * tiles;
     const unsigned short* tc = rb.tc + (int64_t)f * tiles;
-    for (int t = blockIdx.x * 4 + wv; t < tiles; t += gridDim.x * 4) {
-        if (td[t]) continue;
+    for (int t0 = blockIdx.x * 4 + wv; t0 < tiles; t0 += 64 * gridDim.x * 4) {
+        for (unsigned long long tm = active_tiles(td, t0, gridDim.x * 4, tiles); tm; tm &= tm - 1) {
+            const int t = t0 + (__ffsll((long long)tm) - 1) * (gridDim.x * 4);
         const int cnt = tc[t];
         for (int k = lane; k < cnt; k += 64) {
             const int64_t px = rec_px(d, tiles_x, t, k);
@@ -1666,6 +1675,7 @@ __global__ __launch_bounds__(256) void k_boruvka_recs(Ws w, int r, RecBufs rb) {
                 uf_union(w.uf + f * d.N, comp[p], comp[q]);
             }
         }
+    }
     }
 }
 
@@ -2207,24 +2217,40 @@ __global__ __launch_bounds__(256) void k_boruvka_relabel_t(Ws w, int r, RecBufs 
     const unsigned char* td = rb.td + (int64_t)f * tiles;
     int* comp = w.comp + f * d.N;
     int* uf = w.uf + f * d.N;
-    for (int t = blockIdx.x * 4 + wv; t < tiles; t += gridDim.x * 4) {
-        const int tx = t % tiles_x, ty = t / tiles_x;
+    const int stride = gridDim.x * 4;
+    for (int t0 = blockIdx.x * 4 + wv; t0 < tiles; t0 += 64 * stride) {
+        // lane i decides for tile t0 + i * stride: it or one of its neighbours still active (the
+        // nine flags of 64 tiles loaded at once)
         bool act = false;
-        if (lane < 9) {
-            const int nx = tx + lane % 3 - 1, ny = ty + lane / 3 - 1;
-            act = nx >= 0 && nx < tiles_x && ny >= 0 && ny < tiles_y && td[ny * tiles_x + nx] == 0;
+        {
+            const int tl = t0 + lane * stride;
+            if (tl < tiles) {
+                const int tx = tl % tiles_x, ty = tl / tiles_x;
+                unsigned char fl[9];
+#pragma unroll
+                for (int n = 0; n < 9; ++n) {
+                    const int nx = tx + n % 3 - 1, ny = ty + n / 3 - 1;
+                    const bool in = nx >= 0 && nx < tiles_x && ny >= 0 && ny < tiles_y;
+                    fl[n] = td[in ? ny * tiles_x + nx : tl];
+                }
+#pragma unroll
+                for (int n = 0; n < 9; ++n) act |= fl[n] == 0;
+            }
         }
-        if (!__ballot(act)) continue;  // wave-uniform
-        const int x0 = tx * kTileX + (lane & 7) * 4, y = ty * kTileY + (lane >> 3);
-        if (x0 >= d.W || y >= d.H) continue;  // W % 4 == 0: a lane's four pixels are all in or all out
-        int4* p4 = reinterpret_cast<int4*>(comp + (int64_t)y * d.W + x0);
-        const int4 v = *p4;
-        int4 o;
-        o.x = uf_find_ro_halve(uf, v.x);
-        o.y = v.y == v.x ? o.x : uf_find_ro_halve(uf, v.y);
-        o.z = v.z == v.y ? o.y : uf_find_ro_halve(uf, v.z);
-        o.w = v.w == v.z ? o.z : uf_find_ro_halve(uf, v.w);
-        if (o.x != v.x || o.y != v.y || o.z != v.z || o.w != v.w) *p4 = o;
+        for (unsigned long long tm = __ballot(act); tm; tm &= tm - 1) {
+            const int t = t0 + (__ffsll((long long)tm) - 1) * stride;
+            const int tx = t % tiles_x, ty = t / tiles_x;
+            const int x0 = tx * kTileX + (lane & 7) * 4, y = ty * kTileY + (lane >> 3);
+            if (x0 >= d.W || y >= d.H) continue;  // W % 4 == 0: a lane's four pixels are all in or all out
+            int4* p4 = reinterpret_cast<int4*>(comp + (int64_t)y * d.W + x0);
+            const int4 v = *p4;
+            int4 o;
+            o.x = uf_find_ro_halve(uf, v.x);
+            o.y = v.y == v.x ? o.x : uf_find_ro_halve(uf, v.y);
+            o.z = v.z == v.y ? o.y : uf_find_ro_halve(uf, v.z);
+            o.w = v.w == v.z ? o.z : uf_find_ro_halve(uf, v.w);
+            if (o.x != v.x || o.y != v.y || o.z != v.z || o.w != v.w) *p4 = o;
+        }
     }
 }
 
