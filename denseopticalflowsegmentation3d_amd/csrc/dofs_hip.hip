@@ -3130,7 +3130,24 @@ struct HipBackend {
         int N;
         __host__ __device__ int operator()(int x) const { return x < N ? 1 : 0; }
     };
+    // a frame holds exactly N leaves, so subtracting N at every frame's last position makes the
+    // batch-wide exclusive sum frame-local (it is 0 at each frame's first): no per-frame rebase pass
+    struct LeafFlag {
+        const int* ord;
+        int64_t n;
+        int N;
+        __host__ __device__ int operator()(int64_t i) const {
+            return (ord[i] < N ? 1 : 0) - ((i + 1) % n == 0 ? N : 0);  // -N at each frame's last
+        }
+    };
     void scan_excl_leaf(const int* ord, int* out, int64_t n, int nf, int64_t N) {
+        if ((int64_t)n * nf < (int64_t)0x7FFFFFFF) {
+            hipcub::CountingInputIterator<int64_t> ci(0);
+            hipcub::TransformInputIterator<int, LeafFlag, hipcub::CountingInputIterator<int64_t>> it(
+                ci, LeafFlag{ord, n, (int)N});
+            scan_excl_it(it, out, n * nf, 1);  // the whole batch, already frame-local
+            return;
+        }
         hipcub::TransformInputIterator<int, IsLeaf, const int*> it(ord, IsLeaf{(int)N});
         scan_excl_it(it, out, n, nf);
     }
