@@ -1652,11 +1652,31 @@ __global__ __launch_bounds__(256) void k_boruvka_recs(Ws w, int r, RecBufs rb) {
     const int* rk = rb.rk + f * d.N;
     const unsigned char* td = rb.td + (int64_t)f * tiles;
     const unsigned short* tc = rb.tc + (int64_t)f * tiles;
-    for (int t0 = blockIdx.x * 4 + wv; t0 < tiles; t0 += 64 * gridDim.x * 4) {
-        for (unsigned long long tm = active_tiles(td, t0, gridDim.x * 4, tiles); tm; tm &= tm - 1) {
-            const int t = t0 + (__ffsll((long long)tm) - 1) * (gridDim.x * 4);
-        const int cnt = tc[t];
-        for (int k = lane; k < cnt; k += 64) {
+    __shared__ int pfx[4][65];  // per wave: record-count prefix over its 64 candidate tiles
+    const int stride = gridDim.x * 4;
+    for (int t0 = blockIdx.x * 4 + wv; t0 < tiles; t0 += 64 * stride) {
+        // the records of 64 grid-stride tiles at once, flattened over the wave's lanes (later rounds
+        // leave a tile few records: one tile per pass would leave most lanes idle behind a chain of
+        // dependent loads); lane i reads tile i's flag and record count
+        const int tl = t0 + lane * stride;
+        const int c = (tl < tiles && td[tl] == 0) ? (int)tc[tl] : 0;
+        int incl = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        const int total = __shfl(incl, 63, 64);
+        if (!total) continue;  // wave-uniform
+        pfx[wv][lane + 1] = incl;
+        if (lane == 0) pfx[wv][0] = 0;
+        lds_wait();
+        for (int rr = lane; rr < total; rr += 64) {
+            int lo = 0, hi = 64;  // pfx[lo] <= rr < pfx[hi]: the record's tile
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (pfx[wv][mid] <= rr) lo = mid; else hi = mid;
+            }
+            const int t = t0 + lo * stride, k = rr - pfx[wv][lo];
             const int64_t px = rec_px(d, tiles_x, t, k);
             const int key = rk[px];
             const unsigned long long wb = rw[px];
@@ -1675,7 +1695,6 @@ __global__ __launch_bounds__(256) void k_boruvka_recs(Ws w, int r, RecBufs rb) {
                 uf_union(w.uf + f * d.N, comp[p], comp[q]);
             }
         }
-    }
     }
 }
 
