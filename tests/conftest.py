@@ -8,6 +8,16 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+def locked_make(directory):
+    """`make -s -C directory` under an exclusive file lock, so pytest-xdist workers that build
+    the same test library at once do not load a half-written .so."""
+    import fcntl
+    import subprocess
+    with open(os.path.join(directory, ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", directory], check=True)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 (MI355X) device and the HIP library")
 
@@ -29,10 +39,9 @@ def gpu():
 @pytest.fixture(scope="session")
 def emu():
     """Sequential host model of the product pipeline (tests/emu, test infrastructure only)."""
-    import subprocess
     from denseopticalflowsegmentation3d_amd.runtime import Dofs
     here = os.path.join(ROOT, "tests", "emu")
-    subprocess.run(["make", "-s", "-C", here], check=True)
+    locked_make(here)
     ctx = Dofs(0, lib=os.path.join(here, "_build", "libdofs_emu.so"))
     yield ctx
     ctx.close()

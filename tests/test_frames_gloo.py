@@ -6,6 +6,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+from conftest import locked_make
 
 from denseopticalflowsegmentation3d_amd.frames import (RECORD_DTYPE, decode_gathered, frame_shard, gather_records,
                                                         records_nbytes)
@@ -100,10 +101,9 @@ EMU = os.path.join(ROOT, "tests", "emu", "_build", "libdofs_emu.so")
 def test_gather_real_pipeline_world2(calib):
     """Each gloo rank segments its frames through the product pipeline (host emulator, same kernel
     bodies) and the gathered box records equal the oracle's snapshots of every frame, in frame order."""
-    import subprocess
     from oracle import binding as ob
     from parity import params
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "emu")], check=True)
+    locked_make(os.path.join(ROOT, "tests", "emu"))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29700 + os.getpid() % 500

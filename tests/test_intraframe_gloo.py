@@ -3,13 +3,13 @@ halo exchange, per-band minimum spanning forests, gather to rank 0 and the maske
 through the test-only host emulator of the product pipeline (tests/emu), and compared with the
 oracle's single-frame result (bit-exact, lifting included)."""
 import os
-import subprocess
 
 import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+from conftest import locked_make
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EMU = os.path.join(ROOT, "tests", "emu", "_build", "libdofs_emu.so")
@@ -45,7 +45,7 @@ def _worker(rank, world, port, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_intraframe_matches_single_frame(world, calib):
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "emu")], check=True)
+    locked_make(os.path.join(ROOT, "tests", "emu"))
     from oracle import binding as ob
     from parity import check_exact, params
     ctx = mp.get_context("spawn")
