@@ -274,6 +274,9 @@ struct LongShared {
     int go;                    // blocked step: 1 = its light child completed (continue), 0 = park
 };
 constexpr unsigned long long kSpinTicks = 5000000ull;  // 50 ms of s_memrealtime (100 MHz)
+#ifndef DOFS_SPIN_SLEEP
+#define DOFS_SPIN_SLEEP 8  // s_sleep units (64 cycles) between polls of a flag another workgroup sets
+#endif
 
 // Resolve position p for wave `wv`. Returns the meta flags (kLongOk when the inputs are ready).
 __device__ inline int long_resolve(const Ws& w, int64_t lb, int p, int top, int round, int wv, ChainRec* cr,
@@ -468,7 +471,7 @@ __device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can
                     rd = __hip_atomic_load(w.ready + lb + lq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (!can_wait || rd <= 2 * round + 1 || rd == kIntMax || rd == kParkBase - round) break;
                     if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) break;
-                    __builtin_amdgcn_s_sleep(8);
+                    __builtin_amdgcn_s_sleep(DOFS_SPIN_SLEEP);
                 }
                 const int go = rd <= 2 * round + 1;
                 sh.go = go;
@@ -689,7 +692,7 @@ __device__ void replay_long_path1(const Ws& w, int f, int jj, int round, bool ca
                     rd = __hip_atomic_load(w.ready + lb + lq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (!can_wait || rd <= 2 * round + 1 || rd == kIntMax || rd == kParkBase - round) break;
                     if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) break;
-                    __builtin_amdgcn_s_sleep(8);
+                    __builtin_amdgcn_s_sleep(DOFS_SPIN_SLEEP);
                 }
                 go = rd <= 2 * round + 1;
                 if (go) {
@@ -2476,7 +2479,7 @@ __global__ __launch_bounds__(kDeepT) void k_krt_fused(Ws w, int* progress) {
         KT_DECL
         if (tid == 0) {
             while (__hip_atomic_load(progress + f * kCounters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k + 1)
-                __builtin_amdgcn_s_sleep(8);
+                __builtin_amdgcn_s_sleep(DOFS_SPIN_SLEEP);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
