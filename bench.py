@@ -234,7 +234,7 @@ def main(argv=None):
 
     from denseopticalflowsegmentation3d_amd import runtime
     from denseopticalflowsegmentation3d_amd.abi import default_params
-    from denseopticalflowsegmentation3d_amd.frames import FrameParallel, frame_shard
+    from denseopticalflowsegmentation3d_amd.frames import FrameParallel, Pipelined, job_plan
 
     if world > 1:
         dist.init_process_group("nccl")
@@ -249,15 +249,14 @@ def main(argv=None):
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     fp = FrameParallel(ctx, world, GATHER_PER_FRAME)
-    lag = ctx.batch_slots() - 1
 
     if a.frames:  # config 4: a fixed job split over the ranks
-        mine = frame_shard(a.frames, rank, world)
-        per_rank = -(-a.frames // world)
+        mine, chunks = job_plan(a.frames, rank, world, a.batch)
         flows = torch.empty((max(len(mine), 1), H, W, 2), dtype=torch.float32, device=dev)
-        if len(mine):
-            runtime.synth_flow_device(flows.data_ptr(), len(mine), H, W, seed0=mine.start, stream=sh)
-        chunks = [(s, min(a.batch, per_rank - s)) for s in range(0, per_rank, a.batch)]
+        # a rank without frames of its own (e.g. F = 9 on 8 GPUs: ceil(9/8) = 2 per rank leaves ranks
+        # 5-7 empty) still runs every chunk, on a placeholder frame (seed F, not counted in `value`)
+        runtime.synth_flow_device(flows.data_ptr(), max(len(mine), 1), H, W,
+                                  seed0=mine.start if len(mine) else a.frames, stream=sh)
         frames_per_step = a.frames
         B = chunks[0][1]
     else:
@@ -267,25 +266,14 @@ def main(argv=None):
         chunks = [(0, B)]
         frames_per_step = world * B
 
-    pending = []
-
-    def submit(s, n, src=None):
-        # ranks with fewer real frames (F not a multiple of N) still run every chunk (the gather is
-        # collective); their padding frames repeat the first frame and are not counted in `value`
-        v = (src if src is not None else flows)
-        n_real = max(1, min(n, v.shape[0] - s))
-        part = v[s:s + n_real] if n_real == n else torch.cat([v[s:s + n_real], v[:n - n_real]])
-        pending.append(fp.submit(part, persp, inv, up, params=prm, stream=sh))
-        if len(pending) > lag:
-            fp.collect(pending.pop(0), stream=sh)
-
-    def flush():
-        while pending:
-            fp.collect(pending.pop(0), stream=sh)
+    # ranks with fewer real frames (F not a multiple of N) still run every chunk with n frames (the gather
+    # is collective and its blocks are equal): padding positions cycle through the rank's own frames
+    # (batch_view) and are not counted in `value`
+    pipe = Pipelined(fp, persp, inv, up, params=prm, stream=sh)
+    flush = pipe.flush
 
     def step(src=None):
-        for s, n in chunks:
-            submit(s, n, src)
+        pipe.run_chunks(src if src is not None else flows, chunks)
         if a.frames:  # one step = the whole job
             flush()
 

@@ -385,14 +385,17 @@ int api_band_msf(Context<Backend>* cx, const F2* d_rows, int row0, int rows, int
     return cx->check();
 }
 
+// Results of frame `frame` of batch id `batch` (one of the last nslots issued; -1 = the last).
 template <class Backend>
-int api_fetch(Context<Backend>* cx, int frame, dofs_result* out) {
+int api_fetch(Context<Backend>* cx, int frame, dofs_result* out, int64_t batch = -1) {
     if (!cx->have_batch() || !out) return cx->fail(DOFS_ERR_INVALID_ARG, "no batch");
-    const int slot = cx->last_slot();
+    if (batch < 0) batch = cx->nbatch - 1;
+    if (!cx->live(batch)) return cx->fail(DOFS_ERR_INVALID_ARG, "batch no longer readable");
+    const int slot = cx->slot_of(batch);
     const typename Context<Backend>::Meta& m = cx->meta[slot];
     if (frame < 0 || frame >= m.B) return cx->fail(DOFS_ERR_INVALID_ARG, "no frame");
     Backend& be = cx->be;
-    cx->join(cx->nbatch - 1);
+    cx->join(batch);
     const Ws& w = cx->pipe(slot).w;
     const Dims& d = w.d;
     int ctr[kCounters];
@@ -475,6 +478,25 @@ int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity
     return cx->check();
 }
 
+// The single-frame calls (dofs_segment, dofs_segment_graph) return every history slot: when the
+// frame has more than the context's snapshot capacity, `rerun` runs it again with a capacity grown
+// for this call only; the context's capacity (the batch API's, dofs_set_snapshot_capacity) is restored
+// afterwards, so the next batch on that workspace re-lays it out at the caller's size.
+template <class Backend, class Rerun>
+int fetch_grown(Context<Backend>* cx, dofs_result* out, Rerun rerun) {
+    int n = 0;
+    cx->join(cx->nbatch - 1);
+    cx->be.d2h(&n, cx->pipe(cx->last_slot()).w.ctr + C_SNAP, sizeof(int));
+    cx->be.sync();
+    if (n <= cx->snap_cap) return api_fetch(cx, 0, out);
+    const int64_t keep = cx->snap_cap;
+    while (cx->snap_cap < n) cx->snap_cap *= 2;
+    int rc = rerun();
+    if (!rc) rc = api_fetch(cx, 0, out);
+    cx->snap_cap = keep;
+    return rc;
+}
+
 template <class Backend>
 int api_segment(Context<Backend>* cx, const float* flow, int H, int W, size_t stride, const float persp[9],
                 const float inv[9], const float inv_upper[27], const dofs_params* params, dofs_result* out) {
@@ -497,16 +519,11 @@ int api_segment(Context<Backend>* cx, const float* flow, int H, int W, size_t st
     }
     int rc = api_run(cx, (const F2*)cx->d_in, (int64_t)H * W, 1, H, W, persp, inv, inv_upper, params);
     if (rc) return rc;
-    int n = 0;  // more history slots than the device snapshot capacity: grow it and run again
-    cx->join(cx->nbatch - 1);
-    cx->be.d2h(&n, cx->pipe(cx->last_slot()).w.ctr + C_SNAP, sizeof(int));
-    cx->be.sync();
-    if (n > cx->snap_cap) {
-        while (cx->snap_cap < n) cx->snap_cap *= 2;
-        rc = api_run(cx, (const F2*)cx->d_in, (int64_t)H * W, 1, H, W, persp, inv, inv_upper, params);
-        if (rc) return rc;
-    }
-    return api_fetch(cx, 0, out);
+    // more history slots than the device snapshot capacity: run again with a capacity grown for this
+    // call only (the batch API's capacity stays the one dofs_set_snapshot_capacity chose)
+    return fetch_grown(cx, out, [&]() {
+        return api_run(cx, (const F2*)cx->d_in, (int64_t)H * W, 1, H, W, persp, inv, inv_upper, params);
+    });
 }
 
 // Upload a host flow field (row stride in bytes, 0 = packed) into the context's input buffer.
@@ -590,16 +607,9 @@ int api_segment_graph(Context<Backend>* cx, const float* flow, int H, int W, siz
     int* acc = (int*)(g + eb);
     int rc = api_run(cx, (const F2*)cx->d_in, N, 1, H, W, persp, inv, inv_upper, params, nullptr, de, E, acc);
     if (rc) return rc;
-    int n = 0;  // more history slots than the device snapshot capacity: grow it and run again
-    cx->join(cx->nbatch - 1);
-    cx->be.d2h(&n, cx->pipe(cx->last_slot()).w.ctr + C_SNAP, sizeof(int));
-    cx->be.sync();
-    if (n > cx->snap_cap) {
-        while (cx->snap_cap < n) cx->snap_cap *= 2;
-        rc = api_run(cx, (const F2*)cx->d_in, N, 1, H, W, persp, inv, inv_upper, params, nullptr, de, E, acc);
-        if (rc) return rc;
-    }
-    return api_fetch(cx, 0, out);
+    return fetch_grown(cx, out, [&]() {
+        return api_run(cx, (const F2*)cx->d_in, N, 1, H, W, persp, inv, inv_upper, params, nullptr, de, E, acc);
+    });
 }
 
 // Snapshot records beyond the per-frame capacity are not written (labels stay exact: KPaint works
@@ -615,20 +625,25 @@ int check_overflow(Context<Backend>* cx, int64_t batch) {
     return cx->check();
 }
 
+// The first per_frame records of every frame are the first per_frame of its snapshots (slot order):
+// KSnapshot writes the first snap_cap of them whatever the count, so with per_frame <= snap_cap every
+// copied record exists and the copy needs no host wait — the counts say when a frame had more. A
+// per_frame above the workspace's capacity is refused whatever the data (DOFS_ERR_CAPACITY), so ranks
+// of one configuration all copy or all fail: a frame-parallel gather never sees one rank drop out.
 template <class Backend>
 int api_records_copy(Context<Backend>* cx, int64_t batch, void* dst, int per_frame, void* stream) {
     if (!cx->live(batch) || !dst || per_frame < 0) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
     const int slot = cx->slot_of(batch);
     const Ws& w = cx->pipe(slot).w;
     const int B = cx->meta[slot].B;
-    const int k = per_frame < w.snap_cap ? per_frame : w.snap_cap;
-    if (int rc = check_overflow(cx, batch)) return rc;
+    if (per_frame > w.snap_cap)
+        return cx->fail(DOFS_ERR_CAPACITY, "per_frame exceeds the snapshot capacity (dofs_set_snapshot_capacity)");
     cx->be.set_stream(stream);
     cx->join(batch);
     cx->be.copy2d(dst, sizeof(int), w.ctr + C_SNAP, sizeof(int) * kCounters, sizeof(int), B);
-    if (k > 0)
+    if (per_frame > 0)
         cx->be.copy2d((char*)dst + sizeof(int) * B, sizeof(dofs_box_record) * per_frame, w.recs,
-                      sizeof(dofs_box_record) * w.snap_cap, sizeof(dofs_box_record) * k, B);
+                      sizeof(dofs_box_record) * w.snap_cap, sizeof(dofs_box_record) * per_frame, B);
     return cx->check();
 }
 

@@ -104,6 +104,12 @@ int32_t dofs_batch_fetch(dofs_ctx* ctx, int32_t frame, dofs_result* out) {
     return dofs::api_fetch(ctx, frame, out);
 }
 
+int32_t dofs_batch_fetch_id(dofs_ctx* ctx, int64_t batch, int32_t frame, dofs_result* out) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    ctx->be.use_own();
+    return dofs::api_fetch(ctx, frame, out, batch);
+}
+
 int32_t dofs_batch_records_device(dofs_ctx* ctx, void** d_records, void** d_counts, int32_t* capacity) {
     if (!ctx || !ctx->have_batch()) return DOFS_ERR_INVALID_ARG;
     ctx->be.event_sync(ctx->evDone[ctx->last_slot()]);  // the pointers are read after the batch ended

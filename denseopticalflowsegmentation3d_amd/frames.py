@@ -23,6 +23,32 @@ def frame_shard(total: int, rank: int, world: int) -> range:
     return range(lo, min(total, lo + per))
 
 
+def job_plan(total: int, rank: int, world: int, batch: int) -> tuple[range, list[tuple[int, int]]]:
+    """A fixed job of `total` frames over `world` ranks (BASELINE config 4): this rank's frames and the
+    chunks (start, n) every rank runs — ceil(total / world) frame positions in batches of at most `batch`,
+    the same on every rank, so each collective gather moves equal blocks. A rank with fewer real frames
+    fills its positions by cycling its own frames (`batch_view`); those are not counted as work."""
+    if total < 1 or world < 1 or batch < 1 or not 0 <= rank < world:
+        raise ValueError("job_plan: total, world and batch must be >= 1 and 0 <= rank < world")
+    per_rank = -(-total // world)
+    return frame_shard(total, rank, world), [(s, min(batch, per_rank - s)) for s in range(0, per_rank, batch)]
+
+
+def batch_view(flows: torch.Tensor, start: int, n: int) -> torch.Tensor:
+    """Frames [start, start + n) of a rank's resident frames, positions past the last one cycling through
+    its frames (a rank without frames of its own holds one placeholder frame). Always n frames."""
+    L = flows.shape[0]
+    if L < 1:
+        raise ValueError("batch_view: a rank needs at least one (placeholder) frame")
+    if start + n <= L:
+        part = flows[start:start + n]
+    else:
+        ids = torch.arange(start, start + n, device=flows.device)
+        part = flows[torch.where(ids < L, ids, ids % L)]
+    assert part.shape[0] == n
+    return part
+
+
 def records_nbytes(frames: int, per_frame: int) -> int:
     """Layout written by dofs_batch_records_copy: int32 counts[frames], then frames × per_frame records."""
     return 4 * frames + frames * per_frame * RECORD_DTYPE.itemsize
@@ -90,3 +116,38 @@ class FrameParallel:
 
     def step(self, flows: torch.Tensor, persp, inv, inv_upper, params=None, stream: int | None = None):
         return self.collect(self.submit(flows, persp, inv, inv_upper, params, stream), stream)
+
+
+class Pipelined:
+    """The caller's side of the two-stage batch pipeline (bench.py's timed loop and config 4's job): each
+    batch is submitted, and batch k's records are gathered right after batch k + slots - 1 is submitted,
+    so batch k's replay stage overlaps the graph stage of the batches after it. `sink(bid, gathered)`,
+    if given, sees every gathered block (a device tensor reused by the next gather: copy what you keep)
+    while the batch's results are still readable on the context."""
+
+    def __init__(self, fp: FrameParallel, persp, inv, inv_upper, params=None, stream: int | None = None, sink=None):
+        self.fp, self.args, self.params, self.stream, self.sink = fp, (persp, inv, inv_upper), params, stream, sink
+        slots = fp.ctx.batch_slots() if hasattr(fp.ctx, "batch_slots") else 2
+        self.lag = slots - 1
+        self.pending: list[int] = []
+
+    def _collect(self):
+        bid = self.pending.pop(0)
+        g = self.fp.collect(bid, stream=self.stream)
+        if self.sink is not None:
+            self.sink(bid, g)
+
+    def submit(self, flows: torch.Tensor) -> int:
+        bid = self.fp.submit(flows, *self.args, params=self.params, stream=self.stream)
+        self.pending.append(bid)
+        if len(self.pending) > self.lag:
+            self._collect()
+        return bid
+
+    def flush(self):
+        while self.pending:
+            self._collect()
+
+    def run_chunks(self, flows: torch.Tensor, chunks) -> list[int]:
+        """Submit every chunk (start, n) of this rank's resident frames (batch_view); returns the batch ids."""
+        return [self.submit(batch_view(flows, s, n)) for s, n in chunks]

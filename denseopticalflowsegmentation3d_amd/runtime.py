@@ -70,6 +70,9 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_segment_masked_device.restype = C.c_int32
     L.dofs_batch_fetch.argtypes = [C.c_void_p, C.c_int32, C.POINTER(DofsResult)]
     L.dofs_batch_fetch.restype = C.c_int32
+    if hasattr(L, "dofs_batch_fetch_id"):
+        L.dofs_batch_fetch_id.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.POINTER(DofsResult)]
+        L.dofs_batch_fetch_id.restype = C.c_int32
     L.dofs_batch_records_device.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _ip]
     L.dofs_batch_records_device.restype = C.c_int32
     L.dofs_batch_records_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
@@ -306,10 +309,14 @@ class Dofs:
         self._last_merges = None
         return int(self.lib.dofs_batch_count(self.ctx)) - 1
 
-    def fetch(self, frame: int, capacity: int = 65536, want_blur: bool = True) -> FrameResult:
+    def fetch(self, frame: int, capacity: int = 65536, want_blur: bool = True, batch: int | None = None) -> FrameResult:
+        """Results of `frame` of the last batch, or of batch id `batch` (one of the last batch_slots())."""
         H, W = self._last_hw
         r, snaps, labels, leaf, blurred = self._result(H, W, capacity, want_blur)
-        self._err(self.lib.dofs_batch_fetch(self.ctx, frame, C.byref(r)), "dofs_batch_fetch")
+        if batch is None:
+            self._err(self.lib.dofs_batch_fetch(self.ctx, frame, C.byref(r)), "dofs_batch_fetch")
+        else:
+            self._err(self.lib.dofs_batch_fetch_id(self.ctx, batch, frame, C.byref(r)), "dofs_batch_fetch_id")
         return FrameResult(H, W, snaps[:r.n_snapshots].copy(), labels, leaf, blurred, self._stats(r))
 
     def records_device(self):
@@ -321,7 +328,7 @@ class Dofs:
 
     def records_copy(self, d_dst: int, per_frame: int, stream: int | None = None, batch: int | None = None) -> None:
         """int32 counts[B] then B × per_frame DofsBoxRecord into a device buffer (stream-ordered), of the
-        last batch or of batch id `batch` (one of the last two)."""
+        last batch or of batch id `batch` (one of the last batch_slots())."""
         if batch is None:
             rc = self.lib.dofs_batch_records_copy(self.ctx, C.c_void_p(d_dst), per_frame, C.c_void_p(stream or 0))
         else:

@@ -203,6 +203,8 @@ int32_t dofs_segment_batch_device(dofs_ctx* ctx, const float* d_flow, int32_t B,
                                   const float persp[9], const float inv[9], const float inv_upper[27],
                                   const dofs_params* params, void* stream);
 int32_t dofs_batch_fetch(dofs_ctx* ctx, int32_t frame, dofs_result* out);
+/* dofs_batch_fetch for batch id `batch` (one of the last dofs_batch_slots() issued). Waits for it. */
+int32_t dofs_batch_fetch_id(dofs_ctx* ctx, int64_t batch, int32_t frame, dofs_result* out);
 
 /* Intra-frame sharding of the MST stage (BASELINE config 5: one large frame split
  * into row bands across GPUs). The global MST (graph.cpp:519-531 accepts exactly it) is contained in
@@ -230,10 +232,12 @@ int32_t dofs_segment_masked_device(dofs_ctx* ctx, const float* d_flow, int32_t H
 int32_t dofs_batch_records_device(dofs_ctx* ctx, void** d_records, void** d_counts, int32_t* capacity);
 
 /* Copy the batch's box records to a caller device buffer on `stream`: int32 counts[B] (snapshots per
- * frame), then B × per_frame dofs_box_record (the first per_frame records of each frame).
- * Capacity: each frame keeps at most dofs_snapshot_capacity() records (default 4096). Waits on the
- * host for the batch to finish, then returns DOFS_ERR_CAPACITY (copying nothing) if any frame's
- * snapshot count exceeded it — records are never dropped silently. The labels are exact either way. */
+ * frame, the full count), then B × per_frame dofs_box_record (the first per_frame records of each
+ * frame, slot order; entries past a frame's count have slot == -1). A frame with count > per_frame
+ * was truncated by the caller's per_frame, which the counts show. Each frame keeps its first
+ * dofs_snapshot_capacity() records (default 4096), so per_frame must not exceed that capacity:
+ * DOFS_ERR_CAPACITY (nothing copied) otherwise, whatever the data — ranks of one configuration
+ * therefore all copy or all fail. Never waits on the host. The labels are exact in every case. */
 int32_t dofs_batch_records_copy(dofs_ctx* ctx, void* d_dst, int32_t per_frame, void* stream);
 /* Same for batch id `batch` (one of the last three issued); ordered after that batch on `stream`. */
 int32_t dofs_batch_records_copy_id(dofs_ctx* ctx, int64_t batch, void* d_dst, int32_t per_frame,

@@ -54,6 +54,10 @@ def lib(opt: str = "O2") -> C.CDLL:
     L.oracle_segment_graph.argtypes = [fp, C.c_int32, C.c_int32, ip, ip, dp, C.c_int64, fp, fp, fp,
                                        C.POINTER(DofsParams), C.c_int32, C.POINTER(DofsResult), C.POINTER(DofsEvent)]
     L.oracle_segment_graph.restype = C.c_int32
+    L.oracle_segment_ex.argtypes = [fp, C.c_int32, C.c_int32, ip, ip, dp, C.c_int64, fp, fp, fp,
+                                    C.POINTER(DofsParams), C.c_int32, C.POINTER(DofsResult), C.POINTER(DofsEvent), dp,
+                                    ip]
+    L.oracle_segment_ex.restype = C.c_int32
     _LIBS[name] = L
     return L
 
@@ -137,7 +141,7 @@ def synth_flow(H: int, W: int, seed: int = 0) -> np.ndarray:
 
 
 class OracleResult:
-    def __init__(self, H, W, snaps, labels, leaf_order, blurred, stats, events):
+    def __init__(self, H, W, snaps, labels, leaf_order, blurred, stats, events, scores=None, boxes=None):
         self.H, self.W = H, W
         self.snapshots = snaps
         self.labels = labels
@@ -145,74 +149,67 @@ class OracleResult:
         self.blurred = blurred
         self.stats = stats
         self.events = events
+        self.scores = scores  # Forest::segment_scores (N doubles, graph.cpp:326) when forest=True
+        self.boxes = boxes    # Forest::bboxes after the run (N x 4, -1 rows = empty, graph.cpp:208)
 
     def members(self, snap) -> np.ndarray:
         return np.sort(self.leaf_order[snap["seg_begin"]:snap["seg_begin"] + snap["size"]])
 
 
-def segment(flow: np.ndarray, persp, inv, inv_upper, params: DofsParams | None = None, mode: int = 0,
-            events: bool = False, opt: str = "O2") -> OracleResult:
-    """get_segmented_array restated on the CPU (mode 0 fast, 1 faithful, 2 faithful + self-check)."""
+def _run(flow, edges, persp, inv, inv_upper, params, mode, events, forest, opt):
     flow = _f(flow)
     H, W = flow.shape[:2]
     N = H * W
     if params is None:
         params = default_params()
+    if edges is None:
+        s = e = w = None
+        E = -1
+    else:
+        s = np.ascontiguousarray(edges[0], np.int32)
+        e = np.ascontiguousarray(edges[1], np.int32)
+        w = np.ascontiguousarray(edges[2], np.float64)
+        E = len(s)
     cap = max(N, 1)
     snaps = np.zeros(cap, dtype=DofsSnapshot.np_dtype())
     labels = np.zeros(N, np.int32)
     leaf = np.zeros(N, np.int32)
     blurred = np.zeros((H, W, 2), np.float32)
     ev = np.zeros(max(N - 1, 1), dtype=DofsEvent.np_dtype()) if events else None
+    scores = np.zeros(N, np.float64) if forest else None
+    boxes = np.zeros((N, 4), np.int32) if forest else None
     res = DofsResult()
     res.snapshots = snaps.ctypes.data_as(C.POINTER(DofsSnapshot))
     res.snapshot_capacity = cap
     res.labels = _ptr(labels, C.c_int32)
     res.leaf_order = _ptr(leaf, C.c_int32)
     res.blurred = _ptr(blurred, C.c_float)
-    rc = lib(opt).oracle_segment(_ptr(flow, C.c_float), H, W, _ptr(_f(persp), C.c_float), _ptr(_f(inv), C.c_float),
-                                 _ptr(_f(inv_upper), C.c_float), C.byref(params), mode, C.byref(res),
-                                 ev.ctypes.data_as(C.POINTER(DofsEvent)) if events else None)
+    ip = (lambda a: _ptr(a, C.c_int32) if a is not None else None)
+    rc = lib(opt).oracle_segment_ex(_ptr(flow, C.c_float), H, W, ip(s), ip(e), _ptr(w, C.c_double) if w is not None else None,
+                                    C.c_int64(E), _ptr(_f(persp), C.c_float), _ptr(_f(inv), C.c_float),
+                                    _ptr(_f(inv_upper), C.c_float), C.byref(params), mode, C.byref(res),
+                                    ev.ctypes.data_as(C.POINTER(DofsEvent)) if events else None,
+                                    _ptr(scores, C.c_double) if forest else None, ip(boxes))
     if rc != 0:
         raise RuntimeError(f"oracle_segment failed with status {rc}")
     st = {k: getattr(res.stats, k) for k, _ in res.stats._fields_}
+    n_ev = max(N - 1, 0) if edges is None else int(res.stats.n_merges)
     return OracleResult(H, W, snaps[:res.n_snapshots].copy(), labels, leaf, blurred, st,
-                        ev[:max(N - 1, 0)] if events else None)
+                        ev[:n_ev] if events else None, scores, boxes)
+
+
+def segment(flow: np.ndarray, persp, inv, inv_upper, params: DofsParams | None = None, mode: int = 0,
+            events: bool = False, opt: str = "O2", forest: bool = False) -> OracleResult:
+    """get_segmented_array restated on the CPU (mode 0 fast, 1 faithful, 2 faithful + self-check).
+    forest=True also returns the Forest's segment_scores and final bboxes (.scores, .boxes)."""
+    return _run(flow, None, persp, inv, inv_upper, params, mode, events, forest, opt)
 
 
 def segment_graph(flow: np.ndarray, start, end, weight, persp, inv, inv_upper, params: DofsParams | None = None,
-                  mode: int = 0, events: bool = False) -> OracleResult:
+                  mode: int = 0, events: bool = False, forest: bool = False) -> OracleResult:
     """segment_graph(flow, edges, ...) restated on the CPU: Kruskal over the given edge list in order, on the
     flow as given (no blur)."""
-    flow = _f(flow)
-    H, W = flow.shape[:2]
-    N = H * W
-    if params is None:
-        params = default_params()
-    s = np.ascontiguousarray(start, np.int32)
-    e = np.ascontiguousarray(end, np.int32)
-    w = np.ascontiguousarray(weight, np.float64)
-    cap = max(N, 1)
-    snaps = np.zeros(cap, dtype=DofsSnapshot.np_dtype())
-    labels = np.zeros(N, np.int32)
-    leaf = np.zeros(N, np.int32)
-    blurred = np.zeros((H, W, 2), np.float32)
-    ev = np.zeros(max(N - 1, 1), dtype=DofsEvent.np_dtype()) if events else None
-    res = DofsResult()
-    res.snapshots = snaps.ctypes.data_as(C.POINTER(DofsSnapshot))
-    res.snapshot_capacity = cap
-    res.labels = _ptr(labels, C.c_int32)
-    res.leaf_order = _ptr(leaf, C.c_int32)
-    res.blurred = _ptr(blurred, C.c_float)
-    rc = lib().oracle_segment_graph(_ptr(flow, C.c_float), H, W, _ptr(s, C.c_int32), _ptr(e, C.c_int32),
-                                    _ptr(w, C.c_double), C.c_int64(len(s)), _ptr(_f(persp), C.c_float),
-                                    _ptr(_f(inv), C.c_float), _ptr(_f(inv_upper), C.c_float), C.byref(params), mode,
-                                    C.byref(res), ev.ctypes.data_as(C.POINTER(DofsEvent)) if events else None)
-    if rc != 0:
-        raise RuntimeError(f"oracle_segment_graph failed with status {rc}")
-    st = {k: getattr(res.stats, k) for k, _ in res.stats._fields_}
-    return OracleResult(H, W, snaps[:res.n_snapshots].copy(), labels, leaf, blurred, st,
-                        ev[:int(res.stats.n_merges)] if events else None)
+    return _run(flow, (start, end, weight), persp, inv, inv_upper, params, mode, events, forest, "O2")
 
 
 # ---- Farneback dense optical flow (SURVEY.md §8(f) #1; oracle/farneback.cpp) ----------------------

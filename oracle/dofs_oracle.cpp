@@ -447,7 +447,10 @@ struct Slot {
 };
 
 // Shared per-merge scoring of new_merge (graph.cpp:280-356). Returns true when the slot improved.
-bool score_merge(Ctx& cx, int root, int size, float mx, float my, const int bbox[4], Slot& slot, int event) {
+// last_score (optional) is Forest::segment_scores[root]: written for every scored candidate, before the
+// convexity and threshold tests (graph.cpp:326), so it ends as the root's last scored score.
+bool score_merge(Ctx& cx, int root, int size, float mx, float my, const int bbox[4], Slot& slot, int event,
+                 double* last_score) {
     if (size < cx.prm->min_size) return false;  // :280
     int y = root / cx.W;
     if (y < cx.H / 10) return false;  // :286-292
@@ -460,6 +463,7 @@ bool score_merge(Ctx& cx, int root, int size, float mx, float my, const int bbox
     double score = get_score(bbox, mx, my, cx.persp, cx.inv, cx.inv_upper, cx.prm->obj_size, &sol);  // :312
     if (score == -1) return false;  // :318
     cx.st.n_scored++;
+    if (last_score) *last_score = score;  // :326
     double min_convexity = 1.0 / 2.0;
     if (sol.cls == 0) min_convexity = cx.prm->min_convexity[0];  // :328-339
     if (sol.cls == 1) min_convexity = cx.prm->min_convexity[1];
@@ -545,8 +549,15 @@ void fill_snapshot(dofs_snapshot* s, int slot, const Slot& sl, int seg_begin) {
 
 // --- fast mode ------------------------------------------------------------------------------
 // given: segment_graph on a caller's edge list (graph.cpp:503-536), else build_graph's (graph.cpp:51-103)
+// Optional Forest state after the run: scores = segment_scores (N, graph.cpp:139,326), boxes = bboxes
+// (N x 4; {-1,-1,-1,-1} where merge cleared it, graph.cpp:208 — every node but the final roots).
+struct Extras {
+    double* scores = nullptr;
+    int32_t* boxes = nullptr;
+};
+
 int segment_fast(Ctx& cx, const float* blurred, std::vector<Slot>& hist, Krt& krt, std::vector<dofs_event>* ev,
-                 const std::vector<Edge>* given = nullptr) {
+                 const std::vector<Edge>* given, const Extras& x) {
     const int W = cx.W, H = cx.H, N = W * H;
     bool nbr8 = (cx.prm->neighbor == 8);
     std::vector<Edge> built;
@@ -574,6 +585,7 @@ int segment_fast(Ctx& cx, const float* blurred, std::vector<Slot>& hist, Krt& kr
     };
     krt.init(N);
     hist.assign(N, Slot());
+    if (x.scores) std::fill(x.scores, x.scores + N, 0.0);  // segment_scores.resize(N), graph.cpp:139
     int event = 0;
     for (const Edge& e : edges) {
         int a = find(e.start), b = find(e.end);
@@ -607,9 +619,12 @@ int segment_fast(Ctx& cx, const float* blurred, std::vector<Slot>& hist, Krt& kr
             r.mean[1] = fy[pb];
         }
         int box[4] = {bb[pb][0], bb[pb][1], bb[pb][2], bb[pb][3]};
-        score_merge(cx, pb, size[pb], fx[pb], fy[pb], box, hist[pb], event);
+        score_merge(cx, pb, size[pb], fx[pb], fy[pb], box, hist[pb], event, x.scores ? x.scores + pb : nullptr);
         ++event;
     }
+    if (x.boxes)
+        for (int i = 0; i < N; ++i)
+            for (int k = 0; k < 4; ++k) x.boxes[4 * (size_t)i + k] = parent[i] == i ? bb[i][k] : -1;
     return event;
 }
 
@@ -626,7 +641,7 @@ struct FSegmentData {  // graph.hpp:48-57
 };
 
 int segment_faithful(Ctx& cx, const float* blurred, std::vector<Slot>& hist, Krt& krt, std::vector<dofs_event>* ev,
-                     std::vector<std::set<int>>* snap_sets, const std::vector<Edge>* given = nullptr) {
+                     std::vector<std::set<int>>* snap_sets, const std::vector<Edge>* given, const Extras& x) {
     const int W = cx.W, H = cx.H, N = W * H;
     bool nbr8 = (cx.prm->neighbor == 8);
     std::vector<Edge> built;
@@ -696,13 +711,21 @@ int segment_faithful(Ctx& cx, const float* blurred, std::vector<Slot>& hist, Krt
         // new_merge scoring, graph.cpp:280-356 (bbox copy as in get_bounding_box, :446-452)
         std::vector<std::pair<int, int>> bbox = bboxes[pb];
         int box[4] = {bbox[0].first, bbox[0].second, bbox[1].first, bbox[1].second};
-        if (score_merge(cx, pb, nodes[pb].size, nodes[pb].fx, nodes[pb].fy, box, hist[pb], event)) {
-            segment_scores[pb] = hist[pb].score;
+        if (score_merge(cx, pb, nodes[pb].size, nodes[pb].fx, nodes[pb].fy, box, hist[pb], event, &segment_scores[pb])) {
             // SegmentData(score, seg, solution, move) — copies the member set, graph.cpp:354
             segment_history[pb] = FSegmentData{hist[pb].score, segments[pb], hist[pb].sol, hist[pb].move};
         }
         ++event;
     }
+    if (x.scores) std::memcpy(x.scores, segment_scores.data(), sizeof(double) * (size_t)N);
+    if (x.boxes)
+        for (int i = 0; i < N; ++i) {
+            const bool has = !bboxes[i].empty();  // Forest::get_bounding_box(i), graph.cpp:446-452
+            x.boxes[4 * (size_t)i + 0] = has ? bboxes[i][0].first : -1;
+            x.boxes[4 * (size_t)i + 1] = has ? bboxes[i][0].second : -1;
+            x.boxes[4 * (size_t)i + 2] = has ? bboxes[i][1].first : -1;
+            x.boxes[4 * (size_t)i + 3] = has ? bboxes[i][1].second : -1;
+        }
     if (snap_sets) {
         snap_sets->assign((size_t)N, std::set<int>());
         for (int i = 0; i < N; ++i)
@@ -827,7 +850,7 @@ void oracle_synth_flow(float* out, int32_t H, int32_t W, uint64_t seed) {
 // events (optional) must hold H*W-1 records. Returns DOFS_OK or an error code.
 static int32_t segment_common(const float* flow_uv, int32_t H, int32_t W, const float persp[9], const float inv[9],
                               const float inv_upper[27], const dofs_params* params, int32_t mode, dofs_result* out,
-                              dofs_event* events, const std::vector<Edge>* given);
+                              dofs_event* events, const std::vector<Edge>* given, const Extras& x = Extras());
 
 int32_t oracle_segment(const float* flow_uv, int32_t H, int32_t W, const float persp[9], const float inv[9],
                        const float inv_upper[27], const dofs_params* params, int32_t mode, dofs_result* out,
@@ -852,9 +875,30 @@ int32_t oracle_segment_graph(const float* flow_uv, int32_t H, int32_t W, const i
     return segment_common(flow_uv, H, W, persp, inv, inv_upper, params, mode, out, events, &edges);
 }
 
+// Either form (E < 0: get_segmented_array; else segment_graph on the list) plus the Forest state after
+// the run: scores[N] = Forest::get_segment_best_score(id) (graph.cpp:386-389), boxes[N x 4] =
+// Forest::get_bounding_box(id) (graph.cpp:446-452; {-1,-1,-1,-1} = the empty vector). Either may be NULL.
+int32_t oracle_segment_ex(const float* flow_uv, int32_t H, int32_t W, const int32_t* start, const int32_t* end,
+                          const double* weight, int64_t E, const float persp[9], const float inv[9],
+                          const float inv_upper[27], const dofs_params* params, int32_t mode, dofs_result* out,
+                          dofs_event* events, double* scores, int32_t* boxes) {
+    Extras x;
+    x.scores = scores;
+    x.boxes = boxes;
+    if (E < 0) return segment_common(flow_uv, H, W, persp, inv, inv_upper, params, mode, out, events, nullptr, x);
+    const int64_t N = (int64_t)H * W;
+    if (E > 0 && (!start || !end || !weight)) return DOFS_ERR_INVALID_ARG;
+    std::vector<Edge> edges((size_t)E);
+    for (int64_t i = 0; i < E; ++i) {
+        if (start[i] < 0 || start[i] >= N || end[i] < 0 || end[i] >= N) return DOFS_ERR_INVALID_ARG;
+        edges[(size_t)i] = Edge{start[i], end[i], weight[i]};
+    }
+    return segment_common(flow_uv, H, W, persp, inv, inv_upper, params, mode, out, events, &edges, x);
+}
+
 static int32_t segment_common(const float* flow_uv, int32_t H, int32_t W, const float persp[9], const float inv[9],
                               const float inv_upper[27], const dofs_params* params, int32_t mode, dofs_result* out,
-                              dofs_event* events, const std::vector<Edge>* given) {
+                              dofs_event* events, const std::vector<Edge>* given, const Extras& x) {
     if (H <= 0 || W <= 0 || !flow_uv || !out) return DOFS_ERR_INVALID_ARG;
     dofs_params prm;
     if (params)
@@ -875,10 +919,10 @@ static int32_t segment_common(const float* flow_uv, int32_t H, int32_t W, const 
     std::vector<std::set<int>> sets;
     int merges;
     if (mode == 0)
-        merges = segment_fast(cx, blurred.data(), hist, krt, events ? &ev : nullptr, given);
+        merges = segment_fast(cx, blurred.data(), hist, krt, events ? &ev : nullptr, given, x);
     else
         merges = segment_faithful(cx, blurred.data(), hist, krt, events ? &ev : nullptr, mode == 2 ? &sets : nullptr,
-                                  given);
+                                  given, x);
     cx.st.n_merges = merges;
     std::vector<int> leaf_order, first;
     krt.order(leaf_order, first);

@@ -1,4 +1,4 @@
-"""Snapshot-record capacity of the batch API: an overflow is reported (DOFS_ERR_CAPACITY from
+"""Snapshot-record capacity of the batch API: an overflow is reported (the full counts from
 dofs_batch_records_copy, dofs_batch_fetch and the overlay), never dropped silently, and the labels stay
 exact (KPaint works per history slot, not per stored record). Run on the host emulator of the product
 pipeline (CPU) and on the GPU."""
@@ -7,6 +7,7 @@ import ctypes as C
 import numpy as np
 import pytest
 
+from denseopticalflowsegmentation3d_amd.frames import RECORD_DTYPE
 from oracle import binding as ob
 from parity import params
 
@@ -29,8 +30,18 @@ def _check(ctx, calib, dev_alloc, dev_ptr, to_host):
     try:
         bid = _run(ctx, flows, calib, prm, dev_ptr)
         blk = dev_alloc(np.zeros(4 * B + B * 4 * 88, np.uint8))
+        # more records per frame than the workspace keeps: refused whatever the data (all ranks alike)
         with pytest.raises(RuntimeError, match=r"\(4\)"):
             ctx.records_copy(dev_ptr(blk), 4, stream=0, batch=bid)
+        # up to the capacity: the first records of every frame exist, the counts show the truncation
+        ctx.records_copy(dev_ptr(blk), CAP, stream=0, batch=bid)
+        h = to_host(blk)
+        counts = h[:4 * B].view(np.int32)
+        assert list(counts) == [len(o.snapshots) for o in oracle]
+        recs = h[4 * B:4 * B + B * CAP * 88].view(RECORD_DTYPE).reshape(B, CAP)
+        for f in range(B):
+            assert list(recs[f]["slot"]) == list(oracle[f].snapshots["slot"][:CAP])
+            assert list(recs[f]["size"]) == list(oracle[f].snapshots["size"][:CAP])
         for f in range(B):
             r, snaps, labels, leaf, _ = ctx._result(H, W, 64, want_blur=False)
             rc = ctx.lib.dofs_batch_fetch(ctx.ctx, f, C.byref(r))
