@@ -7,6 +7,7 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -423,6 +424,77 @@ int api_fetch(Context<Backend>* cx, int frame, dofs_result* out, int64_t batch =
     return cx->check();
 }
 
+// Forest::get_segment_best_score for every id (graph.cpp:386-389) of frame `frame` of batch id `batch`.
+template <class Backend>
+int api_segment_scores(Context<Backend>* cx, int64_t batch, int frame, double* out, int64_t capacity) {
+    if (!cx->have_batch() || !out) return cx->fail(DOFS_ERR_INVALID_ARG, "no batch");
+    if (batch < 0) batch = cx->nbatch - 1;
+    if (!cx->live(batch)) return cx->fail(DOFS_ERR_INVALID_ARG, "batch no longer readable");
+    const int slot = cx->slot_of(batch);
+    if (frame < 0 || frame >= cx->meta[slot].B) return cx->fail(DOFS_ERR_INVALID_ARG, "no frame");
+    Pipeline<Backend>& P = cx->pipe(slot);
+    const int64_t N = P.w.d.N;
+    if (capacity < N) return cx->fail(DOFS_ERR_CAPACITY, "score capacity (H*W doubles)");
+    double* d = (double*)cx->scratch(sizeof(double) * (size_t)N);
+    if (!d) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    Backend& be = cx->be;
+    cx->join(batch);
+    if (P.w.d.M <= 0 || !P.pre)
+        be.memset(d, 0, sizeof(double) * (size_t)N);
+    else
+        be.launch(1, N, KSegScores{P.w, P.pre, frame, d});
+    be.d2h(out, d, sizeof(double) * (size_t)N);
+    be.sync();
+    return cx->check();
+}
+
+// Forest::get_bounding_box after the run (graph.cpp:446-452): the final union-find roots and their boxes,
+// {root, xmin, ymin, xmax, ymax} ascending by root; *n = their number (min(n, capacity) written).
+template <class Backend>
+int api_final_roots(Context<Backend>* cx, int64_t batch, int frame, int32_t* out, int64_t capacity, int64_t* n) {
+    if (!cx->have_batch() || (!out && capacity > 0)) return cx->fail(DOFS_ERR_INVALID_ARG, "no batch");
+    if (batch < 0) batch = cx->nbatch - 1;
+    if (!cx->live(batch)) return cx->fail(DOFS_ERR_INVALID_ARG, "batch no longer readable");
+    const int slot = cx->slot_of(batch);
+    if (frame < 0 || frame >= cx->meta[slot].B) return cx->fail(DOFS_ERR_INVALID_ARG, "no frame");
+    Pipeline<Backend>& P = cx->pipe(slot);
+    const Ws& w = P.w;
+    const Dims& d = w.d;
+    Backend& be = cx->be;
+    cx->join(batch);
+    std::vector<int32_t> rec;
+    if (d.M <= 0) {  // one pixel
+        rec = {0, 0, 0, 0, 0};
+    } else if (w.mreal >= d.M) {  // connected: the last merge's root keeps the frame's box
+        int q = 0;
+        RepVal r;
+        be.d2h(&q, P.pre + (int64_t)frame * d.NL + d.N + d.M - 1, sizeof(int));
+        be.sync();
+        be.d2h(&r, w.Rv + (int64_t)frame * d.NL + q, sizeof(RepVal));
+        be.sync();
+        rec = {r.root, r.bb.x0, r.bb.y0, r.bb.x1, r.bb.y1};
+    } else {  // a forest: the components joined by the completion merges
+        const int64_t k = d.M - w.mreal + 1;
+        int32_t* dv = (int32_t*)cx->scratch(sizeof(int32_t) * 5 * (size_t)k);
+        if (!dv) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+        be.launch(1, d.M - w.mreal, KFinalRoots{w, P.pre, frame, dv});
+        rec.resize(5 * (size_t)k);
+        be.d2h(rec.data(), dv, sizeof(int32_t) * rec.size());
+        be.sync();
+        std::vector<int64_t> idx((size_t)k);
+        for (int64_t i = 0; i < k; ++i) idx[(size_t)i] = i;
+        std::sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return rec[5 * a] < rec[5 * b]; });
+        std::vector<int32_t> sorted(rec.size());
+        for (int64_t i = 0; i < k; ++i)
+            for (int t = 0; t < 5; ++t) sorted[5 * i + t] = rec[5 * idx[(size_t)i] + t];
+        rec.swap(sorted);
+    }
+    const int64_t cnt = (int64_t)rec.size() / 5;
+    if (n) *n = cnt;
+    for (int64_t i = 0; i < cnt && i < capacity; ++i) memcpy(out + 5 * i, rec.data() + 5 * i, 5 * sizeof(int32_t));
+    return cx->check();
+}
+
 template <class Backend>
 int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity) {
     if (!cx->have_batch() || !ev) return cx->fail(DOFS_ERR_INVALID_ARG, "no batch");
@@ -682,6 +754,43 @@ int api_lift_batch(Context<Backend>* cx, int n, const float* dirs, const int* bo
     }
     be.launch(1, n, k);
     be.d2h(out, s + o_out, b_out);
+    be.sync();
+    return cx->check();
+}
+
+// get_upper_face / get_upper_face_simple (lifting_3d.cpp:290-348 / :261-288) on the device, n boxes.
+struct KUpperFaceBatch {
+    const int* boxes;  // n x {xmin, ymin, xmax, ymax}
+    const float* lf;   // n x 4 x (x, y)
+    float* out;        // n x 4 x (x, y)
+    int simple;
+    DOFS_HD void operator()(int, int64_t i) const {
+        P2 l[4], u[4];
+        for (int k = 0; k < 4; ++k) l[k] = mk(lf[8 * i + 2 * k], lf[8 * i + 2 * k + 1]);
+        if (simple)
+            upper_face_simple(boxes + 4 * i, l, u);
+        else
+            upper_face(boxes + 4 * i, l, u);
+        for (int k = 0; k < 4; ++k) {
+            out[8 * i + 2 * k] = u[k].x;
+            out[8 * i + 2 * k + 1] = u[k].y;
+        }
+    }
+};
+
+template <class Backend>
+int api_upper_face_batch(Context<Backend>* cx, int n, const int* boxes, const float* lower, int simple, float* out) {
+    if (n <= 0 || !boxes || !lower || !out) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
+    cx->be.use_own();
+    const size_t b_box = 16 * (size_t)n, b_f = 32 * (size_t)n;
+    const size_t o_lf = (b_box + 255) & ~(size_t)255, o_out = (o_lf + b_f + 255) & ~(size_t)255;
+    char* s = (char*)cx->scratch(o_out + b_f);
+    if (!s) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    Backend& be = cx->be;
+    be.h2d(s, boxes, b_box);
+    be.h2d(s + o_lf, lower, b_f);
+    be.launch(1, n, KUpperFaceBatch{(const int*)s, (const float*)(s + o_lf), (float*)(s + o_out), simple});
+    be.d2h(out, s + o_out, b_f);
     be.sync();
     return cx->check();
 }

@@ -33,6 +33,34 @@ void dofs_intersect(const float a1[2], const float a2[2], const float b1[2], con
     out[1] = r.y;
 }
 
+void dofs_upper_face(const int32_t box[4], const float lower_face[8], float upper_face[8]) {
+    dofs::P2 l[4], u[4];
+    for (int k = 0; k < 4; ++k) l[k] = dofs::mk(lower_face[2 * k], lower_face[2 * k + 1]);
+    dofs::upper_face(box, l, u);
+    for (int k = 0; k < 4; ++k) {
+        upper_face[2 * k] = u[k].x;
+        upper_face[2 * k + 1] = u[k].y;
+    }
+}
+
+void dofs_upper_face_simple(const int32_t box[4], const float lower_face[8], float upper_face[8]) {
+    dofs::P2 l[4], u[4];
+    for (int k = 0; k < 4; ++k) l[k] = dofs::mk(lower_face[2 * k], lower_face[2 * k + 1]);
+    dofs::upper_face_simple(box, l, u);
+    for (int k = 0; k < 4; ++k) {
+        upper_face[2 * k] = u[k].x;
+        upper_face[2 * k + 1] = u[k].y;
+    }
+}
+
+int32_t dofs_obj_size(int32_t cls, double out[2]) {
+    int sz[2];
+    if (!out || !dofs::obj_size_of(cls, sz)) return DOFS_ERR_INVALID_ARG;
+    out[0] = sz[0];
+    out[1] = sz[1];
+    return DOFS_OK;
+}
+
 dofs_ctx* dofs_create(int32_t device) {
     if (!DofsBackend::device_ok(device)) return nullptr;
     dofs_ctx* c = new dofs_ctx(device);
@@ -108,6 +136,19 @@ int32_t dofs_batch_fetch_id(dofs_ctx* ctx, int64_t batch, int32_t frame, dofs_re
     if (!ctx) return DOFS_ERR_INVALID_ARG;
     ctx->be.use_own();
     return dofs::api_fetch(ctx, frame, out, batch);
+}
+
+int32_t dofs_segment_scores(dofs_ctx* ctx, int64_t batch, int32_t frame, double* scores, int64_t capacity) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    ctx->be.use_own();
+    return dofs::api_segment_scores(ctx, batch, frame, scores, capacity);
+}
+
+int32_t dofs_final_roots(dofs_ctx* ctx, int64_t batch, int32_t frame, int32_t* roots_bbox, int64_t capacity,
+                         int64_t* n_roots) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    ctx->be.use_own();
+    return dofs::api_final_roots(ctx, batch, frame, roots_bbox, capacity, n_roots);
 }
 
 int32_t dofs_batch_records_device(dofs_ctx* ctx, void** d_records, void** d_counts, int32_t* capacity) {
@@ -229,6 +270,12 @@ int32_t dofs_lift_batch(dofs_ctx* ctx, int32_t n, const float* dirs, const int32
                         const float mat[9], const float inv[9], const float inv_upper[27], dofs_solution* out) {
     if (!ctx) return DOFS_ERR_INVALID_ARG;
     return dofs::api_lift_batch(ctx, n, dirs, boxes, cls, mat, inv, inv_upper, out);
+}
+
+int32_t dofs_upper_face_batch(dofs_ctx* ctx, int32_t n, const int32_t* boxes, const float* lower_faces,
+                              int32_t simple, float* upper_faces) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    return dofs::api_upper_face_batch(ctx, n, boxes, lower_faces, simple, upper_faces);
 }
 
 int32_t dofs_intersect_batch(dofs_ctx* ctx, int32_t n, const float* pts, float* out) {

@@ -93,6 +93,8 @@ struct Ws {
     int* lposr;  // per frame (stride N): preorder position of the leaf of each leaf rank (aliases uf,
                  // dead after the MST); KPathInit's path bottoms
     int* cur;
+    int* slast;  // per slot: the last scored candidate merge (Forest::segment_scores, graph.cpp:326); aliases
+                 // cur, the replay's path cursors, dead once the replay ended
     int* ptop;
     int* list_short;
     int* list_long;
@@ -1353,10 +1355,11 @@ struct KLift {
         // no early return: every lane reaches the counters and the keyed max, which aggregates a
         // wave's lanes of one slot (a frame's largest cluster root takes most of its candidate events)
         bool scored = false, qual = false;
-        int root = 0;
+        int root = 0, merge = -1;
         double score = -1.0;
         if (valid && j < w.C(f)[C_CAND]) {
             const int i = w.cand[f * d.M + j];
+            merge = i;
             const NodeVal v = node_val(w, pre, f, d.N + i);
             const double rect_area = (double)((v.x1 - v.x0 + 1) * (v.y1 - v.y0 + 1));
             const double convexity = v.size / rect_area;
@@ -1370,6 +1373,8 @@ struct KLift {
         int unused[3];
         t.take3(w.C(f) + C_SCORED, scored, w.C(f) + C_QUAL, qual, nullptr, false, unused, unused + 1, unused + 2);
         dofs_agg_max_u64(w.sbest + f * d.N, root, dbits(score), qual);
+        // segment_scores[root] = score for every scored candidate (graph.cpp:326): the latest merge wins
+        dofs_agg_max(w.slast + f * d.N, root, merge, scored);
     }
 };
 
@@ -1378,6 +1383,7 @@ struct KSlotInit {
     DOFS_HD void operator()(int f, int64_t s) const {
         w.sbest[f * w.d.N + s] = 0ull;
         w.sevent[f * w.d.N + s] = kIntMax;
+        w.slast[f * w.d.N + s] = -1;
     }
 };
 
@@ -1439,6 +1445,62 @@ struct KSnapshot {
             rec.upper_face[t][1] = sn.sol.upper_face[t][1];
         }
         w.recs[(int64_t)f * w.snap_cap + k] = rec;
+    }
+};
+
+// Forest::get_segment_best_score (graph.cpp:386-389) of every slot of frame f, on demand: the score of
+// the slot's last scored candidate, recomputed from its merge's replay record by the scoring function
+// KLift used (same operations, same result); 0.0, segment_scores' initial value (graph.cpp:139), where
+// the slot never had one.
+struct KSegScores {
+    Ws w;
+    const int* pre;
+    int frame;
+    double* out;
+    DOFS_HD void operator()(int, int64_t s) const {
+        const int i = w.slast[frame * w.d.N + s];
+        double v = 0.0;
+        if (i >= 0) {
+            int cls;
+            v = event_score(w, node_val(w, pre, frame, w.d.N + i), &cls, nullptr);
+        }
+        out[s] = v;
+    }
+};
+
+// The final union-find roots of frame f's run and their boxes — Forest::get_bounding_box after the loop
+// (graph.cpp:446-452): merge clears the non-root side's box (:208), so only the roots of the components
+// left by the caller's merges keep one. Those components are the children of the completion merges
+// mreal .. M-1 (dofs_pipeline run_a_edges: merge mreal + j joins the chain of components 0..j with
+// component j + 1), written to out[5 * slot] = {root, xmin, ymin, xmax, ymax}: completion merge 0 fills
+// slots 0 and 1, merge j >= 1 slot j + 1 (its other child is the chain). One thread per completion merge.
+struct KFinalRoots {
+    Ws w;
+    const int* pre;
+    int frame;
+    int* out;
+    DOFS_HD void operator()(int, int64_t j) const {
+        const Dims& d = w.d;
+        const int64_t k = w.mreal + j;
+        const int c[2] = {w.lu[frame * d.M + k], w.lv[frame * d.M + k]};
+        int slot = j == 0 ? 0 : (int)j + 1;
+        for (int t = 0; t < 2; ++t) {
+            if (c[t] >= d.N + w.mreal) continue;  // the chain of the earlier completion merges
+            int* o = out + 5 * slot;
+            if (c[t] < d.N) {  // a pixel no caller edge joined: its own box
+                o[0] = c[t];
+                o[1] = o[3] = c[t] % d.W;
+                o[2] = o[4] = c[t] / d.W;
+            } else {
+                const RepVal r = w.Rv[frame * d.NL + pre[frame * d.NL + c[t]]];
+                o[0] = r.root;
+                o[1] = r.bb.x0;
+                o[2] = r.bb.y0;
+                o[3] = r.bb.x1;
+                o[4] = r.bb.y1;
+            }
+            ++slot;
+        }
     }
 };
 

@@ -91,7 +91,8 @@ DOFS_HDM inline double motion_direction(P2 dir, const int box[4], const float* p
     return atan2(v_y, v_x);
 }
 
-// lifting_3d.cpp:290-348
+// get_upper_face, lifting_3d.cpp:290-348 (the catch branch :325-338 is unreachable: get_intersect
+// returns NaN for parallel lines instead of throwing, :77-82)
 DOFS_HDM inline void upper_face(const int box[4], const P2 lf[4], P2 uf[4]) {
     uf[2] = p_sub(lf[2], mk(0.0f, lf[2].y - (float)box[1]));
     P2 right_van = intersect(lf[1], lf[2], lf[0], lf[3]);
@@ -99,6 +100,26 @@ DOFS_HDM inline void upper_face(const int box[4], const P2 lf[4], P2 uf[4]) {
     P2 left_van = intersect(lf[2], lf[3], lf[0], lf[1]);
     uf[3] = intersect(uf[2], left_van, mk((float)box[2], (float)box[1]), mk((float)box[2], (float)box[3]));
     uf[0] = intersect(left_van, uf[1], right_van, uf[3]);
+}
+
+// get_upper_face_simple, lifting_3d.cpp:261-288 (not called by the path; public in lifting_3d.hpp:23-24).
+// h_min = 0 - ymin + std::min(lf[1].y, lf[2].y) in double (xmin, ymin as double; h_max is unused), then
+// every corner minus cv::Point2f(0, h_min): the double narrowed to float, the subtraction in float.
+DOFS_HDM inline void upper_face_simple(const int box[4], const P2 lf[4], P2 uf[4]) {
+    const double ymin = box[1];
+    const float lo = lf[2].y < lf[1].y ? lf[2].y : lf[1].y;  // std::min(a, b) == (b < a) ? b : a
+    const double h_min = 0 - ymin + (double)lo;
+    const float h = (float)h_min;
+    for (int k = 0; k < 4; ++k) uf[k] = p_sub(lf[k], mk(0.0f, h));
+}
+
+// getObjSize / get_obj_size (lifting_3d.cpp:255-259, :524-528): the class BEV sizes (length, width).
+DOFS_HDM inline bool obj_size_of(int cls, int out[2]) {
+    if (cls < 0 || cls > 2) return false;  // the reference indexes its 3-entry vector unchecked
+    const int sz[3][2] = {{258, 84}, {349, 165}, {370, 180}};
+    out[0] = sz[cls][0];
+    out[1] = sz[cls][1];
+    return true;
 }
 
 struct LiftMats {

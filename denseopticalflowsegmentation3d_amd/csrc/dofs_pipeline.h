@@ -141,6 +141,7 @@ struct Pipeline {
         w.ready = (int*)take(4 * B * NL);
         w.leaf_order = (int*)take(4 * B * N);
         w.cur = (int*)take(4 * B * N);
+        w.slast = w.cur;  // the replay's cursors are dead when KSlotInit fills it
         w.ptop = (int*)take(4 * B * N);
         w.list_short = (int*)take(4 * B * N);
         w.list_long = (int*)take(4 * B * N);

@@ -40,6 +40,17 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_calib.argtypes = [_fp, _fp, _fp]
     L.dofs_calib.restype = C.c_int32
     L.dofs_intersect.argtypes = [_fp, _fp, _fp, _fp, _fp]
+    if hasattr(L, "dofs_upper_face"):
+        L.dofs_upper_face.argtypes = [_ip, _fp, _fp]
+        L.dofs_upper_face_simple.argtypes = [_ip, _fp, _fp]
+        L.dofs_obj_size.argtypes = [C.c_int32, C.POINTER(C.c_double)]
+        L.dofs_obj_size.restype = C.c_int32
+        L.dofs_upper_face_batch.argtypes = [C.c_void_p, C.c_int32, _ip, _fp, C.c_int32, _fp]
+        L.dofs_upper_face_batch.restype = C.c_int32
+        L.dofs_segment_scores.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.POINTER(C.c_double), C.c_int64]
+        L.dofs_segment_scores.restype = C.c_int32
+        L.dofs_final_roots.argtypes = [C.c_void_p, C.c_int64, C.c_int32, _ip, C.c_int64, C.POINTER(C.c_int64)]
+        L.dofs_final_roots.restype = C.c_int32
     L.dofs_create.argtypes = [C.c_int32]
     L.dofs_create.restype = C.c_void_p
     L.dofs_destroy.argtypes = [C.c_void_p]
@@ -159,6 +170,26 @@ def intersect(a1, a2, b1, b2, lib: C.CDLL | None = None) -> np.ndarray:
     out = np.zeros(2, np.float32)
     L.dofs_intersect(*[_p(_f32(v)) for v in (a1, a2, b1, b2)], _p(out))
     return out
+
+
+def upper_face(box, lower_face, simple: bool = False, lib: C.CDLL | None = None) -> np.ndarray:
+    """get_upper_face (lifting_3d.cpp:290-348) or get_upper_face_simple (:261-288), host code: box =
+    (xmin, ymin, xmax, ymax), lower_face = 4 x 2 → upper face 4 x 2 float32."""
+    L = lib or load()
+    b = np.ascontiguousarray(box, dtype=np.int32)
+    lf = _f32(lower_face).reshape(8)
+    out = np.zeros(8, np.float32)
+    (L.dofs_upper_face_simple if simple else L.dofs_upper_face)(_p(b, C.c_int32), _p(lf), _p(out))
+    return out.reshape(4, 2)
+
+
+def obj_size(cls: int, lib: C.CDLL | None = None) -> tuple[float, float]:
+    """get_obj_size(cls) (lifting_3d.cpp:524-528): the class's BEV (length, width)."""
+    L = lib or load()
+    out = np.zeros(2, np.float64)
+    if L.dofs_obj_size(cls, _p(out, C.c_double)) != 0:
+        raise ValueError(f"get_obj_size: cls must be 0..2, got {cls}")
+    return float(out[0]), float(out[1])
 
 
 @dataclass
@@ -318,6 +349,34 @@ class Dofs:
         else:
             self._err(self.lib.dofs_batch_fetch_id(self.ctx, batch, frame, C.byref(r)), "dofs_batch_fetch_id")
         return FrameResult(H, W, snaps[:r.n_snapshots].copy(), labels, leaf, blurred, self._stats(r))
+
+    def segment_scores(self, frame: int = 0, batch: int | None = None) -> np.ndarray:
+        """Forest::get_segment_best_score(id) for every id (graph.cpp:386-389, :326): H*W float64."""
+        H, W = self._last_hw
+        out = np.zeros(H * W, np.float64)
+        self._err(self.lib.dofs_segment_scores(self.ctx, -1 if batch is None else batch, frame, _p(out, C.c_double),
+                                               out.size), "dofs_segment_scores")
+        return out
+
+    def final_roots(self, frame: int = 0, batch: int | None = None) -> np.ndarray:
+        """Forest::get_bounding_box after the loop (graph.cpp:446-452): the final roots' {root, xmin, ymin,
+        xmax, ymax} rows (int32, ascending root); every other id's box is empty."""
+        n = C.c_int64()
+        bid = -1 if batch is None else batch
+        self._err(self.lib.dofs_final_roots(self.ctx, bid, frame, None, 0, C.byref(n)), "dofs_final_roots")
+        out = np.zeros((max(n.value, 1), 5), np.int32)
+        self._err(self.lib.dofs_final_roots(self.ctx, bid, frame, _p(out, C.c_int32), n.value, C.byref(n)),
+                  "dofs_final_roots")
+        return out[:n.value]
+
+    def upper_face_batch(self, boxes, lower_faces, simple: bool = False) -> np.ndarray:
+        """get_upper_face(_simple) on the device for n boxes: boxes n x 4, lower_faces n x 4 x 2."""
+        b = np.ascontiguousarray(boxes, dtype=np.int32).reshape(-1, 4)
+        lf = _f32(lower_faces).reshape(-1, 8)
+        out = np.zeros((len(b), 8), np.float32)
+        self._err(self.lib.dofs_upper_face_batch(self.ctx, len(b), _p(b, C.c_int32), _p(lf), 1 if simple else 0,
+                                                 _p(out)), "dofs_upper_face_batch")
+        return out.reshape(-1, 4, 2)
 
     def records_device(self):
         """(device ptr of B×cap DofsBoxRecord, device ptr of counters, cap)."""

@@ -29,6 +29,16 @@
  *   dofs_intersect ← cv::Point2f get_intersect(a1, a2, b1, b2)   cpp/inc/lifting_3d.hpp:26, lifting_3d.cpp:63-110
  *   dofs_calib     ← std::pair<Matx33f,Matx33f> get_mat()        cpp/inc/lifting_3d.hpp:17, lifting_3d.cpp:482-514
  *                    cv::Matx33f get_mat_upper(int cls)          cpp/inc/lifting_3d.hpp:18, lifting_3d.cpp:441-480
+ *   dofs_upper_face        ← std::vector<cv::Point2f> get_upper_face(box_2d, lower_face)
+ *                            cpp/inc/lifting_3d.hpp:21-22, lifting_3d.cpp:290-348
+ *   dofs_upper_face_simple ← std::vector<cv::Point2f> get_upper_face_simple(box_2d, lower_face)
+ *                            cpp/inc/lifting_3d.hpp:23-24, lifting_3d.cpp:261-288
+ *   dofs_obj_size          ← std::pair<double,double> get_obj_size(int cls)
+ *                            cpp/inc/lifting_3d.hpp:25, lifting_3d.cpp:524-528
+ *   dofs_segment_scores    ← double Forest::get_segment_best_score(int node_id) const
+ *                            cpp/inc/graph.hpp:96, graph.cpp:386-389 (segment_scores, :139, :326)
+ *   dofs_final_roots       ← std::vector<cv::Point2i> Forest::get_bounding_box(int node_id) const after the run
+ *                            cpp/inc/graph.hpp:103, graph.cpp:446-452 (bboxes cleared by merge, :208)
  *
  * Conventions
  *   - Plain C types only. Matrices are row-major float[9] (cv::Matx33f layout).
@@ -206,6 +216,23 @@ int32_t dofs_batch_fetch(dofs_ctx* ctx, int32_t frame, dofs_result* out);
 /* dofs_batch_fetch for batch id `batch` (one of the last dofs_batch_slots() issued). Waits for it. */
 int32_t dofs_batch_fetch_id(dofs_ctx* ctx, int64_t batch, int32_t frame, dofs_result* out);
 
+/* Forest::get_segment_best_score(id) for every id of frame `frame` of batch id `batch` (-1 = the last
+ * batch; dofs_segment / dofs_segment_graph run as one-frame batches): scores[id] = segment_scores[id],
+ * which new_merge writes for EVERY scored candidate (get_score != -1) of root id, before the convexity
+ * and score-threshold tests (graph.cpp:326) — the root's last scored candidate's score, not its best
+ * (that is the snapshot's score) — and 0.0, the vector's initial value (graph.cpp:139), where none.
+ * capacity >= H*W doubles (host). Waits for the batch. */
+int32_t dofs_segment_scores(dofs_ctx* ctx, int64_t batch, int32_t frame, double* scores, int64_t capacity);
+
+/* Forest::get_bounding_box(id) AFTER the Kruskal loop (graph.cpp:446-452): merge clears the non-root
+ * side's box (graph.cpp:208), so only the final union-find roots still have one — one per connected
+ * component of the processed edges (one for get_segmented_array's grid, with the whole frame's box).
+ * Writes min(n, capacity) records {root, xmin, ymin, xmax, ymax} (inclusive) ascending by root;
+ * *n_roots = n. Every other id's box is the empty vector. (A snapshot's box at its winning merge is
+ * dofs_snapshot.bbox.) batch = -1: the last batch. Waits for the batch. */
+int32_t dofs_final_roots(dofs_ctx* ctx, int64_t batch, int32_t frame, int32_t* roots_bbox, int64_t capacity,
+                         int64_t* n_roots);
+
 /* Intra-frame sharding of the MST stage (BASELINE config 5: one large frame split
  * into row bands across GPUs). The global MST (graph.cpp:519-531 accepts exactly it) is contained in
  * the union of every row band's minimum spanning forest and the edges crossing band boundaries.
@@ -292,6 +319,19 @@ int32_t dofs_lift(dofs_ctx* ctx, const float dir[2], const int32_t box[4], const
 int32_t dofs_lift_batch(dofs_ctx* ctx, int32_t n, const float* dirs, const int32_t* boxes,
                         const int32_t* cls, const float mat[9], const float inv[9],
                         const float inv_upper[27], dofs_solution* out);
+
+/* get_upper_face (lifting_3d.cpp:290-348; the path's own upper face, :418) and get_upper_face_simple
+ * (:261-288), host code: box = {xmin, ymin, xmax, ymax} (box_2d[0], box_2d[1]), lower_face / upper_face =
+ * 4 corners x (x, y). Exact float / double semantics of the reference (cv::Point2f arithmetic, no FMA). */
+void dofs_upper_face(const int32_t box[4], const float lower_face[8], float upper_face[8]);
+void dofs_upper_face_simple(const int32_t box[4], const float lower_face[8], float upper_face[8]);
+/* The same on the device for n boxes (simple = 0: get_upper_face, 1: get_upper_face_simple); boxes =
+ * n x 4 int32, lower_faces / upper_faces = n x 8 floats. Synchronous. */
+int32_t dofs_upper_face_batch(dofs_ctx* ctx, int32_t n, const int32_t* boxes, const float* lower_faces,
+                              int32_t simple, float* upper_faces);
+/* get_obj_size(cls) (lifting_3d.cpp:524-528): the class's BEV (length, width); cls outside 0..2 is
+ * DOFS_ERR_INVALID_ARG (the reference indexes its 3-entry vector unchecked). */
+int32_t dofs_obj_size(int32_t cls, double out[2]);
 
 /* get_intersect (host code, exact float semantics of lifting_3d.cpp:63-89). */
 void dofs_intersect(const float a1[2], const float a2[2], const float b1[2], const float b2[2], float out[2]);

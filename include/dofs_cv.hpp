@@ -14,12 +14,20 @@
 //       cpp/inc/lifting_3d.hpp:17-18, cpp/src/lifting_3d.cpp:441-514
 //   cv::Point2f get_intersect(a1, a2, b1, b2)                                        get_intersect
 //       cpp/inc/lifting_3d.hpp:26, cpp/src/lifting_3d.cpp:63-110
+//   std::vector<cv::Point2f> get_upper_face(box_2d, lower_face)                      get_upper_face
+//       cpp/inc/lifting_3d.hpp:21-22, cpp/src/lifting_3d.cpp:290-348
+//   std::vector<cv::Point2f> get_upper_face_simple(box_2d, lower_face)               get_upper_face_simple
+//       cpp/inc/lifting_3d.hpp:23-24, cpp/src/lifting_3d.cpp:261-288
+//   std::pair<double, double> get_obj_size(int cls)                                  get_obj_size
+//       cpp/inc/lifting_3d.hpp:25, cpp/src/lifting_3d.cpp:524-528
 //
-// What the adapter returns instead of a Forest. The reference's callers read a Forest only through
-// Forest::get_best_segments() (graph.cpp:391-429 — it returns the whole private segment_history vector,
-// graph.hpp:109) and Forest::get_bounding_box (graph.cpp:446-452); plot_best_segments_simple
-// (draw.cpp:101-160) takes the Forest to call exactly get_best_segments(). dofs_cv::Segmentation offers
-// those two accessors with the same results, so a call site changes from
+// What the adapter returns instead of a Forest. The Forest's public accessors are get_best_segments()
+// (graph.cpp:391-429 — it returns the whole private segment_history vector, graph.hpp:109),
+// get_bounding_box (graph.cpp:446-452) and get_segment_best_score (graph.cpp:386-389);
+// plot_best_segments_simple (draw.cpp:101-160) takes the Forest to call exactly get_best_segments().
+// dofs_cv::Segmentation offers those three with the results a Forest gives after segment_graph returns
+// (every non-root box cleared by merge, graph.cpp:208; segment_scores as new_merge left it, :326), so a
+// call site changes from
 //     Forest forest = get_segmented_array(flow, bev, persp, inv, inv_upper);
 //     std::vector<SegmentData> history = forest.get_best_segments();
 // to
@@ -128,6 +136,8 @@ public:
     std::vector<dofs_snapshot> snapshots;  // non-empty segment_history slots, ascending slot id
     std::vector<int32_t> leaf_order;       // pixel ids; slot s's members = leaf_order[seg_begin, + size)
     std::vector<int32_t> label;            // overlay label per pixel (draw.cpp:118-147), -1 = none
+    std::vector<double> segment_scores;    // Forest::segment_scores (graph.cpp:139, :326), H*W
+    std::vector<int32_t> final_roots;      // {root, xmin, ymin, xmax, ymax} of every final union-find root
     dofs_stats stats{};
 
     std::set<int> members(const dofs_snapshot& s) const {
@@ -143,9 +153,19 @@ public:
             h[(size_t)s.slot] = SegmentDataT(s.score, members(s), to_solution<SolutionT>(s.sol), s.move);
         return h;
     }
-    // Forest::get_bounding_box (graph.cpp:446-452) of a history slot at its recorded merge:
-    // {(xmin, ymin), (xmax, ymax)} inclusive.
-    std::vector<cv::Point2i> get_bounding_box(int slot) const {
+    // Forest::get_bounding_box (graph.cpp:446-452) after the loop: {(xmin, ymin), (xmax, ymax)} inclusive
+    // for a final union-find root, the empty vector for every other id (merge cleared it, graph.cpp:208).
+    std::vector<cv::Point2i> get_bounding_box(int node_id) const {
+        for (size_t k = 0; k + 4 < final_roots.size(); k += 5)
+            if (final_roots[k] == node_id)
+                return {cv::Point2i(final_roots[k + 1], final_roots[k + 2]), cv::Point2i(final_roots[k + 3], final_roots[k + 4])};
+        return {};
+    }
+    // Forest::get_segment_best_score (graph.cpp:386-389): the score of root node_id's LAST scored
+    // candidate (written before the convexity / threshold tests, graph.cpp:326), 0.0 if it had none.
+    double get_segment_best_score(int node_id) const { return segment_scores.at((size_t)node_id); }
+    // Not a Forest accessor: a history slot's box at its winning merge (the snapshot's box).
+    std::vector<cv::Point2i> get_snapshot_bounding_box(int slot) const {
         for (const dofs_snapshot& s : snapshots)
             if (s.slot == slot) return {cv::Point2i(s.bbox[0], s.bbox[1]), cv::Point2i(s.bbox[2], s.bbox[3])};
         throw std::runtime_error("dofs_cv: slot has no snapshot");
@@ -185,6 +205,13 @@ Segmentation collect(const cv::Mat& flow, bool want_blur, std::vector<float>* bl
         check(rc, "segment");
         r.snapshots.resize((size_t)res.n_snapshots);
         r.stats = res.stats;
+        // the Forest state after the loop: segment_scores and the final roots' boxes
+        r.segment_scores.resize(N);
+        check(dofs_segment_scores(context(), -1, 0, r.segment_scores.data(), (int64_t)N), "segment_scores");
+        int64_t n = 0;
+        check(dofs_final_roots(context(), -1, 0, nullptr, 0, &n), "final_roots");
+        r.final_roots.resize(5 * (size_t)n);
+        check(dofs_final_roots(context(), -1, 0, r.final_roots.data(), n, &n), "final_roots");
         return r;
     }
 }
@@ -286,6 +313,35 @@ inline cv::Point2f get_intersect(cv::Point2f a1, cv::Point2f a2, cv::Point2f b1,
     float r[2];
     dofs_intersect(A1, A2, B1, B2, r);
     return cv::Point2f(r[0], r[1]);
+}
+
+// get_upper_face (lifting_3d.cpp:290-348) and get_upper_face_simple (:261-288): host code.
+namespace detail {
+template <class F>
+std::vector<cv::Point2f> upper(const std::vector<cv::Point2i>& box_2d, const std::vector<cv::Point2f>& lower_face, F f) {
+    if (box_2d.size() < 2 || lower_face.size() < 4) throw std::runtime_error("dofs_cv: box_2d / lower_face size");
+    const int32_t box[4] = {box_2d[0].x, box_2d[0].y, box_2d[1].x, box_2d[1].y};
+    float lf[8], uf[8];
+    for (int k = 0; k < 4; ++k) lf[2 * k] = lower_face[k].x, lf[2 * k + 1] = lower_face[k].y;
+    f(box, lf, uf);
+    std::vector<cv::Point2f> out;
+    for (int k = 0; k < 4; ++k) out.emplace_back(uf[2 * k], uf[2 * k + 1]);
+    return out;
+}
+}  // namespace detail
+inline std::vector<cv::Point2f> get_upper_face(const std::vector<cv::Point2i>& box_2d,
+                                               const std::vector<cv::Point2f>& lower_face) {
+    return detail::upper(box_2d, lower_face, dofs_upper_face);
+}
+inline std::vector<cv::Point2f> get_upper_face_simple(std::vector<cv::Point2i> box_2d, std::vector<cv::Point2f> lower_face) {
+    return detail::upper(box_2d, lower_face, dofs_upper_face_simple);
+}
+
+// get_obj_size (lifting_3d.cpp:524-528): host code.
+inline std::pair<double, double> get_obj_size(int cls) {
+    double o[2];
+    if (dofs_obj_size(cls, o) != DOFS_OK) throw std::runtime_error("dofs_cv: get_obj_size: cls must be 0..2");
+    return {o[0], o[1]};
 }
 
 }  // namespace dofs_cv

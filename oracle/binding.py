@@ -58,6 +58,8 @@ def lib(opt: str = "O2") -> C.CDLL:
                                     C.POINTER(DofsParams), C.c_int32, C.POINTER(DofsResult), C.POINTER(DofsEvent), dp,
                                     ip]
     L.oracle_segment_ex.restype = C.c_int32
+    L.oracle_upper_face.argtypes = [ip, fp, C.c_int32, fp]
+    L.oracle_obj_size.argtypes = [C.c_int32, dp]
     _LIBS[name] = L
     return L
 
@@ -106,6 +108,21 @@ def score(box, direction, persp, inv, inv_upper27):
     v = lib().oracle_score(_ptr(b, C.c_int32), _ptr(_f(direction), C.c_float), _ptr(_f(persp), C.c_float),
                            _ptr(_f(inv), C.c_float), _ptr(_f(inv_upper27), C.c_float), C.byref(s))
     return v, s
+
+
+def upper_face(box, lower_face, simple: bool = False) -> np.ndarray:
+    """get_upper_face / get_upper_face_simple (lifting_3d.cpp:290-348 / :261-288): 4 x 2 float32."""
+    b = np.ascontiguousarray(box, dtype=np.int32)
+    lf = _f(lower_face).reshape(8)
+    out = np.zeros(8, np.float32)
+    lib().oracle_upper_face(_ptr(b, C.c_int32), _ptr(lf, C.c_float), 1 if simple else 0, _ptr(out, C.c_float))
+    return out.reshape(4, 2)
+
+
+def obj_size(cls: int) -> tuple[float, float]:
+    out = np.zeros(2, np.float64)
+    lib().oracle_obj_size(cls, _ptr(out, C.c_double))
+    return float(out[0]), float(out[1])
 
 
 def calib():

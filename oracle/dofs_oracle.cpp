@@ -151,7 +151,19 @@ void get_upper_face(const int box[4], const P2 lf[4], P2 uf[4]) {
     uf[0] = get_intersect(left_van, uf[1], right_van, uf[3]);  // :322
 }
 
+// get_upper_face_simple, lifting_3d.cpp:261-288 (public, lifting_3d.hpp:23-24; not called by the path).
+void get_upper_face_simple(const int box[4], const P2 lf[4], P2 uf[4]) {
+    double ymin = box[1];                                        // :267 (xmin/xmax/ymax unused)
+    double h_min = 0 - ymin + std::min(lf[1].y, lf[2].y);        // :272 (h_max, :271, is unused)
+    const P2 dh = p2(0.0f, (float)h_min);                        // cv::Point2f(0, h_min): double -> float
+    uf[0] = sub(lf[0], dh);                                      // :274
+    uf[3] = sub(lf[3], dh);                                      // :275
+    uf[1] = sub(lf[1], dh);                                      // :277
+    uf[2] = sub(lf[2], dh);                                      // :278
+}
+
 const int kDefaultObjSize[3][2] = {{258, 84}, {349, 165}, {370, 180}};  // lifting_3d.cpp:255-259
+const double kObjSizeD[3][2] = {{258, 84}, {349, 165}, {370, 180}};     // get_obj_size, lifting_3d.cpp:524-528
 
 // get_bottom_variants, lifting_3d.cpp:350-439.
 void get_bottom_variants(P2 dir, const int box[4], const float* mat, const float* inv, const float* inv_upper,
@@ -784,6 +796,27 @@ double oracle_score(const int32_t box[4], const float dir[2], const float persp[
 }
 
 void oracle_calib(float persp[9], float inv[9], float inv_upper[27]) { calib(persp, inv, inv_upper); }
+
+// get_upper_face (simple = 0) / get_upper_face_simple (simple = 1) on box {xmin, ymin, xmax, ymax}.
+void oracle_upper_face(const int32_t box[4], const float lf[8], int32_t simple, float uf[8]) {
+    int b[4] = {box[0], box[1], box[2], box[3]};
+    P2 l[4], u[4];
+    for (int k = 0; k < 4; ++k) l[k] = p2(lf[2 * k], lf[2 * k + 1]);
+    if (simple)
+        get_upper_face_simple(b, l, u);
+    else
+        get_upper_face(b, l, u);
+    for (int k = 0; k < 4; ++k) {
+        uf[2 * k] = u[k].x;
+        uf[2 * k + 1] = u[k].y;
+    }
+}
+
+// get_obj_size(cls), lifting_3d.cpp:524-528 (cls must be 0..2).
+void oracle_obj_size(int32_t cls, double out[2]) {
+    out[0] = kObjSizeD[cls][0];
+    out[1] = kObjSizeD[cls][1];
+}
 
 void oracle_perspective_transform(const float src[8], const float dst[8], double out[9]) {
     P2 s[4], d[4];

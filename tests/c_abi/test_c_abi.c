@@ -43,6 +43,19 @@ int main(int argc, char** argv) {
     dofs_intersect(c1, c2, d1, d2, r); /* :80-89: parallel lines -> NaN */
     CHECK(isnan(r[0]) && isnan(r[1]));
 
+    { /* get_upper_face_simple (lifting_3d.cpp:261-288): every corner lifted by min(lf[1].y, lf[2].y) - ymin */
+        const int32_t box[4] = {10, 20, 60, 90};
+        const float lf[8] = {12, 80, 15, 50, 55, 45, 58, 85};
+        float uf[8];
+        double os[2];
+        dofs_upper_face_simple(box, lf, uf);
+        CHECK(uf[0] == 12.0f && uf[1] == 80.0f - 25.0f && uf[5] == 45.0f - 25.0f);
+        dofs_upper_face(box, lf, uf); /* get_upper_face (:290-348): E = (lf[2].x, ymin) */
+        CHECK(uf[4] == 55.0f && uf[5] == 20.0f);
+        CHECK(dofs_obj_size(0, os) == DOFS_OK && os[0] == 258.0 && os[1] == 84.0); /* :524-528 */
+        CHECK(dofs_obj_size(3, os) == DOFS_ERR_INVALID_ARG);
+    }
+
     dofs_default_flow_params(&fp);
     CHECK(fp.pyr_scale == 0.5 && fp.levels == 3 && fp.winsize == 15 && fp.iterations == 3);
     CHECK(fp.poly_n == 5 && fp.poly_sigma == 1.2 && fp.flags == 0);
@@ -73,6 +86,15 @@ int main(int argc, char** argv) {
             res.leaf_order = leaf;
             CHECK(dofs_segment_graph(ctx, flow, 3, 4, 0, edges, n, persp, inv, up, &p, &res) == DOFS_OK);
             CHECK(res.stats.n_merges == 11 && res.stats.n_edges == n);
+            { /* the Forest after the loop: one final root holding the whole 4x3 frame's box */
+                int32_t rb[5];
+                double sc[12];
+                int64_t nr = 0;
+                CHECK(dofs_final_roots(ctx, -1, 0, rb, 5, &nr) == DOFS_OK && nr == 1);
+                CHECK(rb[1] == 0 && rb[2] == 0 && rb[3] == 3 && rb[4] == 2);
+                CHECK(dofs_segment_scores(ctx, -1, 0, sc, 12) == DOFS_OK);
+                CHECK(dofs_segment_scores(ctx, -1, 0, sc, 11) == DOFS_ERR_CAPACITY);
+            }
             dofs_destroy(ctx);
         }
     }

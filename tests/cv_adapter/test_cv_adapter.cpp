@@ -4,6 +4,7 @@
 // arguments are exercised as in a real reference build. CPU: get_mat / get_mat_upper / get_intersect
 // (test_liftig_3d.cpp:69-89, :183-185). "device": get_segmented_array, build_graph + segment_graph,
 // get_best_segments, get_bounding_box and get_bottom_variants on the reference's KAT (:179-227, tol 0.1).
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -79,6 +80,30 @@ int main(int argc, char** argv) {
     CHECK(std::fabs(r.x - 2.4f) < 1e-2f && std::fabs(r.y - 2.4f) < 1e-2f);
     const cv::Point2f n = dofs_cv::get_intersect({1, 1}, {1, 2}, {3, 3}, {3, 4});  // :80-89
     CHECK(std::isnan(n.x) && std::isnan(n.y));
+    // get_upper_face / get_upper_face_simple / get_obj_size (lifting_3d.hpp:21-25): host code, same results
+    // as the C-ABI entries (which tests/test_forest_accessors.py pins against the oracle)
+    {
+        const std::vector<cv::Point2i> box = {cv::Point2i(375, 92), cv::Point2i(576, 286)};
+        const std::vector<cv::Point2f> lf = {{385.3f, 283.1f}, {380.2f, 215.7f}, {560.9f, 210.4f}, {570.5f, 280.6f}};
+        const int32_t b4[4] = {375, 92, 576, 286};
+        float l8[8], u8[8];
+        for (int k = 0; k < 4; ++k) l8[2 * k] = lf[k].x, l8[2 * k + 1] = lf[k].y;
+        std::vector<cv::Point2f> u = dofs_cv::get_upper_face(box, lf);
+        dofs_upper_face(b4, l8, u8);
+        CHECK(u.size() == 4 && u[2].x == u8[4] && u[2].y == 92.0f && u[0].x == u8[0] && u[3].y == u8[7]);
+        std::vector<cv::Point2f> us = dofs_cv::get_upper_face_simple(box, lf);
+        dofs_upper_face_simple(b4, l8, u8);
+        CHECK(us.size() == 4 && us[1].y == u8[3] && us[0].x == lf[0].x);
+        CHECK(us[1].y == lf[1].y - (float)(0 - 92.0 + (double)std::min(lf[1].y, lf[2].y)));  // :272-277
+        CHECK(dofs_cv::get_obj_size(1) == std::make_pair(349.0, 165.0));
+        bool threw = false;
+        try {
+            dofs_cv::get_obj_size(3);
+        } catch (const std::runtime_error&) {
+            threw = true;
+        }
+        CHECK(threw);
+    }
 
     if (argc > 1 && std::strcmp(argv[1], "device") == 0) {
         std::vector<cv::Matx33f> ups = {dofs_cv::get_mat_upper(0), dofs_cv::get_mat_upper(1), up2};
@@ -107,8 +132,18 @@ int main(int argc, char** argv) {
         CHECK(nonempty == a.snapshots.size());
         const dofs_snapshot& s0 = a.snapshots[0];
         CHECK((int)hist[s0.slot].seg.size() == s0.size && hist[s0.slot].sol.cls == s0.sol.cls);
-        std::vector<cv::Point2i> bb = a.get_bounding_box(s0.slot);
+        std::vector<cv::Point2i> bb = a.get_snapshot_bounding_box(s0.slot);
         CHECK(bb[0].x == s0.bbox[0] && bb[1].y == s0.bbox[3]);
+        // Forest::get_bounding_box after the loop: only the final root keeps a box — the whole frame
+        CHECK(a.final_roots.size() == 5);
+        if (a.final_roots.size() == 5) {
+            std::vector<cv::Point2i> fb = a.get_bounding_box(a.final_roots[0]);
+            CHECK(fb.size() == 2 && fb[0].x == 0 && fb[0].y == 0 && fb[1].x == W - 1 && fb[1].y == H - 1);
+            CHECK(a.get_bounding_box(a.final_roots[0] == 0 ? 1 : 0).empty());
+        }
+        // get_segment_best_score: a scored slot's last score (the snapshot slots were all scored)
+        for (const dofs_snapshot& s : a.snapshots) CHECK(a.get_segment_best_score(s.slot) != 0.0);
+        CHECK(a.segment_scores == b.segment_scores && a.final_roots == b.final_roots);
         cv::Mat lab = a.labels();
         CHECK(lab.rows == H && lab.cols == W && lab.type() == CV_32S);
         // get_bottom_variants on the reference's KAT (test_liftig_3d.cpp:179-227, tolerance 0.1)
