@@ -50,9 +50,12 @@ C_LONGM = 57           # counters: merges on long heavy paths
 #     16-B union-find record of the sweep read = 47 B.
 #   k_replay_long — unit: a merge on a long heavy path: its step inputs (StepIn, 32 B) in and its
 #     replay record (RepVal, 32 B) out = 64 B (a light merge child's 32-B record read is not counted).
+#   k_replay_flow — the whole replay in one dataflow launch; unit: a merge (every merge of the batch):
+#     StepIn 32 B in, RepVal 32 B out = 64 B.
 BYTES = {"k_boruvka_min4": (12, 16), "k_boruvka_pick4": 16, "k_boruvka_min": (24, 16), "k_krt_fused": 47,
-         "k_replay_long": 64}
-PROBES = ("k_boruvka_min4", "k_boruvka_pick4", "k_krt_fused", "k_replay_long")
+         "k_replay_long": 64, "k_replay_flow": 64}
+PROBES = ("k_boruvka_min4", "k_boruvka_pick4", "k_krt_fused", "k_replay_flow", "k_replay_long")
+C_FLOWERR = 58         # counters (frame 0): the dataflow replay gave up a bounded wait
 ROOF_KERNEL = "k_boruvka_min4"
 
 
@@ -314,6 +317,8 @@ def main(argv=None):
     # device-event time (events recorded on the stream the kernel runs on); units from the last batch
     # (every batch of the bench is the same workload shape)
     counters = ctx.batch_counters(chunks[-1][1])
+    if counters[0, C_FLOWERR]:
+        raise RuntimeError("the dataflow replay gave up a bounded wait: results of the timed batches are invalid")
     tiles = ctx.tile_pixels(chunks[-1][1])
     recs = ctx.records(chunks[-1][1])
     pmc = {}
@@ -348,6 +353,9 @@ def main(argv=None):
             entry["alg_bytes_per_unit"] = "24 (pass 0) / 16 (pass 1) per pixel of a processed tile"
             entry["units_per_batch"] = {"pass0_px": p0, "pass1_px": p1}
         elif name == "k_krt_fused" and len(chunks) == 1:
+            alg = BYTES[name] * (N - 1) * B * batches
+            entry["alg_bytes_per_unit"] = f"{BYTES[name]} per merge"
+        elif name == "k_replay_flow" and len(chunks) == 1:
             alg = BYTES[name] * (N - 1) * B * batches
             entry["alg_bytes_per_unit"] = f"{BYTES[name]} per merge"
         elif name == "k_replay_long" and len(chunks) == 1:

@@ -1,0 +1,596 @@
+// dofs_dataflow.h — K5, the replay of Forest::merge (graph.cpp:170-218) along heavy paths, as ONE
+// dataflow launch per batch (included by dofs_hip.hip after the round-based kernels it replaces;
+// DOFS_REPLAY_FLOW=0 selects those).
+//
+// Why: a heavy path advances until it meets a light child whose own path is not complete. The round
+// launches park such a path until the next round, so a round lasts as long as the longest advance
+// of any frame's path in it, and the batch pays the sum over rounds of those maxima (a kernel trace of
+// the 96-frame 1080p bench: rounds 0, 7, 8 and 9 took 37.6, 13.8, 15.2 and 13.5 ms, 93 ms in all, while
+// a frame's longest chain — its KRT height, ~370k merges — needs ~20 ms). Here a path that blocks
+// registers itself on its light child and gives its wave away; the child's completion hands the
+// parked path to whoever completed it, so every frame's chain runs as soon as its inputs exist and
+// the batch takes about its longest chain.
+//
+// Tasks. A task is one heavy path of one frame, word t = f * N + j (path j of frame f, < 2^30) | kFlowLong
+// for a long path (>= long_path merges, run by a whole wave as in k_replay_long1: 64 steps resolved in
+// parallel per chunk, both mean chains in one instruction stream); short paths run one per lane.
+//
+// State word of a path top (ready[] at top positions): open (kIntMax / kPendLong from KPathInit) → the
+// task word of the parent path parked on it (a light child has one parent position, so one waiter) →
+// kFlowDone. The parker publishes its cursor and running state, then CASes its task word in; the
+// completer publishes the top's record, then exchanges kFlowDone in and continues the waiter it got
+// back (a lane a short waiter; a long waiter goes to the long-path queue, whose tickets the dedicated
+// long workers hold). No task waits for another, so there is no deadlock and no residency requirement:
+// short workers leave when the pool is empty and their lanes are done, long workers when every long
+// path completed.
+//
+// Visibility inside the launch (MI355X_MICROARCH.md § visibility, cdna_hip_programming.md Guideline
+// 16): every word handed between workgroups — records of path tops and parked states, cursors, state
+// words, queue slots — is stored with agent-scope (sc1, write-through) stores, drained with
+// s_waitcnt vmcnt(0) before the state word that signals it, and read only with agent-scope (sc1)
+// loads, so no fence is needed. Everything else the launch reads was written by earlier launches.
+#pragma once
+
+namespace dofs {
+
+constexpr int kFlowDone = 0x7FFFFFF0;  // state word of a completed path top (open words are above it)
+constexpr int kFlowLong = 1 << 30;     // task word bit: a long path (run by a whole wave)
+constexpr int kFlowIdMask = kFlowLong - 1;
+
+// control block (ints), zeroed and filled by k_flow_prep each launch; per-frame prefix sums follow. Every
+// word that waves update or poll sits on a 256-byte line of its own: thousands of waves touch them, and
+// words sharing a line share its memory channel's queue (a CAS storm on the queue head there stalled
+// the pool claims next to it).
+constexpr int kFlowLine = 64;  // ints per line
+enum FlowCtlIdx {
+    FC_LONG_NEXT = 0 * kFlowLine,   // initial long pool: next unclaimed index
+    FC_SHORT_NEXT = 1 * kFlowLine,  // initial short pool (tiny paths of every frame first, then the others)
+    FC_QHEAD = 2 * kFlowLine,       // long-path queue (slots in w.bw, dead after the MST): head / tail
+    FC_QTAIL = 3 * kFlowLine,
+    FC_ERR = 4 * kFlowLine,         // a bounded wait gave up (results invalid; reported through C_FLOWERR)
+    FC_LDONE = 5 * kFlowLine,       // long paths completed
+    FC_NL = 7 * kFlowLine,          // read-only after k_flow_prep: pool sizes (long, tiny, other short)
+    FC_NT = FC_NL + 1,
+    FC_NS = FC_NL + 2,
+    FC_HDR = 8 * kFlowLine,         // then pl[B + 1], pt[B + 1], ps[B + 1]
+};
+constexpr int kFlowSpin = 1 << 22;  // polls of a queue slot before giving up (s_sleep between)
+
+// launch anatomy (a few atomics per task, not per step): read by dofs_debug_flow_stats (tools/flow_stats.py)
+constexpr int kFsStride = 32;  // u64 per stat: one 256-byte line each
+enum FlowStat {
+    FS_T0 = 0,         // first wave start (100 MHz wall clock, min)
+    FS_T_SHORT = 1,    // last short worker done (max)
+    FS_T_LONG = 2,     // last long-path completion (max)
+    FS_T_EXIT = 3,     // last wave exit (max)
+    FS_LRUNS = 4,      // flow_long calls
+    FS_LPARKS = 5,     // long paths parked
+    FS_LCHUNKS = 6,    // 64-step chunks of long paths
+    FS_PUSH = 7,       // long waiters queued by lanes
+    FS_INJECT = 8,     // short waiters handed to a short round by a long completion
+    FS_LDONE = 9,      // long completions
+    FS_LTICKS = 10,    // wall time inside flow_long, summed over waves
+    FS_SROUNDS = 11,   // flow_short calls
+    FS_STICKS = 12,    // wall time inside flow_short, summed over waves
+    FS_LSTEPS = 13,    // merges replayed by long paths
+    FS_N = 16
+};
+__device__ unsigned long long g_fs[FS_N * kFsStride];
+__device__ inline unsigned long long fs_now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ inline void fs_add(int i, unsigned long long v) { atomicAdd(&g_fs[i * kFsStride], v); }
+__device__ inline void fs_min(int i, unsigned long long v) { atomicMin(&g_fs[i * kFsStride], v); }
+__device__ inline void fs_max(int i, unsigned long long v) { atomicMax(&g_fs[i * kFsStride], v); }
+
+__device__ inline int f_ld(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ inline void f_st(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ inline unsigned long long f_ld64(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void f_st64(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void f_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// a RepVal handed to another workgroup: three 8-byte write-through stores / loads (the pads are unused)
+__device__ inline void rv_publish(RepVal* p, float mx, float my, int rank, int root, B4 bb) {
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    f_st64(q, (unsigned long long)__float_as_uint(mx) | ((unsigned long long)__float_as_uint(my) << 32));
+    f_st64(q + 1, (unsigned long long)(unsigned)rank | ((unsigned long long)(unsigned)root << 32));
+    unsigned long long b;
+    __builtin_memcpy(&b, &bb, 8);
+    f_st64(q + 2, b);
+}
+__device__ inline RepVal rv_fetch(const RepVal* p) {
+    const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+    const unsigned long long a = f_ld64(q), b = f_ld64(q + 1), c = f_ld64(q + 2);
+    RepVal r;
+    r.mx = __uint_as_float((unsigned)a);
+    r.my = __uint_as_float((unsigned)(a >> 32));
+    r.rank = (int)(unsigned)b;
+    r.root = (int)(unsigned)(b >> 32);
+    __builtin_memcpy(&r.bb, &c, 8);
+    r.pad0 = r.pad1 = 0;
+    return r;
+}
+
+// the state below a cursor q: the bottom leaf's singleton set (static), or a record a parker published
+__device__ inline void flow_start(const Ws& w, int f, int64_t qb, float* mx, float* my, int* rank, int* root, B4* bb) {
+    const Dims& d = w.d;
+    const int64_t lb = f * d.NL;
+    const int x = w.ord[lb + qb];
+    if (x < d.N) {
+        path_start(w, f, qb, mx, my, rank, root, bb);
+        return;
+    }
+    const RepVal v = rv_fetch(w.Rv + lb + qb);
+    *mx = v.mx;
+    *my = v.my;
+    *rank = v.rank;
+    *root = v.root;
+    *bb = v.bb;
+}
+
+__device__ inline int flow_frame(const int* pre, int B, int i) {  // largest f with pre[f] <= i
+    int lo = 0, hi = B;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (pre[mid] <= i)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+__device__ inline int flow_long_task(const Ws& w, const int* ctl, int i) {
+    const int B = w.d.B;
+    const int* pl = ctl + FC_HDR;
+    const int f = flow_frame(pl, B, i);
+    const int j = w.list_long[f * w.d.N + (i - pl[f])];
+    return (int)(f * w.d.N + j) | kFlowLong;
+}
+__device__ inline int flow_short_task(const Ws& w, const int* ctl, int i) {
+    const int B = w.d.B;
+    const int nt = ctl[FC_NT];
+    if (i < nt) {
+        const int* pt = ctl + FC_HDR + (B + 1);
+        const int f = flow_frame(pt, B, i);
+        const int j = w.list_short[f * w.d.N + w.d.N - 1 - (i - pt[f])];
+        return (int)(f * w.d.N + j);
+    }
+    const int* ps = ctl + FC_HDR + 2 * (B + 1);
+    const int f = flow_frame(ps, B, i - nt);
+    const int j = w.list_short[f * w.d.N + (i - nt - ps[f])];
+    return (int)(f * w.d.N + j);
+}
+
+// one thread: zero the control words, prefix sums of the per-frame pool sizes
+__global__ void k_flow_prep(Ws w, int* ctl) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int B = w.d.B;
+    int* pl = ctl + FC_HDR;
+    int* pt = pl + (B + 1);
+    int* ps = pt + (B + 1);
+    int sl = 0, st = 0, ss = 0;
+    for (int f = 0; f < B; ++f) {
+        pl[f] = sl;
+        pt[f] = st;
+        ps[f] = ss;
+        sl += w.C(f)[C_LONG];
+        st += w.C(f)[C_TINY];
+        ss += w.C(f)[C_SHORT];
+    }
+    pl[B] = sl;
+    pt[B] = st;
+    ps[B] = ss;
+    for (int k = 0; k < FC_HDR; ++k) ctl[k] = 0;
+    for (int k = 0; k < FS_N; ++k) g_fs[k * kFsStride] = (k == FS_T0) ? ~0ull : 0ull;
+    ctl[FC_NL] = sl;
+    ctl[FC_NT] = st;
+    ctl[FC_NS] = ss;
+}
+
+__device__ inline void flow_push(const Ws& w, int* ctl, unsigned epoch, int t) {
+    const int s = atomicAdd(ctl + FC_QTAIL, 1);
+    f_st64(w.bw + s, ((unsigned long long)epoch << 32) | (unsigned)t);
+}
+// Resolve position p of a long path (one lane per step, as one_resolve); light children through the
+// state words and published records.
+__device__ inline int flow_resolve(const Ws& w, int64_t lb, int p, int top, OneRec* o, B4* lbb, int accept = -1) {
+    lbb->x0 = lbb->y0 = 0x7fff;
+    lbb->x1 = lbb->y1 = -1;
+    if (p < top) return 0;
+    const StepIn in = w.In[lb + p];
+    int meta = in.meta;
+    int lrank = 0, lroot = in.lb;
+    if (in.meta & kStepDyn) {
+        const int lq = in.lb;
+        if (p != accept && f_ld(w.ready + lb + lq) != kFlowDone) return meta;  // accept: seen done by a CAS
+        const RepVal lv = rv_fetch(w.Rv + lb + lq);
+        o->h[0].wb = lv.mx * (float)in.la;
+        o->h[1].wb = lv.my * (float)in.la;
+        lrank = lv.rank;
+        lroot = lv.root;
+        *lbb = lv.bb;
+    } else {
+        o->h[0].wb = in.wbx;
+        o->h[1].wb = in.wby;
+        lbb->x0 = lbb->x1 = (int16_t)(in.la & 0xffff);
+        lbb->y0 = lbb->y1 = (int16_t)(in.la >> 16);
+    }
+    meta |= kLongOk;
+    o->h[0].fs = o->h[1].fs = in.fs;
+    o->h[0].r = o->h[1].r = in.r;
+    o->pad = 0;
+    o->lk = rk_pack(lrank, lroot);
+    o->lkp = o->lk + (1u << kRankShift);
+    o->bm = (meta & kStepB) ? ~0u : 0u;
+    return meta;
+}
+
+// A long path (task word t) on this wave, from its cursor: returns the task word of the parent path
+// that was parked on its top (to run next), or -1 (parked itself, or completed with nobody waiting).
+__device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut* ob) {
+    const Dims& d = w.d;
+    const int g = t & kFlowIdMask;
+    const int f = g / (int)d.N, j = g - f * (int)d.N;
+    int* curp = w.cur + f * d.N + j;
+    const int lane = threadIdx.x & 63;
+    int q = f_ld(curp);
+    const int top = w.ptop[f * d.N + j];
+    if (q < top) return -1;  // (never: a task is handed out only while its path is not complete)
+    const int64_t lb = f * d.NL;
+    const int h = lane & 1;
+    float v;
+    unsigned K;
+    B4 bb;
+    {
+        float mx, my;
+        int rank, root;
+        flow_start(w, f, q + 1, &mx, &my, &rank, &root, &bb);
+        v = h ? my : mx;
+        K = rk_pack(rank, root);
+    }
+    int cb = 0;
+    OneRec rec;
+    B4 lbb;
+    int meta = flow_resolve(w, lb, q - lane, top, &rec, &lbb);
+    buf[cb][lane] = rec;
+    unsigned chunks = 0, steps = 0;  // anatomy, added once per call
+    auto tally = [&]() {
+        if (lane == 0) {
+            fs_add(FS_LCHUNKS, chunks);
+            fs_add(FS_LSTEPS, steps);
+        }
+    };
+    for (;;) {
+        OneRec nrec;
+        B4 nlbb;
+        const int nmeta = flow_resolve(w, lb, q - 64 - lane, top, &nrec, &nlbb);
+        const unsigned long long blocked = __ballot(!(meta & kLongOk));
+        const unsigned long long tops = __ballot((meta & kLongOk) && (meta & kStepTop));
+        const int fb = blocked ? __ffsll((long long)blocked) - 1 : 64;
+        const int ft = tops ? __ffsll((long long)tops) - 1 : 64;
+        const int finished = ft < fb;
+        const int n = finished ? ft + 1 : fb;
+        ++chunks;
+        steps += n;
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this chunk's LDS records have landed
+        __builtin_amdgcn_wave_barrier();
+        const OneRec* c = buf[cb];
+        auto step = [&](int k, uint4 a, OneHalf b) {  // a = {lk, bm, lkp}, b = {r, wb, fs}
+            v = (float)((double)(v * b.fs + b.wb) * b.r);
+            const unsigned lk = a.x, bm = a.y, lkp = a.z;
+            unsigned eq = (bm & lkp) | (~bm & (K + (1u << kRankShift)));
+            unsigned ne = K > lk ? K : lk;
+            asm volatile("" : "+v"(eq), "+v"(ne));
+            K = (K ^ lk) < (1u << kRankShift) ? eq : ne;
+            OneOut o;
+            o.v = v;
+            o.k = K;
+            ob[2 * k + h] = o;
+        };
+        auto lda = [&](int k) { return *reinterpret_cast<const uint4*>(&c[k]); };
+        int k = 0;
+        uint4 a0 = lda(0), a1 = lda(1), a2 = lda(2), a3 = lda(3);
+        OneHalf b0 = c[0].h[h], b1 = c[1].h[h], b2 = c[2].h[h], b3 = c[3].h[h];
+        for (; k + 4 <= n; k += 4) {
+            const int m = (k + 4) & 63;
+            const uint4 na0 = lda(m), na1 = lda(m + 1), na2 = lda(m + 2), na3 = lda(m + 3);
+            const OneHalf nb0 = c[m].h[h], nb1 = c[m + 1].h[h], nb2 = c[m + 2].h[h], nb3 = c[m + 3].h[h];
+            step(k, a0, b0);
+            step(k + 1, a1, b1);
+            step(k + 2, a2, b2);
+            step(k + 3, a3, b3);
+            a0 = na0, a1 = na1, a2 = na2, a3 = na3;
+            b0 = nb0, b1 = nb1, b2 = nb2, b3 = nb3;
+        }
+        for (; k < n; ++k) step(k, lda(k), c[k].h[h]);
+        B4 obb;
+        {  // bbox: inclusive prefix join over the chunk (lane = step), then the carried box
+            B4 x = lbb;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const B4 y = bb_shfl_up(x, o);
+                if (lane >= o) x = bb_join(x, y);
+            }
+            x = bb_join(x, bb);
+            obb = x;
+            const int src = n > 0 ? n - 1 : 0;
+            const int lo = __shfl((int)((unsigned short)x.x0 | ((unsigned)(unsigned short)x.y0 << 16)), src, 64);
+            const int hi = __shfl((int)((unsigned short)x.x1 | ((unsigned)(unsigned short)x.y1 << 16)), src, 64);
+            if (n > 0) {
+                bb.x0 = (int16_t)(lo & 0xffff);
+                bb.y0 = (int16_t)(lo >> 16);
+                bb.x1 = (int16_t)(hi & 0xffff);
+                bb.y1 = (int16_t)(hi >> 16);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // the chunk's output records are in LDS
+        __builtin_amdgcn_wave_barrier();
+        if (lane < n) {
+            const OneOut sx = ob[2 * lane], sy = ob[2 * lane + 1];
+            const int rank = (int)(sx.k >> kRankShift), root = (int)(sx.k & ((1u << kRankShift) - 1));
+            RepVal* dst = w.Rv + lb + q - lane;
+            if (lane == n - 1 && (finished || n < 64)) {  // the top's record (parent path) or a parked state
+                rv_publish(dst, sx.v, sy.v, rank, root, obb);
+            } else {
+                RepVal o;
+                o.mx = sx.v;
+                o.my = sy.v;
+                o.rank = rank;
+                o.root = root;
+                o.bb = obb;
+                o.pad0 = o.pad1 = 0;
+                *dst = o;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // ob reads done before the next chunk overwrites it
+        __builtin_amdgcn_wave_barrier();
+        if (finished) {  // publish the top: records drained, then the state word; continue its waiter
+            f_drain();
+            int old = 0;
+            if (lane == 0) {
+                f_st(curp, -1);
+                old = __hip_atomic_exchange(w.ready + lb + top, kFlowDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (t & kFlowLong) atomicAdd(ctl + FC_LDONE, 1);
+                fs_add(FS_LDONE, 1);
+                fs_max(FS_T_LONG, fs_now());
+            }
+            old = __shfl(old, 0, 64);
+            tally();
+            return old < kFlowDone ? old : -1;
+        }
+        if (n < 64) {  // blocked at pb on light child lq: park on it unless it completed meanwhile
+            const int pb = q - n;
+            if (n == 0 && w.ord[lb + pb + 1] >= d.N) {  // the state at pb + 1 came from an earlier chunk
+                const float mx = __shfl(v, 0, 64), my = __shfl(v, 1, 64);
+                if (lane == 0)
+                    rv_publish(w.Rv + lb + pb + 1, mx, my, (int)(K >> kRankShift), (int)(K & ((1u << kRankShift) - 1)),
+                               bb);
+            }
+            int parked = 0;
+            if (lane == 0) {
+                f_st(curp, pb);
+                f_drain();
+                const int lq = w.In[lb + pb].lb;
+                const int s0 = f_ld(w.ready + lb + lq);
+                if (s0 != kFlowDone)
+                    parked = atomicCAS(w.ready + lb + lq, s0, t) == s0;
+            }
+            parked = __shfl(parked, 0, 64);
+            if (parked) {
+                if (lane == 0) fs_add(FS_LPARKS, 1);
+                tally();
+                return -1;
+            }
+            q = pb;  // completed meanwhile: re-resolve the chunk from the blocked step
+            __builtin_amdgcn_wave_barrier();
+            meta = flow_resolve(w, lb, q - lane, top, &rec, &lbb, pb);
+            buf[cb][lane] = rec;
+            continue;
+        }
+        q -= 64;
+        cb ^= 1;
+        meta = nmeta;
+        lbb = nlbb;
+        buf[cb][lane] = nrec;
+    }
+}
+
+constexpr int kFlowChunk = 256;  // initial short tasks a wave claims per atomic (its lanes take them in turn)
+
+// Short paths, one per lane, until no lane has one: idle lanes take initial tasks while `grab` holds (from
+// the wave's claimed chunk [*cbp, *cep), refilled by one atomic per kFlowChunk tasks); a lane whose path
+// completes continues the short path parked on its top, and queues a long one (a long worker takes it).
+// inject: a short task handed over by a long path's completion (lane 0 starts with it).
+__device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch, int inject, bool grab, int* cbp,
+                                           int* cep) {
+    const Dims& d = w.d;
+    const int lane = threadIdx.x & 63;
+    const int ntot = ctl[FC_NT] + ctl[FC_NS];
+    int t = (lane == 0) ? inject : -1;  // task word (short: no kFlowLong bit)
+    bool fresh = t >= 0;
+    int q = 0, f = 0;
+    int64_t lb = 0;
+    int* curp = nullptr;
+    RunState s;
+    s.mx = s.my = 0.f;
+    s.rank = s.root = 0;
+    s.bb.x0 = s.bb.y0 = s.bb.x1 = s.bb.y1 = 0;
+    for (int it = 0;; ++it) {
+        if (grab) {
+            unsigned long long idle = __ballot(t < 0);
+            while (idle) {
+                if (*cbp >= *cep) {  // claim the next chunk of the pool
+                    int base = 0;
+                    if (lane == 0) base = atomicAdd(ctl + FC_SHORT_NEXT, kFlowChunk);
+                    base = __shfl(base, 0, 64);
+                    if (base >= ntot) {
+                        grab = false;
+                        break;
+                    }
+                    *cbp = base;
+                    *cep = base + kFlowChunk < ntot ? base + kFlowChunk : ntot;
+                }
+                const int avail = *cep - *cbp;
+                const int r = __popcll(idle & ((1ull << lane) - 1));
+                if (t < 0 && r < avail) {
+                    t = flow_short_task(w, ctl, *cbp + r);
+                    fresh = true;
+                }
+                const int took = __popcll(idle) < avail ? __popcll(idle) : avail;
+                *cbp += took;
+                idle = __ballot(t < 0);
+            }
+        }
+        if (fresh) {  // a new path on this lane: its cursor and the state below it
+            fresh = false;
+            f = t / (int)d.N;
+            const int j = t - f * (int)d.N;
+            curp = w.cur + f * d.N + j;
+            q = f_ld(curp);
+            lb = f * d.NL;
+            flow_start(w, f, q + 1, &s.mx, &s.my, &s.rank, &s.root, &s.bb);
+        }
+        if (!__ballot(t >= 0)) break;
+        if (it >= (1 << 26)) {  // (bounded: never reached by a correct run)
+            f_st(ctl + FC_ERR, 1);
+            break;
+        }
+        if (t < 0) continue;
+        const StepIn in = w.In[lb + q];
+        float wbx = in.wbx, wby = in.wby;
+        int lrank = 0, lroot = in.lb;
+        B4 lbb;
+        if (in.meta & kStepDyn) {
+            const int lq = in.lb;
+            int st = f_ld(w.ready + lb + lq);
+            if (st != kFlowDone) {  // park on the light child: publish the state below q, the cursor
+                if (w.ord[lb + q + 1] >= d.N) rv_publish(w.Rv + lb + q + 1, s.mx, s.my, s.rank, s.root, s.bb);
+                f_st(curp, q);
+                f_drain();
+                st = f_ld(w.ready + lb + lq);
+                if (st != kFlowDone && atomicCAS(w.ready + lb + lq, st, t) == st) {
+                    t = -1;
+                    continue;
+                }
+            }
+            const RepVal lv = rv_fetch(w.Rv + lb + lq);
+            wbx = lv.mx * (float)in.la;
+            wby = lv.my * (float)in.la;
+            lrank = lv.rank;
+            lroot = lv.root;
+            lbb = lv.bb;
+        } else {
+            lbb.x0 = lbb.x1 = (int16_t)(in.la & 0xffff);
+            lbb.y0 = lbb.y1 = (int16_t)(in.la >> 16);
+        }
+        step_merge(s, in.fs, wbx, wby, in.r, in.meta, lrank, lroot, lbb);
+        if (in.meta & kStepTop) {  // path complete: publish its top, then continue its waiter
+            rv_publish(w.Rv + lb + q, s.mx, s.my, s.rank, s.root, s.bb);
+            f_st(curp, -1);
+            f_drain();
+            const int old = __hip_atomic_exchange(w.ready + lb + q, kFlowDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            t = -1;
+            if (old < kFlowDone) {
+                if (old & kFlowLong) {
+                    flow_push(w, ctl, epoch, old);
+                    fs_add(FS_PUSH, 1);
+                } else {
+                    t = old;
+                    fresh = true;
+                }
+            }
+            continue;
+        }
+        RepVal o;
+        o.mx = s.mx;
+        o.my = s.my;
+        o.rank = s.rank;
+        o.root = s.root;
+        o.bb = s.bb;
+        o.pad0 = o.pad1 = 0;
+        w.Rv[lb + q] = o;
+        --q;
+    }
+}
+
+// A long worker's next task: the initial long pool first, then a ticket of the long-path queue, whose
+// slot its pusher fills (tickets are taken only by waiting long workers: no CAS, no herd on the head).
+// -1: every long path completed (the ticket's slot will never be filled), or a wait gave up.
+__device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int nl) {
+    const int lane = threadIdx.x & 63;
+    int t = -1;
+    if (lane == 0) {
+        if (f_ld(ctl + FC_LONG_NEXT) < nl) {
+            const int i = atomicAdd(ctl + FC_LONG_NEXT, 1);
+            if (i < nl) t = flow_long_task(w, ctl, i);
+        }
+        if (t < 0) {
+            const int h = atomicAdd(ctl + FC_QHEAD, 1);
+            for (int spin = 0;; ++spin) {
+                const unsigned long long v = f_ld64(w.bw + h);
+                if ((unsigned)(v >> 32) == epoch) {
+                    t = (int)(unsigned)v;
+                    break;
+                }
+                if ((spin & 15) == 15 && f_ld(ctl + FC_LDONE) >= nl) break;  // nothing more will come
+                if (spin >= (1 << 26)) {
+                    f_st(ctl + FC_ERR, 1);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(16);
+            }
+        }
+    }
+    return __shfl(t, 0, 64);
+}
+
+// The batch's whole replay. One wave per workgroup, persistent. Workgroups [0, nlong) are long workers:
+// they run long paths (initial pool, then queue tickets) following their completions' long waiters, and
+// a short waiter as a one-lane short round; they leave when every long path completed. The others are
+// short workers: rounds of short paths from the initial pool; they leave when it is empty and their
+// lanes are done (short paths parked on a path that completes later are continued by its completer).
+__global__ __launch_bounds__(64) void k_replay_flow(Ws w, int* ctl, unsigned epoch, int nlong) {
+    __shared__ OneRec buf[2][64];
+    __shared__ OneOut ob[128];
+    const int lane = threadIdx.x & 63;
+    const int nl = ctl[FC_NL];
+    int cb = 0, ce = 0;  // this wave's claimed, not yet started initial short tasks
+    if (lane == 0) fs_min(FS_T0, fs_now());
+    if ((int)blockIdx.x < nlong) {
+        __builtin_amdgcn_s_setprio(3);  // the chains go first in their SIMD's arbitration
+        for (int it = 0; it < (1 << 26); ++it) {
+            int t = flow_next_long(w, ctl, epoch, nl);
+            if (t < 0) break;
+            const unsigned long long t1 = fs_now();
+            while (t >= 0) {
+                if (lane == 0) fs_add(FS_LRUNS, 1);
+                const int nx = flow_long(w, ctl, t, buf, ob);
+                if (nx >= 0 && !(nx & kFlowLong)) {  // a short waiter: a one-lane short round (and its waiters)
+                    if (lane == 0) fs_add(FS_INJECT, 1);
+                    flow_short(w, ctl, epoch, nx, false, &cb, &ce);
+                    break;
+                }
+                t = nx;
+            }
+            if (lane == 0) fs_add(FS_LTICKS, fs_now() - t1);
+        }
+    } else {
+        const unsigned long long t1 = fs_now();
+        flow_short(w, ctl, epoch, -1, true, &cb, &ce);
+        if (lane == 0) {
+            fs_add(FS_SROUNDS, 1);
+            fs_add(FS_STICKS, fs_now() - t1);
+            fs_max(FS_T_SHORT, fs_now());
+        }
+    }
+    if (lane == 0) fs_max(FS_T_EXIT, fs_now());
+}
+
+// counter C_FLOWERR of frame 0 = a bounded wait of the launch gave up (dofs_batch_counters)
+__global__ void k_flow_report(Ws w, const int* ctl) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && ctl[FC_ERR]) w.C(0)[C_FLOWERR] = 1;
+}
+
+}  // namespace dofs

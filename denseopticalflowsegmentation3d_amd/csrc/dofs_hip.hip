@@ -740,6 +740,10 @@ __global__ __launch_bounds__(192) void k_replay_long(Ws w, int round, int wait) 
     for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path(w, f, jj, round, can_wait, sh);
 }
 
+}  // namespace dofs
+#include "dofs_dataflow.h"
+namespace dofs {
+
 
 // ---------------------------------------------------------------------------------------------
 // K3 deep levels: once the divide-and-conquer block size is kDeepS merges, every remaining level of
@@ -2635,6 +2639,7 @@ struct HipBackend {
         for (auto e : events) (void)hipEventDestroy(e);
         for (auto& t : tmps)
             if (t.p) (void)hipFree(t.p);
+        if (flow_ctl) (void)hipFree(flow_ctl);
         for (auto st : streams) (void)hipStreamDestroy(st);
         if (own) (void)hipStreamDestroy(own);
     }
@@ -3099,6 +3104,51 @@ struct HipBackend {
         }();
         return n;
     }
+    // K5 as one dataflow launch (dofs_dataflow.h); false: run the round launches (DOFS_REPLAY_FLOW=0, or a
+    // batch whose task ids would not fit 30 bits)
+    int* flow_ctl = nullptr;
+    size_t flow_ctl_n = 0;
+    unsigned flow_epoch = 0;
+    static int flow_grid() {  // short-path workgroups (one wave each) of the persistent replay launch
+        static const int g = [] {
+            const char* e = getenv("DOFS_FLOW_GRID");
+            return e && atoi(e) > 0 ? atoi(e) : 2048;
+        }();
+        return g;
+    }
+    static int flow_long_workers() {  // waves that run long paths (the rest of the grid runs short ones)
+        static const int g = [] {
+            const char* e = getenv("DOFS_FLOW_LONG");
+            return e && atoi(e) > 0 ? atoi(e) : 256;
+        }();
+        return g;
+    }
+    bool replay_flow(const Ws& w) {
+        static const bool on = [] {
+            const char* e = getenv("DOFS_REPLAY_FLOW");
+            return !(e && e[0] == '0');
+        }();
+        if (!on || (int64_t)w.d.B * w.d.N >= (int64_t)kFlowLong) return false;
+        const size_t n = FC_HDR + 3 * (size_t)(w.d.B + 1);
+        if (n > flow_ctl_n) {
+            if (flow_ctl) {
+                note(hipDeviceSynchronize(), "hipDeviceSynchronize");  // a launch in flight may still use it
+                free(flow_ctl);
+            }
+            flow_ctl = (int*)alloc(sizeof(int) * n);
+            flow_ctl_n = flow_ctl ? n : 0;
+            if (!flow_ctl) return false;
+        }
+        flow_epoch = flow_epoch % 0x30000000u + 1;  // queue-slot tag of this launch (never 0)
+        hipLaunchKernelGGL(k_flow_prep, dim3(1), dim3(64), 0, stream, w, flow_ctl);
+        timed("k_replay_flow", [&] {
+            hipLaunchKernelGGL(k_replay_flow, dim3((unsigned)(flow_grid() + flow_long_workers())), dim3(64), 0, stream, w,
+                               flow_ctl, flow_epoch, flow_long_workers());
+        });
+        hipLaunchKernelGGL(k_flow_report, dim3(1), dim3(64), 0, stream, w, flow_ctl);
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_replay_flow launch");
+        return true;
+    }
     void replay_long(const Ws& w, int round) {
         static const bool one = [] {  // DOFS_LONG_WAVES=3: the three-wave form (measured ~1.5 % slower)
             const char* e = getenv("DOFS_LONG_WAVES");
@@ -3247,6 +3297,15 @@ extern "C" int dofs_debug_krt_timing(double* out_us, int n) {
     return 16;
 }
 #endif
+
+// Measurement: the last dataflow replay launch's anatomy (dofs_dataflow.h FlowStat), after a sync.
+extern "C" int dofs_debug_flow_stats(unsigned long long* out, int n) {
+    unsigned long long v[dofs::FS_N * dofs::kFsStride] = {0};
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(dofs::g_fs), sizeof(v)) != hipSuccess) return -1;
+    for (int i = 0; i < n && i < dofs::FS_N; ++i) out[i] = v[i * dofs::kFsStride];
+    return dofs::FS_N;
+}
 
 using DofsBackend = dofs::HipBackend;
 #include "dofs_cabi.inc.h"

@@ -385,8 +385,9 @@ struct Pipeline {
             path_init();
         }
         be.mark(5);
-        // K5 bottom-up replay of Forest::merge along heavy paths
-        const int RR = ceil_log2(N) + 2;
+        // K5 bottom-up replay of Forest::merge along heavy paths: one dataflow launch (HIP), else rounds
+        const bool flow = !(skip_mask & 3) && be.replay_flow(w);
+        const int RR = flow ? 0 : ceil_log2(N) + 2;
         // short paths: round r advances the paths parked in round r - 1 (lists ping-pong between two
         // pixel-sized buffers whose owners, the MST passes, are done)
         int* park[2] = {w.off, w.comp};
