@@ -106,8 +106,9 @@ def parse(argv=None):
     ap.add_argument("--no-stages", action="store_true", help="skip the per-stage event timing pass")
     ap.add_argument("--no-h2d", action="store_true", help="skip the with-H2D (host input) pass")
     ap.add_argument("--probe", default=",".join(PROBES), help="kernels timed with device events (comma list)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02", "pmc_kernels.json"),
-                    help="PMC summary JSON (tools/pmc_kernels.py via tools/pmc_round.sh) for the roofline traffic")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03", "pmc_kernels.json"),
+                    help="PMC summary JSON (tools/pmc_kernels.py via tools/pmc_round.sh) for the roofline traffic; "
+                         "used only when its lib_sha256 is the loaded library's")
     ap.add_argument("--cpu-worker", nargs=4, metavar=("OPT", "H", "W", "SEED"), help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -321,11 +322,18 @@ def main(argv=None):
         raise RuntimeError("the dataflow replay gave up a bounded wait: results of the timed batches are invalid")
     tiles = ctx.tile_pixels(chunks[-1][1])
     recs = ctx.records(chunks[-1][1])
-    pmc = {}
+    pmc, pmc_note = {}, "no PMC summary"
     if a.pmc and os.path.exists(a.pmc):
+        import hashlib
         pj = json.load(open(a.pmc))
-        if pj.get("batch") == B and pj.get("height", H) == H and pj.get("width", W) == W:
+        sha = hashlib.sha256(open(runtime.LIB_PATH, "rb").read()).hexdigest()
+        if pj.get("lib_sha256") != sha:  # counters of another build: stale, never reported
+            pmc_note = f"{os.path.relpath(a.pmc, ROOT)} is for another build of libdofs_hip.so: traffic dropped"
+        elif pj.get("batch") == B and pj.get("height", H) == H and pj.get("width", W) == W:
             pmc = pj.get("kernels", {})
+            pmc_note = f"{os.path.relpath(a.pmc, ROOT)} (lib_sha256 {sha[:12]} matches the loaded library)"
+        else:
+            pmc_note = f"{os.path.relpath(a.pmc, ROOT)} is for another batch shape: traffic dropped"
     batches = a.steps * len(chunks)
     kern = []
     for name, (ms, launches) in probes.items():
@@ -378,12 +386,14 @@ def main(argv=None):
     if main_k:
         roof = {"bound": "hbm", "achieved": main_k["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": main_k["frac"], "traffic": main_k.get("traffic"),
-                "traffic_source": (os.path.relpath(a.pmc, ROOT) + " (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, "
-                                   "tools/pmc_round.sh)") if main_k.get("traffic") else None,
+                "traffic_source": pmc_note + ("; rocprofv3 FETCH_SIZE/WRITE_SIZE passes, tools/pmc_round.sh"
+                                              if main_k.get("traffic") else ""),
                 "kernel": ROOF_KERNEL,
                 "launches": main_k["launches"], "avg_launch_us": main_k["avg_launch_us"],
                 "alg_bytes_per_launch": main_k["alg_bytes_per_launch"],
                 "alg_bytes_per_unit": main_k["alg_bytes_per_unit"],
+                "dominant": ({k: kern[0].get(k) for k in ("kernel", "ms_per_batch", "share_of_step", "achieved", "frac",
+                                                          "traffic", "traffic_over_alg")} if kern else None),
                 "top_kernels_by_time": kern[:3],
                 "path_input_roofline_frac": round(frames_per_step * a.steps * N * 8 / world / elapsed / 1e9
                                                   / HBM_PEAK_GBS, 8)}
@@ -428,7 +438,9 @@ def main(argv=None):
                             f"{W}x{H} synthetic flow, full segment + lifting_3d (BASELINE config 3 shape)"),
                "frames_per_step": frames_per_step, "frames_per_gpu_per_batch": B,
                "frames_per_sec": round(frames_per_step * a.steps / elapsed, 3),
-               "parallelism": f"frame-parallel x{world}", "snapshots_frame0": int(len(res.snapshots)),
+               "parallelism": f"frame-parallel x{world}", "workspaces": ctx.batch_slots(),
+               "workspace_mb_per_frame": round(ctx.workspace_bytes() / B / 1e6, 1),
+               "snapshots_frame0": int(len(res.snapshots)),
                "candidates_frame0": int(res.stats["n_candidates"])}
         out = {
             "metric": "Mpixels/sec segment+lifting_3d @1080p",

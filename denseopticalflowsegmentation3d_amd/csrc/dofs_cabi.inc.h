@@ -199,6 +199,11 @@ int32_t dofs_batch_frames(dofs_ctx* ctx) {
 
 int32_t dofs_batch_slots(dofs_ctx* ctx) { return ctx ? ctx->nslots : -1; }
 
+int64_t dofs_workspace_bytes(dofs_ctx* ctx) {
+    if (!ctx || !ctx->have_batch()) return 0;
+    return (int64_t)ctx->pipe(ctx->last_slot()).base_bytes;
+}
+
 int32_t dofs_profile(dofs_ctx* ctx, int32_t enable) {
     if (!ctx) return DOFS_ERR_INVALID_ARG;
     ctx->be.profile(enable != 0);

@@ -52,6 +52,7 @@ enum FlowCtlIdx {
     FC_NL = 7 * kFlowLine,          // read-only after k_flow_prep: pool sizes (long, tiny, other short)
     FC_NT = FC_NL + 1,
     FC_NS = FC_NL + 2,
+    FC_QCAP = FC_NL + 3,            // queue slots: B * N (w.bw); tickets and pushes stay below it
     FC_HDR = 8 * kFlowLine,         // then pl[B + 1], pt[B + 1], ps[B + 1]
 };
 constexpr int kFlowSpin = 1 << 22;  // polls of a queue slot before giving up (s_sleep between)
@@ -187,10 +188,15 @@ __global__ void k_flow_prep(Ws w, int* ctl) {
     ctl[FC_NL] = sl;
     ctl[FC_NT] = st;
     ctl[FC_NS] = ss;
+    ctl[FC_QCAP] = (int)(B * w.d.N);
 }
 
 __device__ inline void flow_push(const Ws& w, int* ctl, unsigned epoch, int t) {
     const int s = atomicAdd(ctl + FC_QTAIL, 1);
+    if (s >= ctl[FC_QCAP]) {  // (never: a push resumes a path parked on a completed top, < B * N of them)
+        f_st(ctl + FC_ERR, 1);
+        return;
+    }
     f_st64(w.bw + s, ((unsigned long long)epoch << 32) | (unsigned)t);
 }
 // Resolve position p of a long path (one lane per step, as one_resolve); light children through the
@@ -516,8 +522,13 @@ __device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch
 }
 
 // A long worker's next task: the initial long pool first, then a ticket of the long-path queue, whose
-// slot its pusher fills (tickets are taken only by waiting long workers: no CAS, no herd on the head).
-// -1: every long path completed (the ticket's slot will never be filled), or a wait gave up.
+// slot its pusher fills (tickets are taken only by long workers, and only while pushes are pending, so
+// there is no CAS herd on the head and at most the racing workers' tickets run ahead of the pushes).
+// -1: every long path completed (a ticket's slot that will never be filled), or a wait gave up. A slot
+// is accepted only with this launch's tag and a long task word of the batch: slots never written in
+// this launch hold Borůvka minima or older tags, which neither passes (kFlowEpochs < the high word of
+// any weight the MST stores there).
+constexpr unsigned kFlowEpochs = 0xFFFFF;
 __device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int nl) {
     const int lane = threadIdx.x & 63;
     int t = -1;
@@ -526,20 +537,34 @@ __device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int 
             const int i = atomicAdd(ctl + FC_LONG_NEXT, 1);
             if (i < nl) t = flow_long_task(w, ctl, i);
         }
-        if (t < 0) {
-            const int h = atomicAdd(ctl + FC_QHEAD, 1);
-            for (int spin = 0;; ++spin) {
-                const unsigned long long v = f_ld64(w.bw + h);
-                if ((unsigned)(v >> 32) == epoch) {
-                    t = (int)(unsigned)v;
-                    break;
+        for (int spin = 0; t < 0; ++spin) {
+            if (f_ld(ctl + FC_LDONE) >= nl) break;  // every long path completed: nothing more will come
+            if (spin >= (1 << 26)) {
+                f_st(ctl + FC_ERR, 1);
+                break;
+            }
+            if (f_ld(ctl + FC_QHEAD) < f_ld(ctl + FC_QTAIL)) {
+                const int h = atomicAdd(ctl + FC_QHEAD, 1);
+                if (h >= ctl[FC_QCAP]) break;  // (never filled)
+                const long long nframe = w.d.N;
+                for (int s2 = 0;; ++s2) {
+                    const unsigned long long v = f_ld64(w.bw + h);
+                    const int c = (int)(unsigned)v;
+                    if ((unsigned)(v >> 32) == epoch && c >= 0 && (c & kFlowLong) &&
+                        (long long)(c & kFlowIdMask) < nframe * w.d.B) {
+                        t = c;
+                        break;
+                    }
+                    if ((s2 & 15) == 15 && f_ld(ctl + FC_LDONE) >= nl) break;
+                    if (s2 >= (1 << 26)) {
+                        f_st(ctl + FC_ERR, 1);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(16);
                 }
-                if ((spin & 15) == 15 && f_ld(ctl + FC_LDONE) >= nl) break;  // nothing more will come
-                if (spin >= (1 << 26)) {
-                    f_st(ctl + FC_ERR, 1);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(16);
+                if (t < 0) break;  // the ticket's wait ended without a task: all long paths are done
+            } else {
+                __builtin_amdgcn_s_sleep(32);
             }
         }
     }

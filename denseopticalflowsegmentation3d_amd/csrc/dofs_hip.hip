@@ -3112,7 +3112,7 @@ struct HipBackend {
     static int flow_grid() {  // short-path workgroups (one wave each) of the persistent replay launch
         static const int g = [] {
             const char* e = getenv("DOFS_FLOW_GRID");
-            return e && atoi(e) > 0 ? atoi(e) : 2048;
+            return e && atoi(e) > 0 ? atoi(e) : 1024;
         }();
         return g;
     }
@@ -3139,7 +3139,7 @@ struct HipBackend {
             flow_ctl_n = flow_ctl ? n : 0;
             if (!flow_ctl) return false;
         }
-        flow_epoch = flow_epoch % 0x30000000u + 1;  // queue-slot tag of this launch (never 0)
+        flow_epoch = flow_epoch % kFlowEpochs + 1;  // queue-slot tag of this launch (never 0)
         hipLaunchKernelGGL(k_flow_prep, dim3(1), dim3(64), 0, stream, w, flow_ctl);
         timed("k_replay_flow", [&] {
             hipLaunchKernelGGL(k_replay_flow, dim3((unsigned)(flow_grid() + flow_long_workers())), dim3(64), 0, stream, w,

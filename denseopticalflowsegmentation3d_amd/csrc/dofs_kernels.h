@@ -777,7 +777,7 @@ DOFS_HD inline int uf_union_hooked(int* P, int a, int b) {
 DOFS_HD inline void seq_set_size(const Ws& w, int f, int j, int sz) {
     const int64_t o = f * w.d.NL + w.d.N + j;
     w.SZ[o] = sz;
-    ((int*)(w.P + o))[1] = sz;
+    if (w.P) ((int*)(w.P + o))[1] = sz;
 }
 
 // pointer-jumping word: (ancestor, offset sum) packed
@@ -803,8 +803,8 @@ struct KLabelInit {  // pixel sizes, the root's size / jump word / path-top flag
             }
             return;
         }
-        w.MX[o] = 0;
-        w.CS[o] = 0;
+        if (w.MX) w.MX[o] = 0;  // (the global-kernel KRT's arrays exist only where it runs)
+        if (w.CS) w.CS[o] = 0;
         int sz = 0;
         if (x < d.N) {
             sz = 1;
@@ -815,7 +815,7 @@ struct KLabelInit {  // pixel sizes, the root's size / jump word / path-top flag
             w.J[o] = jump_pack(-1, 0);
             w.lite[o] = 1;
         }
-        w.P[o] = (unsigned long long)(unsigned)sz << 32;  // link word epoch 0: a root at every depth
+        if (w.P) w.P[o] = (unsigned long long)(unsigned)sz << 32;  // link word epoch 0: a root at every depth
     }
 };
 

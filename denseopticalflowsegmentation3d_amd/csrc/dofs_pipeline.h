@@ -80,7 +80,11 @@ struct Pipeline {
         return d;
     }
 
-    bool fits(const Dims& d) const { return base && cap.B >= d.B && cap.N == d.N && cap.W == d.W; }
+    bool layout_packed = false;  // the layout treats key_out as dead (batch-wide sort): batches must sort packed
+    bool fits(const Dims& d) const {
+        const bool packed = Backend::mst_packed(std::max<int64_t>(d.M, 1), d.B, ceil_log2(4 * d.N));
+        return base && cap.B >= d.B && cap.N == d.N && cap.W == d.W && (packed || !layout_packed);
+    }
 
     // Carve every buffer from one allocation (grow-only). Returns false on allocation failure.
     bool reserve(const Dims& d) {
@@ -98,6 +102,10 @@ struct Pipeline {
         return true;
     }
 
+    // One allocation per workspace. Phase A (graph) runs before phase B (replay + scoring) of the same
+    // batch and the next batch on this workspace starts only after both, so the phase-B arrays live in
+    // regions phase A is done with (first fit; a fresh block when nothing fits), and the arrays of the
+    // global-kernel KRT (P, CS, MX, own) exist only where that KRT runs (DOFS_KRT_DNC, the emulator).
     size_t layout(const Dims& d, char* p) {
         size_t off = 0;
         auto take = [&](size_t bytes) {
@@ -107,31 +115,59 @@ struct Pipeline {
             return r;
         };
         const int64_t B = d.B, N = d.N, M = std::max<int64_t>(d.M, 1), NL = d.NL;
-        w.tmp = (F2*)take(sizeof(F2) * B * N);
+        const bool words = krt_dnc || Backend::kKrtLabelWords;
+        struct Region {
+            char* p;
+            size_t n;
+        };
+        std::vector<Region> dead;  // free for phase B: dead once phase A ended
+        auto take_dead = [&](size_t bytes) {
+            char* r = take(bytes);
+            dead.push_back(Region{r, bytes});
+            return r;
+        };
+        auto take_b = [&](size_t bytes) {  // a phase-B array: first fit in a dead region
+            for (Region& g : dead) {
+                if (g.n >= bytes) {
+                    char* r = g.p;
+                    const size_t used = (bytes + 255) & ~(size_t)255;
+                    g.p = g.p ? g.p + used : nullptr;
+                    g.n = g.n > used ? g.n - used : 0;
+                    return r;
+                }
+            }
+            return take(bytes);
+        };
+        w.tmp = (F2*)take_dead(sizeof(F2) * B * N);  // row blur, Borůvka records
         w.blur = (F2*)take(sizeof(F2) * B * N);
-        w.comp = (int*)take(4 * B * N);
-        w.bw = (unsigned long long*)take(8 * B * N);
-        w.bi = (unsigned*)take(4 * B * N);
+        w.comp = (int*)take(4 * B * N);  // Borůvka labels; the round-based replay's park lists
+        w.bw = (unsigned long long*)take(8 * B * N);  // Borůvka minima; the dataflow replay's queue
+        w.bi = (unsigned*)take_dead(4 * B * N);
         w.uf = (int*)take(4 * B * N);
         w.lposr = w.uf;  // the MST's union-find is dead once the KRT starts
-        w.mstbits = (int*)take(4 * B * N);
-        w.cnt = (int*)take(4 * B * N);
-        w.off = (int*)take(4 * B * N);
+        w.mstbits = (int*)take_dead(4 * B * N);
+        w.cnt = (int*)take_dead(4 * B * N);
+        w.off = (int*)take(4 * B * N);  // park lists (round-based replay)
         w.key_in = (unsigned long long*)take(8 * B * M);
-        w.val_in = (unsigned*)take(4 * B * M);
-        w.key_out = (unsigned long long*)take(8 * B * M);
-        w.val_out = (unsigned*)take(4 * B * M);
+        w.hls = w.key_in;  // the KRT's children sizes for KPathInit: the sort input is dead by then
+        w.val_in = (unsigned*)take_dead(4 * B * M);
+        // the sorted weights: per frame (read by dofs_events) unless the whole batch is sorted at once
+        // (run_a: the same predicate), when they are in global order and dead after the sort
+        const bool packed = Backend::mst_packed(M, (int)B, ceil_log2(4 * N));
+        layout_packed = packed;
+        w.key_out = (unsigned long long*)(packed ? take_dead(8 * B * M) : take(8 * B * M));
+        w.val_out = (unsigned*)take_dead(4 * B * M);
         w.EU = (int*)take(4 * B * M);
         w.EV = (int*)take(4 * B * M);
         w.lu = (int*)take(4 * B * M);
         w.lv = (int*)take(4 * B * M);
-        w.own = (int*)take(4 * B * M);
+        w.own = words ? (int*)take(4 * B * M) : nullptr;
         w.hlB = (unsigned char*)take(B * M);
-        w.P = (unsigned long long*)take(8 * B * NL);
-        w.CS = (int*)take(4 * B * NL);
-        w.MX = (int*)take(4 * B * NL);
+        w.P = words ? (unsigned long long*)take(8 * B * NL) : nullptr;
+        w.CS = words ? (int*)take(4 * B * NL) : nullptr;
+        w.MX = words ? (int*)take(4 * B * NL) : nullptr;
         w.SZ = (int*)take(4 * B * NL);
-        w.J = (unsigned long long*)take(8 * B * NL);
+        w.J = (unsigned long long*)take_dead(8 * B * NL);  // preorder jump words
         w.lite = (unsigned char*)take(B * NL);
         w.pre = (int*)take(4 * B * NL);
         w.ord = (int*)take(4 * B * NL);
@@ -145,15 +181,15 @@ struct Pipeline {
         w.ptop = (int*)take(4 * B * N);
         w.list_short = (int*)take(4 * B * N);
         w.list_long = (int*)take(4 * B * N);
-        w.sevent = (int*)take(4 * B * N);
-        w.sbest = (unsigned long long*)take(8 * B * N);
-        w.sflag = (int*)take(4 * B * N);
-        w.soff = (int*)take(4 * B * N);
-        w.labels = (int*)take(4 * B * N);
-        w.cand = (int*)take(4 * B * M);
-        w.cscore = (double*)take(8 * B * M);
-        w.hls = reinterpret_cast<unsigned long long*>(w.cscore);  // dead until KLift
-        w.seg = (int*)take(4 * B * 2 * d.P2);
+        // phase B only (written by KFilter .. KLabel, read by them and by the result accessors)
+        w.seg = (int*)take_b(4 * B * 2 * d.P2);
+        w.sbest = (unsigned long long*)take_b(8 * B * N);
+        w.cscore = (double*)take_b(8 * B * M);  // (largest first: the 4-byte arrays fill the rest)
+        w.sevent = (int*)take_b(4 * B * N);
+        w.sflag = (int*)take_b(4 * B * N);
+        w.soff = (int*)take_b(4 * B * N);
+        w.labels = (int*)take_b(4 * B * N);
+        w.cand = (int*)take_b(4 * B * M);
         w.snaps = (dofs_snapshot*)take(sizeof(dofs_snapshot) * B * snap_cap);
         w.recs = (dofs_box_record*)take(sizeof(dofs_box_record) * B * snap_cap);
         w.ctr = (int*)take(4 * B * kCounters);

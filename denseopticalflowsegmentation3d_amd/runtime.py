@@ -100,6 +100,9 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_batch_count.restype = C.c_int64
     L.dofs_batch_slots.argtypes = [C.c_void_p]
     L.dofs_batch_slots.restype = C.c_int32
+    if hasattr(L, "dofs_workspace_bytes"):
+        L.dofs_workspace_bytes.argtypes = [C.c_void_p]
+        L.dofs_workspace_bytes.restype = C.c_int64
     L.dofs_profile.argtypes = [C.c_void_p, C.c_int32]
     L.dofs_profile.restype = C.c_int32
     L.dofs_profile_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), _ip]
@@ -410,6 +413,10 @@ class Dofs:
 
     def batch_count(self) -> int:
         return int(self.lib.dofs_batch_count(self.ctx))
+
+    def workspace_bytes(self) -> int:
+        """Device bytes of the last batch's workspace."""
+        return int(self.lib.dofs_workspace_bytes(self.ctx))
 
     def batch_slots(self) -> int:
         """Batches whose results stay readable (read batch k after submitting k + slots - 1)."""

@@ -279,6 +279,8 @@ int32_t dofs_batch_frames(dofs_ctx* ctx);
 /* Number of batch workspaces (batches whose results stay readable; a caller that reads batch k's
  * results after submitting batch k + slots - 1 keeps every stage of the pipeline busy). */
 int32_t dofs_batch_slots(dofs_ctx* ctx);
+/* Device bytes of the last batch's workspace (one of dofs_batch_slots() such workspaces). */
+int64_t dofs_workspace_bytes(dofs_ctx* ctx);
 
 /* The last batch's per-frame counter blocks (B x 64 int32: candidates, snapshots, MST edges, ... and
  * at 16 + r the flag "Borůvka round r found a cross-component edge"), copied to host; waits for the

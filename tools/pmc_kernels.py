@@ -30,6 +30,7 @@ PATTERN = {
     "KOrd": "stream",            # jump words by node; the ord[] scatter is random 4-B stores
     "k_krt_fused": "random",     # union-find records, label / seed stores
     "k_replay_long1": "stream",  # StepIn / RepVal records by preorder position (64-step chunks)
+    "k_replay_flow": "stream",   # StepIn / RepVal by preorder position (lanes: one path each; waves: 64-step chunks)
     "KJump": "random",
     "KPathInit": "random",
     "KLift": "random",
@@ -103,7 +104,12 @@ def main():
                 e["l2_hit_rate"] = h / (h + m)
         res[k] = e
     batch = int(sys.argv[4]) if len(sys.argv) > 4 else 96
-    print(json.dumps({"batch": batch, "height": 1080, "width": 1920, "kernels": res}, indent=1))
+    # the library the counters were taken from: bench.py uses `traffic` only while this hash matches
+    lib = os.environ.get("DOFS_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                     "denseopticalflowsegmentation3d_amd", "_build", "libdofs_hip.so")
+    import hashlib
+    sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+    print(json.dumps({"batch": batch, "height": 1080, "width": 1920, "lib_sha256": sha, "kernels": res}, indent=1))
 
 
 if __name__ == "__main__":

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 O=gpurun_out/pmc
 rm -rf $O; mkdir -p $O
 B=${B:-96}
-KS=${KS:-k_boruvka_min4,k_krt_fused,k_replay_long1,k_pre_sweep,KPathInit,KLift,KFilter,k_blur_fused}
+KS=${KS:-k_boruvka_min4,k_krt_fused,k_replay_flow,k_pre_sweep,KPathInit,KLift,KFilter,k_blur_fused}
 BENCH="bench.py --steps 2 --warmup 1 --batch $B --cpu-frames 0 --no-stages --no-h2d"
 run() {  # name cmd...
     local name=$1; shift
