@@ -96,7 +96,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=96, help="frames per GPU per step (--frames: per batch)")
+    ap.add_argument("--batch", type=int, default=112, help="frames per GPU per step (--frames: per batch)")
     ap.add_argument("--frames", type=int, default=0, help="fixed job of F frames over all GPUs (config 4: 512)")
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--width", type=int, default=1920)

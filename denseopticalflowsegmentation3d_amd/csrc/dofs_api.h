@@ -317,6 +317,14 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     }
     if (!P.fits(d) && cx->used[s]) be.event_sync(cx->evDone[s]);  // reallocation: batch id-2 must be done
     if (!P.reserve(d)) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    // the workspaces no batch has used yet take this shape now: their first batches then allocate
+    // nothing (a hipMalloc of tens of GB takes seconds), whatever stream work follows
+    for (int k = 0; k < cx->nslots; ++k) {
+        Pipeline<Backend>& Q = cx->pipe(k);
+        if (k == s || cx->used[k] || Q.fits(d)) continue;
+        Q.snap_cap = cx->snap_cap;
+        if (!Q.reserve(d)) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
+    }
     P.set_params(prm, persp, inv, inv_upper);
 
     void* caller = be.cur_stream();

@@ -2945,15 +2945,16 @@ struct HipBackend {
             launch(w.d.B, w.d.N, KSeqInitRec{reinterpret_cast<SeqRec*>(w.In), 2 * w.d.NL});
             // persistent workgroups: the frames' sweeps plus `extra` LDS-KRT workers (DOFS_FUSED_EXTRA),
             // at most one per CU. A workgroup holds a whole CU (151 KB of LDS, all VGPRs), so the
-            // other stream's replay cannot run beside it: by default 1/8 of the CUs stay free for it
-            // (measured at B = 96: 224 workgroups 982 Mpix/s, 256 workgroups 957, 160 workgroups 909)
+            // other stream's replay cannot run beside it: by default 1/16 of the CUs stay free for it
+            // (round 3, dataflow replay, B = 96: 240 workgroups 1,449 Mpix/s, 224 1,425; round 2's
+            // round-based replay needed 1/8: 224 workgroups 982, 256 957, 160 909)
             static const int extra = [] {
                 const char* e = getenv("DOFS_FUSED_EXTRA");
                 return e ? atoi(e) : -1;
             }();
             int dev_cus = 256;
             (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, device);
-            const int cap = extra < 0 ? dev_cus - dev_cus / 8 : dev_cus;
+            const int cap = extra < 0 ? dev_cus - dev_cus / 16 : dev_cus;
             const int nwg = std::max(1, std::min(cap, extra < 0 ? cap : w.d.B + extra));
             timed("k_krt_fused", [&] {
                 hipLaunchKernelGGL(k_krt_fused, dim3((unsigned)nwg), dim3(kDeepT), 0, stream, w, w.ctr + C_PROG);
