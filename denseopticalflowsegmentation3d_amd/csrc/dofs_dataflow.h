@@ -53,6 +53,7 @@ enum FlowCtlIdx {
     FC_NT = FC_NL + 1,
     FC_NS = FC_NL + 2,
     FC_QCAP = FC_NL + 3,            // queue slots: B * N (w.bw); tickets and pushes stay below it
+    FC_NLPOOL = FC_NL + 4,          // initial long pool: B root-path entries, then the frames' other long paths
     FC_HDR = 8 * kFlowLine,         // then pl[B + 1], pt[B + 1], ps[B + 1]
 };
 constexpr int kFlowSpin = 1 << 22;  // polls of a queue slot before giving up (s_sleep between)
@@ -142,11 +143,24 @@ __device__ inline int flow_frame(const int* pre, int B, int i) {  // largest f w
     }
     return lo;
 }
+// Initial long pool entry i: entries [0, B) are the frames' root heavy paths (the KRT root's chain, the
+// longest of a frame: started first), the rest every frame's other long paths (pl: their prefix sums).
+// -1: frame i has no long path.
 __device__ inline int flow_long_task(const Ws& w, const int* ctl, int i) {
     const int B = w.d.B;
     const int* pl = ctl + FC_HDR;
-    const int f = flow_frame(pl, B, i);
-    const int j = w.list_long[f * w.d.N + (i - pl[f])];
+    int f, k;
+    if (i < B) {
+        f = i;
+        k = -1;
+        if (w.C(f)[C_LONG] == 0) return -1;
+    } else {
+        f = flow_frame(pl, B, i - B);
+        k = i - B - pl[f];  // among the frame's long paths other than its first
+    }
+    const int rp = w.C(f)[C_ROOTL] > 0 ? w.C(f)[C_ROOTL] - 1 : 0;  // the entry taken first
+    const int idx = k < 0 ? rp : (k < rp ? k : k + 1);
+    const int j = w.list_long[f * w.d.N + idx];
     return (int)(f * w.d.N + j) | kFlowLong;
 }
 __device__ inline int flow_short_task(const Ws& w, const int* ctl, int i) {
@@ -176,7 +190,7 @@ __global__ void k_flow_prep(Ws w, int* ctl) {
         pl[f] = sl;
         pt[f] = st;
         ps[f] = ss;
-        sl += w.C(f)[C_LONG];
+        sl += w.C(f)[C_LONG] > 0 ? w.C(f)[C_LONG] - 1 : 0;
         st += w.C(f)[C_TINY];
         ss += w.C(f)[C_SHORT];
     }
@@ -185,7 +199,10 @@ __global__ void k_flow_prep(Ws w, int* ctl) {
     ps[B] = ss;
     for (int k = 0; k < FC_HDR; ++k) ctl[k] = 0;
     for (int k = 0; k < FS_N; ++k) g_fs[k * kFsStride] = (k == FS_T0) ? ~0ull : 0ull;
-    ctl[FC_NL] = sl;
+    int nl = 0;
+    for (int f = 0; f < B; ++f) nl += w.C(f)[C_LONG];
+    ctl[FC_NL] = nl;
+    ctl[FC_NLPOOL] = B + sl;
     ctl[FC_NT] = st;
     ctl[FC_NS] = ss;
     ctl[FC_QCAP] = (int)(B * w.d.N);
@@ -533,9 +550,10 @@ __device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int 
     const int lane = threadIdx.x & 63;
     int t = -1;
     if (lane == 0) {
-        if (f_ld(ctl + FC_LONG_NEXT) < nl) {
+        const int np = ctl[FC_NLPOOL];
+        while (t < 0 && f_ld(ctl + FC_LONG_NEXT) < np) {
             const int i = atomicAdd(ctl + FC_LONG_NEXT, 1);
-            if (i < nl) t = flow_long_task(w, ctl, i);
+            if (i < np) t = flow_long_task(w, ctl, i);
         }
         for (int spin = 0; t < 0; ++spin) {
             if (f_ld(ctl + FC_LDONE) >= nl) break;  // every long path completed: nothing more will come
@@ -571,19 +589,30 @@ __device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int 
     return __shfl(t, 0, 64);
 }
 
-// The batch's whole replay. One wave per workgroup, persistent. Workgroups [0, nlong) are long workers:
-// they run long paths (initial pool, then queue tickets) following their completions' long waiters, and
-// a short waiter as a one-lane short round; they leave when every long path completed. The others are
-// short workers: rounds of short paths from the initial pool; they leave when it is empty and their
-// lanes are done (short paths parked on a path that completes later are continued by its completer).
-__global__ __launch_bounds__(64) void k_replay_flow(Ws w, int* ctl, unsigned epoch, int nlong) {
-    __shared__ OneRec buf[2][64];
-    __shared__ OneOut ob[128];
+// The batch's whole replay, as two persistent launches whose waves work independently (no workgroup
+// barrier), packed kW to a workgroup so that they hold few CUs: while they run, the graph stage of the
+// next batches (k_krt_fused takes whole CUs) keeps the rest of the chip. Both run at once, the long
+// workers on a stream of their own (HipBackend::replay_flow).
+//   kLong = false — short workers (8 waves per workgroup): rounds of short paths from the initial pool
+//     until it is empty and their lanes are done. A short path parked on a path that completes later
+//     is continued by that path's completer; a long path parked on a short one is queued by the lane
+//     that completes it.
+//   kLong = true — long workers (4 waves per workgroup, one per SIMD, first in its arbitration): long
+//     paths from the initial pool (every frame's root chain first), then queue tickets, following their
+//     completions' long waiters, and a short waiter as a one-lane short round; they leave when every
+//     long path completed.
+// Measured (112 frames, 1080p, tools/flow_stats.py, serial): short paths done at 26.7 ms, the last
+// chain at 42.4 ms; same-box bench 1,518-1,540 Mpixels/s with 128 long and 2,048 short workers.
+template <bool kLong, int kW>
+__global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigned epoch) {
+    __shared__ OneRec buf[kLong ? kW : 1][2][64];
+    __shared__ OneOut ob[kLong ? kW : 1][128];
     const int lane = threadIdx.x & 63;
+    const int wv = kLong ? (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
     const int nl = ctl[FC_NL];
     int cb = 0, ce = 0;  // this wave's claimed, not yet started initial short tasks
     if (lane == 0) fs_min(FS_T0, fs_now());
-    if ((int)blockIdx.x < nlong) {
+    if constexpr (kLong) {
         __builtin_amdgcn_s_setprio(3);  // the chains go first in their SIMD's arbitration
         for (int it = 0; it < (1 << 26); ++it) {
             int t = flow_next_long(w, ctl, epoch, nl);
@@ -591,7 +620,7 @@ __global__ __launch_bounds__(64) void k_replay_flow(Ws w, int* ctl, unsigned epo
             const unsigned long long t1 = fs_now();
             while (t >= 0) {
                 if (lane == 0) fs_add(FS_LRUNS, 1);
-                const int nx = flow_long(w, ctl, t, buf, ob);
+                const int nx = flow_long(w, ctl, t, buf[wv], ob[wv]);
                 if (nx >= 0 && !(nx & kFlowLong)) {  // a short waiter: a one-lane short round (and its waiters)
                     if (lane == 0) fs_add(FS_INJECT, 1);
                     flow_short(w, ctl, epoch, nx, false, &cb, &ce);
@@ -612,6 +641,8 @@ __global__ __launch_bounds__(64) void k_replay_flow(Ws w, int* ctl, unsigned epo
     }
     if (lane == 0) fs_max(FS_T_EXIT, fs_now());
 }
+constexpr int kFlowShortW = 8;  // waves per short-worker workgroup
+constexpr int kFlowLongW = 4;    // waves per long-worker workgroup (one per SIMD)
 
 // counter C_FLOWERR of frame 0 = a bounded wait of the launch gave up (dofs_batch_counters)
 __global__ void k_flow_report(Ws w, const int* ctl) {

@@ -2640,6 +2640,9 @@ struct HipBackend {
         for (auto& t : tmps)
             if (t.p) (void)hipFree(t.p);
         if (flow_ctl) (void)hipFree(flow_ctl);
+        if (flow_stream) (void)hipStreamDestroy(flow_stream);
+        for (auto e : flow_ev)
+            if (e) (void)hipEventDestroy(e);
         for (auto st : streams) (void)hipStreamDestroy(st);
         if (own) (void)hipStreamDestroy(own);
     }
@@ -3109,18 +3112,20 @@ struct HipBackend {
     // batch whose task ids would not fit 30 bits)
     int* flow_ctl = nullptr;
     size_t flow_ctl_n = 0;
+    hipStream_t flow_stream = nullptr;
+    hipEvent_t flow_ev[2] = {nullptr, nullptr};
     unsigned flow_epoch = 0;
-    static int flow_grid() {  // short-path workgroups (one wave each) of the persistent replay launch
+    static int flow_grid() {  // short-path workers (waves) of the persistent replay
         static const int g = [] {
             const char* e = getenv("DOFS_FLOW_GRID");
-            return e && atoi(e) > 0 ? atoi(e) : 1024;
+            return e && atoi(e) > 0 ? atoi(e) : 2048;
         }();
         return g;
     }
     static int flow_long_workers() {  // waves that run long paths (the rest of the grid runs short ones)
         static const int g = [] {
             const char* e = getenv("DOFS_FLOW_LONG");
-            return e && atoi(e) > 0 ? atoi(e) : 256;
+            return e && atoi(e) > 0 ? atoi(e) : 128;
         }();
         return g;
     }
@@ -3142,9 +3147,24 @@ struct HipBackend {
         }
         flow_epoch = flow_epoch % kFlowEpochs + 1;  // queue-slot tag of this launch (never 0)
         hipLaunchKernelGGL(k_flow_prep, dim3(1), dim3(64), 0, stream, w, flow_ctl);
+        if (!flow_stream) {  // the long workers' launch runs beside the short workers' (no dependency)
+            int least = 0, greatest = 0;
+            (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+            note(hipStreamCreateWithPriority(&flow_stream, hipStreamNonBlocking, greatest), "hipStreamCreate");
+            note(hipEventCreateWithFlags(&flow_ev[0], hipEventDisableTiming), "hipEventCreate");
+            note(hipEventCreateWithFlags(&flow_ev[1], hipEventDisableTiming), "hipEventCreate");
+        }
         timed("k_replay_flow", [&] {
-            hipLaunchKernelGGL(k_replay_flow, dim3((unsigned)(flow_grid() + flow_long_workers())), dim3(64), 0, stream, w,
-                               flow_ctl, flow_epoch, flow_long_workers());
+            const int gs = (flow_grid() + kFlowShortW - 1) / kFlowShortW;
+            const int gl = (flow_long_workers() + kFlowLongW - 1) / kFlowLongW;
+            note(hipEventRecord(flow_ev[0], stream), "hipEventRecord");
+            note(hipStreamWaitEvent(flow_stream, flow_ev[0], 0), "hipStreamWaitEvent");
+            hipLaunchKernelGGL((k_replay_flow<true, kFlowLongW>), dim3((unsigned)gl), dim3(64 * kFlowLongW), 0, flow_stream,
+                               w, flow_ctl, flow_epoch);
+            hipLaunchKernelGGL((k_replay_flow<false, kFlowShortW>), dim3((unsigned)gs), dim3(64 * kFlowShortW), 0, stream,
+                               w, flow_ctl, flow_epoch);
+            note(hipEventRecord(flow_ev[1], flow_stream), "hipEventRecord");
+            note(hipStreamWaitEvent(stream, flow_ev[1], 0), "hipStreamWaitEvent");
         });
         hipLaunchKernelGGL(k_flow_report, dim3(1), dim3(64), 0, stream, w, flow_ctl);
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_replay_flow launch");

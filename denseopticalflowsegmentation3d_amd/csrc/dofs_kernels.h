@@ -1153,8 +1153,10 @@ struct KPathInit {  // one lane per merge node x = N + k; path ids and lists thr
         if (top) {
             w.cur[f * d.N + j] = qb - 1;
             w.ptop[f * d.N + j] = q;
-            if (islong)
+            if (islong) {
                 w.list_long[f * d.N + jl] = j;
+                if (q == 0) w.C(f)[C_ROOTL] = jl + 1;  // the KRT root's path: the frame's longest chain
+            }
             else if (tiny)
                 w.list_short[f * d.N + d.N - 1 - jt] = j;
             else
