@@ -2606,6 +2606,8 @@ struct KLeafPos {
     }
 };
 
+#include "dofs_sortfix.h"
+
 struct HipBackend {
     int device = 0;
     hipStream_t own = nullptr;
@@ -3292,16 +3294,45 @@ struct HipBackend {
         }
         const int fb = frame_bits(nf);
         const int tot = (int)(n * nf);
+        const int cut = g_sort_cut;
         unsigned* vmid = reinterpret_cast<unsigned*>(w.EU);
         size_t b1 = 0, b2 = 0;
-        note(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, w.key_in, w.key_out, w.val_in, vmid, tot, 0, 64, stream),
+        // bits [cut, 63) when truncated: the weights are >= 0 (a sign bit raises the fix-up's fallback), and
+        // this image's rocPRIM sorts [cut > 0, 64) of u64 keys wrongly on its merge-sort path (2k .. 1M
+        // pairs; tools/sort_check.hip) while [cut, 63) is right at every size
+        const int endb = cut > 0 ? 63 : 64;
+        note(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, w.key_in, w.key_out, w.val_in, vmid, tot, cut, endb, stream),
              "sort size");
         note(hipcub::DeviceRadixSort::SortKeys(nullptr, b2, vmid, w.val_out, tot, value_bits, value_bits + fb, stream),
              "sort size");
         void* t = temp(std::max(b1, b2));
-        note(hipcub::DeviceRadixSort::SortPairs(t, b1, w.key_in, w.key_out, w.val_in, vmid, tot, 0, 64, stream), "sort");
+        note(hipcub::DeviceRadixSort::SortPairs(t, b1, w.key_in, w.key_out, w.val_in, vmid, tot, cut, endb, stream),
+             "sort");
+        if (cut > 0 && g_sort_fix) sort_fixup(w, vmid, tot, cut);
+        if (g_sort_dump[0]) {  // diagnosis: the batch order after the fix-up (dofs_debug_sort_dump)
+            const size_t m = (size_t)std::min<int64_t>(tot, g_sort_dump_cap);
+            note(hipMemcpyAsync(g_sort_dump[0], w.key_out, 8 * m, hipMemcpyDeviceToDevice, stream), "dump");
+            note(hipMemcpyAsync(g_sort_dump[1], vmid, 4 * m, hipMemcpyDeviceToDevice, stream), "dump");
+            g_sort_dump[0] = g_sort_dump[1] = nullptr;
+        }
         note(hipcub::DeviceRadixSort::SortKeys(t, b2, vmid, w.val_out, tot, value_bits, value_bits + fb, stream),
              "sort frames");
+    }
+    // dofs_sortfix.h: the groups of equal truncated keys sorted by the full key (val_out, written by the
+    // frame pass next, holds the lists; key_in / val_in, dead after the pair sort, the scratch)
+    void sort_fixup(Ws& w, unsigned* vmid, int64_t tot, int cut) {
+        SortFix s{w.key_out, vmid, w.key_in, w.val_in, w.ctr + C_SORTFIX, tot, cut};
+        const int64_t cap = grid_cap() > 0 ? grid_cap() : 8192;
+        const unsigned gx = (unsigned)std::min<int64_t>((tot + kFixBlock - 1) / kFixBlock, cap);
+        int lgs = 0;
+        while (((int64_t)1 << lgs) < tot) ++lgs;
+        lgs += lgs & 1;  // an even number of merge passes ends in (key_out, vmid)
+        timed("k_sortfix", [&] {
+            hipLaunchKernelGGL(k_sortfix_local, dim3(gx), dim3(kFixBlock), 0, stream, s);
+            for (int lg = 0; lg < lgs; ++lg)  // (each returns at once unless the flag is up)
+                hipLaunchKernelGGL(k_sortfix_merge, dim3(1024), dim3(kFixBlock), 0, stream, s, lg, lg & 1);
+        });
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "sort fix-up launch");
     }
 };
 
@@ -3326,6 +3357,23 @@ extern "C" int dofs_debug_flow_stats(unsigned long long* out, int n) {
     if (hipMemcpyFromSymbol(v, HIP_SYMBOL(dofs::g_fs), sizeof(v)) != hipSuccess) return -1;
     for (int i = 0; i < n && i < dofs::FS_N; ++i) out[i] = v[i * dofs::kFsStride];
     return dofs::FS_N;
+}
+
+// Test knob: the low key bits the batch MST sort leaves to the fix-up (dofs_sortfix.h), 0 .. 48
+// (0: the full 64-bit sort; 48: 16-bit keys, every weight class a mixed group: the fallback's test).
+// cut < 0 only reads it. Returns the previous value. The fix-up's counters: frame 0's C_SORTFIX .. + 2.
+extern "C" int dofs_debug_sort_cut(int cut) {
+    const int old = dofs::g_sort_cut;
+    if (cut >= 0 && cut <= 48) dofs::g_sort_cut = cut;
+    return old;
+}
+// Diagnosis only: fix-up on / off (the truncated order is not Kruskal's: results differ), and a copy of
+// the next packed batch's sorted (key, value) pairs — at most cap — into device buffers.
+extern "C" void dofs_debug_sort_fix(int on) { dofs::g_sort_fix = on != 0; }
+extern "C" void dofs_debug_sort_dump(void* d_keys, void* d_vals, int64_t cap) {
+    dofs::g_sort_dump[0] = d_keys;
+    dofs::g_sort_dump[1] = d_vals;
+    dofs::g_sort_dump_cap = cap;
 }
 
 using DofsBackend = dofs::HipBackend;

@@ -1392,9 +1392,11 @@ struct KSlotInit {
 struct KSlotEvent {  // first event reaching the slot's maximum wins (strict '<' update, graph.cpp:352)
     Ws w;
     const int* pre;
-    DOFS_HD void operator()(int f, int64_t j) const {
+    static constexpr bool kBlockTake = true;  // (takes nothing: the list launch's form, bounded by C_CAND)
+    template <class T>
+    DOFS_HD void operator()(int f, int64_t j, bool valid, T&) const {
         const Dims& d = w.d;
-        if (j >= w.C(f)[C_CAND]) return;
+        if (!valid || j >= w.C(f)[C_CAND]) return;
         const double s = w.cscore[f * d.M + j];
         if (!(s > w.score_threshold)) return;
         const int i = w.cand[f * d.M + j];

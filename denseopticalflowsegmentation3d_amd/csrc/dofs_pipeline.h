@@ -447,8 +447,9 @@ struct Pipeline {
         // K6 new_merge filters, lifting, per-slot arg-max, snapshots
         be.launch(B, M, KFilter{w, pre});
         be.launch(B, N, KSlotInit{w});
-        if (!(skip_mask & 4)) be.launch(B, M, KLift{w, pre});
-        be.launch(B, M, KSlotEvent{w, pre});
+        // the candidate list launches cover [0, C_CAND) of each frame (read on the device), not all M
+        if (!(skip_mask & 4)) be.launch_counted(B, M, KLift{w, pre}, C_CAND);
+        be.launch_counted(B, M, KSlotEvent{w, pre}, C_CAND);
         be.launch(B, N, KSlotFlag{w});
         be.scan_excl(w.sflag, w.soff, N, B);
         be.launch(B, 1, KSnapCount{w});
