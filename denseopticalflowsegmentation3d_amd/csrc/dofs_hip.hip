@@ -3329,8 +3329,10 @@ struct HipBackend {
         lgs += lgs & 1;  // an even number of merge passes ends in (key_out, vmid)
         timed("k_sortfix", [&] {
             hipLaunchKernelGGL(k_sortfix_local, dim3(gx), dim3(kFixBlock), 0, stream, s);
-            for (int lg = 0; lg < lgs; ++lg)  // (each returns at once unless the flag is up)
-                hipLaunchKernelGGL(k_sortfix_merge, dim3(1024), dim3(kFixBlock), 0, stream, s, lg, lg & 1);
+            // (returns at once unless the flag is up; two blocks per CU, all resident for its barrier)
+            int cus = 256;
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+            hipLaunchKernelGGL(k_sortfix_merge, dim3(2 * cus), dim3(kFixBlock), 0, stream, s, lgs);
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "sort fix-up launch");
     }

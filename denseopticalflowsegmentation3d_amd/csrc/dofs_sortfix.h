@@ -9,25 +9,25 @@
 // 2^-28 relative of each other). Sorting every mixed group by (key, value) — all pairs are distinct:
 // the value carries frame and emission index — gives the full-key stable order.
 //
-// Measured (tools/sortfix_stats.py, 16 synthetic 1080p frames, 33M MST edges): cut 24 → 343k mixed
-// groups of at most 7 pairs; cut 32 → 3.4M groups of at most 47; cut 16 → 1.4k groups of 2.
+// Measured (tools/sortfix_stats.py, synthetic 1080p frames): 16 frames (33M MST edges): cut 24 → 343k
+// mixed groups of at most 7 pairs, cut 32 → 3.4M of at most 47, cut 16 → 1.4k of 2; 112 frames (232M):
+// cut 24 → 14.4M mixed groups (the batch's frames share weight values), cut 32 → groups beyond kFixScan.
 //
-// k_sortfix_local, one lane per position p, no atomics, no lists:
-//   - the lane at a group's first position owns the group: it scans forward (at most kFixScan
-//     positions) and, if the group is short and mixed, insertion-sorts it in place by (key, value).
-//     Only the owner writes a group, and the truncated keys every other lane reads never change
-//     under a permutation inside the group, so the pass needs no second kernel;
-//   - a lane at a mixed pair (p - 1, p) checks that its group starts within kFixScan positions. A
-//     longer mixed group (never seen: long groups are exact ties, e.g. zero weights) raises the
-//     fallback flag, and k_sortfix_merge — launched ceil_log2(n) times rounded up to an even count,
-//     each launch returning at once when the flag is clear — merge-sorts the whole batch by (key,
-//     value): slower, never wrong.
+// k_sortfix_local (no atomics but one per wave, no lists): a group inside a wave's 64 positions with at
+// most kFixWin of them is ranked by (key, value) in registers and scattered; a longer or wave-crossing
+// group is insertion-sorted in place by the lane at its first position (at most kFixScan positions).
+// Only a group's sorter writes it, and the truncated keys every other lane reads never change under
+// a permutation inside a group, so one pass suffices. A mixed group longer than kFixScan (never seen:
+// long groups are exact ties, e.g. zero weights) or a negative key raises the fallback flag, and
+// k_sortfix_merge — one launch that returns at once when the flag is clear — merge-sorts the whole
+// batch by (key, value): slower, never wrong.
 #pragma once
 // (included inside namespace dofs by dofs_hip.hip)
 
 constexpr int kSortCut = 24;   // low key bits the batch radix sort leaves to the fix-up
 constexpr int kFixScan = 256;  // longest group the local pass sorts (longer mixed: the fallback)
 constexpr int kFixBlock = 256;
+constexpr int kFixWin = 16;    // longest group the wave ranks in registers (longer or wave-crossing: scalar)
 inline int g_sort_cut = kSortCut;  // host: the cut of the next batch sorts (dofs_debug_sort_cut)
 inline bool g_sort_fix = true;     // host: run the fix-up (off: the truncated order, for diagnosis only)
 inline void* g_sort_dump[2] = {nullptr, nullptr};  // host: device buffers for the next batch's sorted pairs
@@ -38,7 +38,8 @@ struct SortFix {
     unsigned* val;            // their values (the packed sort's middle buffer)
     unsigned long long* k2;   // free buffers of the same sizes (key_in / val_in): the fallback's
     unsigned* v2;
-    int* ctr;  // frame 0's C_SORTFIX counters: [0] groups sorted by the local pass, [1] fallback flag
+    int* ctr;  // frame 0's C_SORTFIX counters: [0] pairs the local pass moved, [1] fallback flag,
+               // [2] the fallback's grid barrier
     int64_t n;
     int cut;
 };
@@ -47,91 +48,156 @@ __device__ inline bool fix_less(unsigned long long ka, unsigned va, unsigned lon
     return ka < kb || (ka == kb && va < vb);
 }
 
-__global__ __launch_bounds__(kFixBlock) void k_sortfix_local(SortFix s) {
-    const int64_t step = (int64_t)gridDim.x * kFixBlock;
-    int sorted = 0;
-    for (int64_t p = (int64_t)blockIdx.x * kFixBlock + threadIdx.x; p < s.n; p += step) {
-        const unsigned long long b = s.key[p];
-        const unsigned long long T = b >> s.cut;
-        if (b >> 63) dofs_st(s.ctr + 1, 1);  // a negative weight (NaN flow): the sort kept bits [cut, 63)
-        bool head = true;
-        if (p >= 1) {
-            const unsigned long long a = s.key[p - 1];
-            head = (a >> s.cut) != T;
-            if (!head && a != b) {  // a mixed pair: its group must start within kFixScan positions
-                int64_t q = p - 1;
-                while (q >= 1 && p - q < kFixScan && (s.key[q - 1] >> s.cut) == T) --q;
-                if (q >= 1 && (s.key[q - 1] >> s.cut) == T) dofs_st(s.ctr + 1, 1);
-            }
+// the scalar path of one group [p, ...) from its first position: at most kFixScan positions, in place
+__device__ inline int fix_group_scalar(const SortFix& s, int64_t p, unsigned long long b) {
+    const unsigned long long T = b >> s.cut;
+    int64_t e = p + 1;
+    bool mixed = false;
+    unsigned long long prev = b;
+    while (e < s.n && e - p < kFixScan) {
+        const unsigned long long k = s.key[e];
+        if ((k >> s.cut) != T) break;
+        mixed |= k != prev;
+        prev = k;
+        ++e;
+    }
+    if (!mixed) return 0;  // exact ties (or a long group's first kFixScan: its mixed pairs further on flag)
+    if (e < s.n && (s.key[e] >> s.cut) == T) {  // longer than kFixScan and mixed: the fallback
+        dofs_st(s.ctr + 1, 1);
+        return 0;
+    }
+    int moved = 0;
+    for (int64_t i = p + 1; i < e; ++i) {  // insertion sort by (key, value)
+        const unsigned long long k = s.key[i];
+        const unsigned v = s.val[i];
+        int64_t j = i;
+        while (j > p && fix_less(k, v, s.key[j - 1], s.val[j - 1])) {
+            s.key[j] = s.key[j - 1];
+            s.val[j] = s.val[j - 1];
+            --j;
         }
-        if (!head) continue;
-        int64_t e = p + 1;  // the group [p, e)
-        bool mixed = false;
-        unsigned long long prev = b;
-        while (e < s.n && e - p < kFixScan) {
-            const unsigned long long k = s.key[e];
-            if ((k >> s.cut) != T) break;
-            mixed |= k != prev;
-            prev = k;
-            ++e;
-        }
-        if (!mixed) continue;  // exact ties (or a long group's first kFixScan: its mixed pairs further on flag)
-        if (e < s.n && (s.key[e] >> s.cut) == T) {  // longer than kFixScan and mixed: the fallback
-            dofs_st(s.ctr + 1, 1);
-            continue;
-        }
-        ++sorted;
-        for (int64_t i = p + 1; i < e; ++i) {  // insertion sort by (key, value), in place
-            const unsigned long long k = s.key[i];
-            const unsigned v = s.val[i];
-            int64_t j = i;
-            while (j > p && fix_less(k, v, s.key[j - 1], s.val[j - 1])) {
-                s.key[j] = s.key[j - 1];
-                s.val[j] = s.val[j - 1];
-                --j;
-            }
+        if (j != i) {
             s.key[j] = k;
             s.val[j] = v;
+            moved += (int)(i - j) + 1;
         }
     }
-    const int tot = wave_reduce(sorted, [](int x, int y) { return x + y; });
-    if (tot && wave_lane() == 0) dofs_aadd(s.ctr, tot);
+    return moved;
 }
 
-// fallback, pass `lg`: merges runs of 2^lg pairs from (ka, va) into (kb, vb); nothing when the flag
-// is clear. Each pair's destination = its offset in its run + the partner run's pairs below it.
-__global__ __launch_bounds__(kFixBlock) void k_sortfix_merge(SortFix s, int lg, int odd) {
+// One wave per 64 consecutive positions (grid-stride). A group that lies inside the wave with at most
+// kFixWin positions is ranked in registers: rank = the group's pairs below this lane's (key, value),
+// read by cross-lane shuffles, then one scatter store per moved pair (every lane read before any
+// writes). A group that crosses the wave's ends or is longer takes the scalar path from its first
+// position (the lane holding it, or the earlier wave's); its other lanes only check, at a mixed pair,
+// that the group starts within kFixScan positions (else the fallback flag).
+__global__ __launch_bounds__(kFixBlock) void k_sortfix_local(SortFix s) {
+    const int lane = wave_lane();
+    const int64_t nw = (int64_t)gridDim.x * (kFixBlock / 64);
+    int moved = 0;
+    for (int64_t wv = (int64_t)blockIdx.x * (kFixBlock / 64) + threadIdx.x / 64; wv * 64 < s.n; wv += nw) {
+        const int64_t base = wv * 64, p = base + lane;
+        const bool valid = p < s.n;
+        const unsigned long long b = valid ? s.key[p] : 0ull;
+        const unsigned long long T = b >> s.cut;
+        if (valid && (b >> 63)) dofs_st(s.ctr + 1, 1);  // a negative weight (NaN flow): bits [cut, 63) sorted
+        unsigned long long a = __shfl_up(b, 1, 64), c = __shfl_down(b, 1, 64);
+        if (lane == 0 && valid && p >= 1) a = s.key[p - 1];
+        if (lane == 63 && p + 1 < s.n) c = s.key[p + 1];
+        const bool same_prev = valid && p >= 1 && (a >> s.cut) == T;
+        const bool same_next = valid && p + 1 < s.n && (c >> s.cut) == T;
+        const unsigned long long mix = __ballot(same_prev && a != b);  // mixed pairs (lane - 1, lane)
+        const bool tail_open = __shfl(same_next ? 1 : 0, 63, 64) != 0;  // a group runs into the next wave
+        if (!mix && !tail_open) continue;  // no mixed group here (one that began earlier: its first lane's)
+        // this lane's group inside the wave: lanes [gs, ge); open at either end if it continues there
+        const unsigned long long heads = __ballot(!same_prev);
+        const unsigned long long upto = lane == 63 ? ~0ull : (2ull << lane) - 1ull;
+        const unsigned long long below = heads & upto, above = heads & ~upto;
+        const bool left_open = below == 0;
+        const int gs = left_open ? 0 : 63 - __clzll(below);
+        const int ge = above ? __ffsll((long long)above) - 1 : 64;
+        const bool right_open = above == 0 && tail_open;
+        const int g = ge - gs;
+        const unsigned long long gmask = (ge == 64 ? ~0ull : (1ull << ge) - 1ull) & ~((1ull << gs) - 1ull);
+        const bool fast = valid && !left_open && !right_open && g >= 2 && g <= kFixWin && (mix & gmask);
+        const unsigned v = fast ? s.val[p] : 0u;
+        const int gmax = wave_reduce(fast ? g : 0, [](int x, int y) { return x > y ? x : y; });
+        if (gmax) {
+            int rank = 0;
+            for (int d = 0; d < gmax; ++d) {
+                const int j = (gs + d) & 63;
+                const unsigned long long kj = __shfl(b, j, 64);
+                const unsigned vj = __shfl(v, j, 64);
+                rank += (fast && d < g && j != lane && fix_less(kj, vj, b, v)) ? 1 : 0;
+            }
+            if (fast && gs + rank != lane) {
+                s.key[base + gs + rank] = b;
+                s.val[base + gs + rank] = v;
+                ++moved;
+            }
+        }
+        if (!valid || fast || (!left_open && !right_open && !(mix & gmask))) continue;  // done, or exact ties
+        if (!same_prev) {
+            moved += fix_group_scalar(s, p, b);  // the group's first position: the scalar path
+        } else if (a != b) {  // a mixed pair of a scalar-path group: it must start within kFixScan
+            int64_t q = p - 1;
+            while (q >= 1 && p - q < kFixScan && (s.key[q - 1] >> s.cut) == T) --q;
+            if (q >= 1 && (s.key[q - 1] >> s.cut) == T) dofs_st(s.ctr + 1, 1);
+        }
+    }
+    const int tot = wave_reduce(moved, [](int x, int y) { return x + y; });
+    if (tot && lane == 0) dofs_aadd(s.ctr, tot);
+}
+
+// fallback: merge passes lg = 0 .. lgs - 1 (runs of 2^lg pairs, ping-pong between (key, val) and (k2, v2);
+// lgs even, so the result ends in (key, val)), one launch, a grid barrier between passes; returns at
+// once when the flag is clear. A pair's destination = its offset in its run + the partner run's pairs
+// below it (all pairs distinct). The barrier counts arrivals on ctr[2] (zero at the batch's start):
+// every block's stores are complete at __syncthreads, lane 0 releases them with the agent fence,
+// arrives, waits for the pass's full count, and acquires with the same fence.
+__global__ __launch_bounds__(kFixBlock) void k_sortfix_merge(SortFix s, int lgs) {
     if (!dofs_ld(s.ctr + 1)) return;
-    const unsigned long long* ka = odd ? s.k2 : s.key;
-    const unsigned* va = odd ? s.v2 : s.val;
-    unsigned long long* kb = odd ? s.key : s.k2;
-    unsigned* vb = odd ? s.val : s.v2;
-    const int64_t W = (int64_t)1 << lg;
     const int64_t step = (int64_t)gridDim.x * kFixBlock;
-    for (int64_t p = (int64_t)blockIdx.x * kFixBlock + threadIdx.x; p < s.n; p += step) {
-        const unsigned long long k = ka[p];
-        const unsigned v = va[p];
-        const int64_t a0 = p & ~(2 * W - 1), mid = a0 + W;
-        int64_t lo, hi, off;
-        if (p < mid) {  // left run: partner [mid, a0 + 2W)
-            lo = mid < s.n ? mid : s.n;
-            hi = a0 + 2 * W < s.n ? a0 + 2 * W : s.n;
-            off = p - a0;
-        } else {
-            lo = a0;
-            hi = mid;
-            off = p - mid;
+    for (int lg = 0; lg < lgs; ++lg) {
+        const bool odd = lg & 1;
+        const unsigned long long* ka = odd ? s.k2 : s.key;
+        const unsigned* va = odd ? s.v2 : s.val;
+        unsigned long long* kb = odd ? s.key : s.k2;
+        unsigned* vb = odd ? s.val : s.v2;
+        const int64_t W = (int64_t)1 << lg;
+        for (int64_t p = (int64_t)blockIdx.x * kFixBlock + threadIdx.x; p < s.n; p += step) {
+            const unsigned long long k = ka[p];
+            const unsigned v = va[p];
+            const int64_t a0 = p & ~(2 * W - 1), mid = a0 + W;
+            int64_t lo, hi, off;
+            if (p < mid) {  // left run: partner [mid, a0 + 2W)
+                lo = mid < s.n ? mid : s.n;
+                hi = a0 + 2 * W < s.n ? a0 + 2 * W : s.n;
+                off = p - a0;
+            } else {
+                lo = a0;
+                hi = mid;
+                off = p - mid;
+            }
+            const int64_t l0 = lo;
+            while (lo < hi) {  // partner pairs below (k, v)
+                const int64_t m = lo + (hi - lo) / 2;
+                if (fix_less(ka[m], va[m], k, v))
+                    lo = m + 1;
+                else
+                    hi = m;
+            }
+            const int64_t d = a0 + off + (lo - l0);
+            kb[d] = k;
+            vb[d] = v;
         }
-        const int64_t l0 = lo;
-        while (lo < hi) {  // partner pairs below (k, v)
-            const int64_t m = lo + (hi - lo) / 2;
-            if (fix_less(ka[m], va[m], k, v))
-                lo = m + 1;
-            else
-                hi = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            dofs_aadd(s.ctr + 2, 1);
+            while (dofs_ld(s.ctr + 2) < (lg + 1) * (int)gridDim.x) __builtin_amdgcn_s_sleep(4);
+            __threadfence();
         }
-        const int64_t d = a0 + off + (lo - l0);
-        kb[d] = k;
-        vb[d] = v;
+        __syncthreads();
     }
 }
