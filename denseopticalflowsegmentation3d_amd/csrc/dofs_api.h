@@ -203,10 +203,13 @@ struct Context {
     bool used[kSlots] = {false, false, false};
     Meta meta[kSlots];
     void* sA = nullptr;
+    void* sA1 = nullptr;  // the graph stage of odd batches (DOFS_DUAL_A=0: all on sA)
     void* sB = nullptr;
     void* evIn = nullptr;
     void* evA[kSlots] = {nullptr, nullptr, nullptr};
+    void* evRead[kSlots] = {nullptr, nullptr, nullptr};  // the batch's input consumed (after the blur)
     void* evDone[kSlots] = {nullptr, nullptr, nullptr};
+    bool dual_a = false;
 
     bool serial = false;
     bool skip_b = false;  // DOFS_SKIP_B=1: measurement only — graph stage alone, results invalid
@@ -231,11 +234,19 @@ struct Context {
         // 1 = graph stage urgent, replay stage least (experiment); 0 = equal
         const char* pr = getenv("DOFS_PRIO");
         const int prio = pr ? atoi(pr) : 2;
+        // DOFS_DUAL_A=1: two graph-stage streams, batches alternating — batch k + 1's graph stage starts
+        // once batch k has read its input, so one batch's latency-bound sweeps (KRT, preorder) may overlap
+        // the next one's bandwidth-bound kernels. Measured equal to one stream (B = 112, same box: 1,485 /
+        // 1,480 vs 1,479 / 1,479 Mpix/s; the chip's total work bounds the step), so it is off by default
+        const char* da = getenv("DOFS_DUAL_A");
+        dual_a = da && da[0] == '1';
         sA = be.new_stream(prio == 1 ? 1 : 0);
+        sA1 = be.new_stream(prio == 1 ? 1 : 0);
         sB = be.new_stream(prio == 1 ? -1 : (prio == 2 ? 1 : 0));
         evIn = be.new_event();
         for (int s = 0; s < kSlots; ++s) {
             evA[s] = be.new_event();
+            evRead[s] = be.new_event();
             evDone[s] = be.new_event();
         }
     }
@@ -328,9 +339,13 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     P.set_params(prm, persp, inv, inv_upper);
 
     void* caller = be.cur_stream();
-    void* sa = cx->sA;
     // stage timing (and DOFS_SERIAL=1, for clean per-kernel profiles) runs the phases back to back
-    void* sb = (be.profiling() || cx->serial) ? cx->sA : cx->sB;
+    const bool serial = be.profiling() || cx->serial;
+    // the caller's own inputs beyond the flow (an edge list, an edge mask) are read past the blur: those
+    // batches release the caller after the whole graph stage, on sA
+    const bool own_in = allow || d_edges || n_edges > 0;
+    void* sa = (cx->dual_a && !serial && !own_in && (id & 1)) ? cx->sA1 : cx->sA;
+    void* sb = serial ? cx->sA : cx->sB;
     be.record(cx->evIn, caller);
     be.wait(sa, cx->evIn);
     if (cx->used[s]) be.wait(sa, cx->evDone[s]);
@@ -341,7 +356,9 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
         mreal = P.run_a_edges(d_flow, d_edges, n_edges, d_acc, d_acc + n_edges);
         if (mreal < 0) return cx->fail(DOFS_ERR_INVALID_ARG, "too many edges");
     } else {
+        P.ev_input = own_in ? nullptr : cx->evRead[s];  // recorded once the blur has read d_flow
         P.run_a(d_flow, fstride);
+        P.ev_input = nullptr;
     }
     P.w.allow = nullptr;
     be.record(cx->evA[s], sa);
@@ -349,7 +366,7 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     be.use(sb);
     if (!cx->skip_b) P.run_b();
     be.record(cx->evDone[s], sb);
-    be.wait(caller, cx->evA[s]);
+    be.wait(caller, own_in ? cx->evA[s] : cx->evRead[s]);
     be.use(caller);
 
     cx->used[s] = true;

@@ -57,6 +57,7 @@ struct Pipeline {
     int preorder_in_b = 0;  // 0: the preorder in phase A; 1: in phase B; 2: the path inputs (KPathInit) in B
     bool krt_dnc = false;  // DOFS_KRT_DNC=1: block-start labels by the top-down global depths
     int skip_mask = 0;          // measurement only (DOFS_SKIPMASK): 1 short replay, 2 long replay, 4 lift
+    void* ev_input = nullptr;   // run_a records it once the input flow has been read (the caller's release)
     bool keys_by_frame = true;  // key_out holds each frame's sorted weights (else: recomputed for events)
     unsigned vmask = ~0u;       // emission index bits of val_out
     int long_path = kLongPath;
@@ -271,8 +272,9 @@ struct Pipeline {
         be.memset(w.ctr, 0, sizeof(int) * (size_t)B * kCounters);
 
         be.mark(0);
-        // K1 blur (segment.cpp:52): KBlurRow + KBlurCol (HIP: LDS-tiled)
+        // K1 blur (segment.cpp:52): KBlurRow + KBlurCol (HIP: LDS-tiled) — the only reader of the input
         be.blur(w);
+        if (ev_input) be.record(ev_input, be.cur_stream());
         if (M <= 0) {  // single pixel: no edge, no merge
             be.launch(B, N, KLabelInit{w, true});
             be.launch(B, 1, KSingle{w});
