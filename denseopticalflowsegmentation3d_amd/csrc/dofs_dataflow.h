@@ -313,19 +313,32 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             ob[2 * k + h] = o;
         };
         auto lda = [&](int k) { return *reinterpret_cast<const uint4*>(&c[k]); };
+        // two register sets, each reloaded right after its last use (4 steps ahead of its next use): no
+        // loop-carried copies (the single-set form with next-group temporaries compiled to ~4 v_mov per step)
         int k = 0;
         uint4 a0 = lda(0), a1 = lda(1), a2 = lda(2), a3 = lda(3);
         OneHalf b0 = c[0].h[h], b1 = c[1].h[h], b2 = c[2].h[h], b3 = c[3].h[h];
-        for (; k + 4 <= n; k += 4) {
-            const int m = (k + 4) & 63;
-            const uint4 na0 = lda(m), na1 = lda(m + 1), na2 = lda(m + 2), na3 = lda(m + 3);
-            const OneHalf nb0 = c[m].h[h], nb1 = c[m + 1].h[h], nb2 = c[m + 2].h[h], nb3 = c[m + 3].h[h];
+        for (; k + 8 <= n; k += 8) {
+            const int m = k + 4, m2 = (k + 8) & 63;
+            const uint4 e0 = lda(m), e1 = lda(m + 1), e2 = lda(m + 2), e3 = lda(m + 3);
+            const OneHalf d0 = c[m].h[h], d1 = c[m + 1].h[h], d2 = c[m + 2].h[h], d3 = c[m + 3].h[h];
             step(k, a0, b0);
             step(k + 1, a1, b1);
             step(k + 2, a2, b2);
             step(k + 3, a3, b3);
-            a0 = na0, a1 = na1, a2 = na2, a3 = na3;
-            b0 = nb0, b1 = nb1, b2 = nb2, b3 = nb3;
+            a0 = lda(m2), a1 = lda(m2 + 1), a2 = lda(m2 + 2), a3 = lda(m2 + 3);
+            b0 = c[m2].h[h], b1 = c[m2 + 1].h[h], b2 = c[m2 + 2].h[h], b3 = c[m2 + 3].h[h];
+            step(k + 4, e0, d0);
+            step(k + 5, e1, d1);
+            step(k + 6, e2, d2);
+            step(k + 7, e3, d3);
+        }
+        if (k + 4 <= n) {
+            step(k, a0, b0);
+            step(k + 1, a1, b1);
+            step(k + 2, a2, b2);
+            step(k + 3, a3, b3);
+            k += 4;
         }
         for (; k < n; ++k) step(k, lda(k), c[k].h[h]);
         B4 obb;

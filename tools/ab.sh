@@ -6,6 +6,6 @@ mkdir -p gpurun_out
 for i in $(seq 1 $N); do
   for v in ${VARIANTS:-A B}; do
     DOFS_LIB=$PWD/exp/$v/libdofs_hip.so timeout -k 10 300 python bench.py --cpu-frames 0 ${ARGS:-} > gpurun_out/ab_$v$i.log 2>&1 || exit 1
-    tail -1 gpurun_out/ab_$v$i.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); s=d['stages_ms_per_batch']; print('$v', d['value'], d['ms_per_step'], ' '.join(f'{k}={v}' for k, v in s.items()))"
+    tail -1 gpurun_out/ab_$v$i.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); s=d['stages_ms_per_batch'] or {}; print('$v', d['value'], d['ms_per_step'], d.get('ms_per_step_median'), ' '.join(f'{k}={v}' for k, v in s.items()))"
   done
 done

@@ -15,7 +15,7 @@ from denseopticalflowsegmentation3d_amd import runtime  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 96
 NB = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 H, W = 1080, 1920
-ctx = runtime.Dofs(0)
+ctx = runtime.Dofs(0, lib=os.environ.get("DOFS_LIB") or None)  # DOFS_LIB: another build, for A/B
 L = ctx.lib
 L.dofs_debug_flow_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 persp, inv, up = runtime.calib()
