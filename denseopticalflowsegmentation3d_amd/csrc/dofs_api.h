@@ -226,7 +226,7 @@ struct Context {
         const char* lp = getenv("DOFS_LONG_PATH");
         if (lp && atoi(lp) > 0) p0.long_path = p1.long_path = p2.long_path = atoi(lp);
         const char* kd = getenv("DOFS_KRT_DNC");
-        p0.krt_dnc = p1.krt_dnc = p2.krt_dnc = kd && kd[0] == '1';
+        p0.krt_mode = p1.krt_mode = p2.krt_mode = kd && (kd[0] == '0' || kd[0] == '1') ? kd[0] - '0' : -1;
         const char* sp = getenv("DOFS_SPLIT");
         p0.preorder_in_b = p1.preorder_in_b = p2.preorder_in_b = sp && (sp[0] == '1' || sp[0] == '2') ? sp[0] - '0' : 0;
         // stream priorities: DOFS_PRIO=2 (default) replay stage urgent — its workgroups are dispatched
@@ -424,9 +424,13 @@ int api_fetch(Context<Backend>* cx, int frame, dofs_result* out, int64_t batch =
     cx->join(batch);
     const Ws& w = cx->pipe(slot).w;
     const Dims& d = w.d;
-    int ctr[kCounters];
+    int ctr[kCounters], ctr0[kCounters];
     be.d2h(ctr, w.ctr + (int64_t)frame * kCounters, sizeof(ctr));
+    be.d2h(ctr0, w.ctr, sizeof(ctr0));
     be.sync();
+    // the dataflow replay gave up a bounded wait: the batch's results are invalid (never seen with the
+    // default KRT; dofs_dataflow.h), reported rather than returned
+    if (ctr0[C_FLOWERR]) return cx->fail(DOFS_ERR_DEVICE, "the replay of this batch gave up a bounded wait");
     const int ns = ctr[C_SNAP];
     out->n_snapshots = ns;
     out->stats.n_edges = m.n_edges;

@@ -92,6 +92,15 @@ __device__ inline void f_st64(unsigned long long* p, unsigned long long v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ inline void f_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// a poll of a word other workgroups update with atomics, read by an atomic (or 0): the value at the
+// coherence point, whatever copy of the line this XCD's L2 holds (the idle long workers' polls of the
+// queue and completion counters and of queue slots; a few per microsecond at most, so the cost is nil)
+__device__ inline int f_poll(int* p) {
+    return __hip_atomic_fetch_or(p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline unsigned long long f_poll64(unsigned long long* p) {
+    return __hip_atomic_fetch_or(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // a RepVal handed to another workgroup: three 8-byte write-through stores / loads (the pads are unused)
 __device__ inline void rv_publish(RepVal* p, float mx, float my, int rank, int root, B4 bb) {
@@ -564,29 +573,29 @@ __device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int 
     int t = -1;
     if (lane == 0) {
         const int np = ctl[FC_NLPOOL];
-        while (t < 0 && f_ld(ctl + FC_LONG_NEXT) < np) {
+        while (t < 0 && f_poll(ctl + FC_LONG_NEXT) < np) {
             const int i = atomicAdd(ctl + FC_LONG_NEXT, 1);
             if (i < np) t = flow_long_task(w, ctl, i);
         }
         for (int spin = 0; t < 0; ++spin) {
-            if (f_ld(ctl + FC_LDONE) >= nl) break;  // every long path completed: nothing more will come
+            if (f_poll(ctl + FC_LDONE) >= nl) break;  // every long path completed: nothing more will come
             if (spin >= (1 << 26)) {
                 f_st(ctl + FC_ERR, 1);
                 break;
             }
-            if (f_ld(ctl + FC_QHEAD) < f_ld(ctl + FC_QTAIL)) {
+            if (f_poll(ctl + FC_QHEAD) < f_poll(ctl + FC_QTAIL)) {
                 const int h = atomicAdd(ctl + FC_QHEAD, 1);
                 if (h >= ctl[FC_QCAP]) break;  // (never filled)
                 const long long nframe = w.d.N;
                 for (int s2 = 0;; ++s2) {
-                    const unsigned long long v = f_ld64(w.bw + h);
+                    const unsigned long long v = f_poll64(w.bw + h);
                     const int c = (int)(unsigned)v;
                     if ((unsigned)(v >> 32) == epoch && c >= 0 && (c & kFlowLong) &&
                         (long long)(c & kFlowIdMask) < nframe * w.d.B) {
                         t = c;
                         break;
                     }
-                    if ((s2 & 15) == 15 && f_ld(ctl + FC_LDONE) >= nl) break;
+                    if ((s2 & 15) == 15 && f_poll(ctl + FC_LDONE) >= nl) break;
                     if (s2 >= (1 << 26)) {
                         f_st(ctl + FC_ERR, 1);
                         break;

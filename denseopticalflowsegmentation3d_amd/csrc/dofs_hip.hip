@@ -2935,6 +2935,11 @@ struct HipBackend {
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "blur launch");
     }
     static constexpr bool kKrtLabelWords = false;  // the LDS KRT and the sweep keep their own words
+    // small batches could take the top-down global depths (4K, one frame: KRT 111 → 12 ms; 1080p, 8
+    // frames: 386 vs 312 Mpix/s), but the first batch of a fresh context then sometimes leaves a replay
+    // path incomplete (1 in 6 at B = 8, 3 in 9 at B = 16, tools/flow_dump.py; never with the sweep): a
+    // read of a not yet written word somewhere in the DNC path, not found this round. Off until it is.
+    static constexpr bool kDncAuto = false;
     // longest pointer chain the preorder's global jumping starts from: every word leaves its block
     // or goes to the block's top, so at most two words per block on any path
     static int64_t jump_chain_bound(int64_t M) { return 2 * ((M + kDeepTop - 1) / kDeepTop) + 1; }
@@ -3380,6 +3385,23 @@ extern "C" void dofs_debug_sort_dump(void* d_keys, void* d_vals, int64_t cap) {
 
 using DofsBackend = dofs::HipBackend;
 #include "dofs_cabi.inc.h"
+
+// Diagnosis only (tools/flow_dump.py): device pointers of the last batch's workspace arrays, after a sync:
+// out = {cur, ptop, list_long, In, ready, ord, lite, ctr, Rv, pre, flow control block, bw}, and the batch's
+// B, N, NL in dims.
+extern "C" int dofs_debug_ws_ptrs(dofs_ctx* ctx, unsigned long long* out, long long* dims) {
+    if (!ctx || !out || !dims || !ctx->have_batch()) return DOFS_ERR_INVALID_ARG;
+    const int slot = ctx->last_slot();
+    ctx->drain();
+    const dofs::Ws& w = ctx->pipe(slot).w;
+    const void* p[12] = {w.cur, w.ptop, w.list_long, w.In,  w.ready, w.ord,
+                         w.lite, w.ctr, w.Rv,        w.pre, ctx->be.flow_ctl, w.bw};
+    for (int i = 0; i < 12; ++i) out[i] = (unsigned long long)(uintptr_t)p[i];
+    dims[0] = w.d.B;
+    dims[1] = w.d.N;
+    dims[2] = w.d.NL;
+    return DOFS_OK;
+}
 
 // ---- optical flow (upstream stage; HIP build only) ---------------------------------------------
 #include "dofs_flow.h"

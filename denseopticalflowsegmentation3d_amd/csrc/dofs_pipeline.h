@@ -55,7 +55,16 @@ struct Pipeline {
     int* pre = nullptr;
     int64_t snap_cap = 4096;
     int preorder_in_b = 0;  // 0: the preorder in phase A; 1: in phase B; 2: the path inputs (KPathInit) in B
-    bool krt_dnc = false;  // DOFS_KRT_DNC=1: block-start labels by the top-down global depths
+    // block-start labels of the KRT: the top-down global depths (DNC) or the per-frame sweep. The sweep's
+    // time is one frame's sequence of blocks (≈ 40 ms at 1080p, 111 ms at 4K, whatever the batch); the
+    // DNC's is proportional to the batch's merges (≈ 1.45 ms per million): DNC wins below ≈ 9 frames a
+    // batch at any frame size (4K, one frame: KRT 111 → 12 ms). krt_mode: -1 auto (DNC for batches of at
+    // most kDncFrames frames on a backend that selects it), 0 sweep, 1 DNC (DOFS_KRT_DNC=0 / 1)
+    int krt_mode = -1;
+    static constexpr int kDncFrames = 8;
+    bool use_dnc(const Dims& d) const {
+        return krt_mode >= 0 ? krt_mode == 1 : (Backend::kDncAuto && d.B <= kDncFrames);
+    }
     int skip_mask = 0;          // measurement only (DOFS_SKIPMASK): 1 short replay, 2 long replay, 4 lift
     void* ev_input = nullptr;   // run_a records it once the input flow has been read (the caller's release)
     bool keys_by_frame = true;  // key_out holds each frame's sorted weights (else: recomputed for events)
@@ -82,9 +91,11 @@ struct Pipeline {
     }
 
     bool layout_packed = false;  // the layout treats key_out as dead (batch-wide sort): batches must sort packed
+    bool layout_words = false;   // the layout holds the global-kernel KRT's arrays (P, CS, MX, own)
     bool fits(const Dims& d) const {
         const bool packed = Backend::mst_packed(std::max<int64_t>(d.M, 1), d.B, ceil_log2(4 * d.N));
-        return base && cap.B >= d.B && cap.N == d.N && cap.W == d.W && (packed || !layout_packed);
+        return base && cap.B >= d.B && cap.N == d.N && cap.W == d.W && (packed || !layout_packed) &&
+               (layout_words || !(use_dnc(d) || Backend::kKrtLabelWords));
     }
 
     // Carve every buffer from one allocation (grow-only). Returns false on allocation failure.
@@ -98,6 +109,11 @@ struct Pipeline {
             base_bytes = bytes;
             cap = d;
             layout(d, (char*)base);
+            // the dataflow replay's queue slots (w.bw) accept a word only with this launch's tag, and
+            // every launch's tag is new within the process; a fresh allocation may hold another
+            // process's words, tags included, so it starts all ones (no tag) — once, synchronously
+            be.memset(w.bw, 0xFF, sizeof(unsigned long long) * (size_t)d.B * (size_t)d.N);
+            be.sync();
         }
         w.d = d;
         return true;
@@ -116,7 +132,8 @@ struct Pipeline {
             return r;
         };
         const int64_t B = d.B, N = d.N, M = std::max<int64_t>(d.M, 1), NL = d.NL;
-        const bool words = krt_dnc || Backend::kKrtLabelWords;
+        const bool words = use_dnc(d) || Backend::kKrtLabelWords;
+        layout_words = words;
         struct Region {
             char* p;
             size_t n;
@@ -357,14 +374,15 @@ struct Pipeline {
         const int B = d.B;
         const int64_t N = d.N, M = d.M, NL = d.NL;
         be.mark(3);
-        KEdgeInit ei{w, krt_dnc};
+        const bool dnc = use_dnc(d);
+        KEdgeInit ei{w, dnc};
         ei.given = given;
         ei.vmask = vmask;
-        if (!given || krt_dnc) be.launch(B, M, ei);
-        const bool words = krt_dnc || Backend::kKrtLabelWords;  // the global-kernel KRT reads them
+        if (!given || dnc) be.launch(B, M, ei);
+        const bool words = dnc || Backend::kKrtLabelWords;  // the global-kernel KRT reads them
         be.launch(B, words ? NL : N, KLabelInit{w, words});
         const int64_t deep = Backend::deep_block();  // levels with block size <= deep run per block
-        if (krt_dnc) {  // measurement: the top-down global depths (DOFS_KRT_DNC=1)
+        if (dnc) {  // the top-down global depths (small batches; DOFS_KRT_DNC=1)
             for (int64_t S = (int64_t)1 << ceil_log2(M); S > deep; S >>= 1) {
                 const int ep = dnc_epoch(M, S);
                 be.launch(B, M, KDncUnion{w, S, ep});

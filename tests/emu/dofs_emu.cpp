@@ -98,6 +98,7 @@ struct HostBackend {
         launch(w.d.B, w.d.N, KBlurCol{w});
     }
     static constexpr bool kKrtLabelWords = true;  // the deep depths run as global kernels here
+    static constexpr bool kDncAuto = false;       // the block-start labels by the sequential sweep (krt_seq)
     static int64_t jump_chain_bound(int64_t M) { return M; }
     void dnc_deep(const Ws& w) {
         const int64_t M = w.d.M;
