@@ -39,10 +39,10 @@ for b in range(NB):
     print(f"batch {b}: flowerr {int(c[0, 58])}", flush=True)
     if not c[0, 58]:
         continue
-    ptrs = (C.c_ulonglong * 12)()
+    ptrs = (C.c_ulonglong * 18)()
     dims = (C.c_longlong * 3)()
     assert L.dofs_debug_ws_ptrs(ctx.ctx, ptrs, dims) == 0
-    cur_p, ptop_p, ll_p, in_p, ready_p, ord_p, lite_p, ctr_p, rv_p, pre_p, ctl_p, bw_p = [int(x) for x in ptrs]
+    cur_p, ptop_p, ll_p, in_p, ready_p, ord_p, lite_p, ctr_p, rv_p, pre_p, ctl_p, bw_p = [int(x) for x in ptrs][:12]
     Bd, N, NL = int(dims[0]), int(dims[1]), int(dims[2])
     ctl = d2h(ctl_p, 0, 4 * 8 * 64, np.int32)
     qh, qt = int(ctl[2 * 64]), int(ctl[3 * 64])
