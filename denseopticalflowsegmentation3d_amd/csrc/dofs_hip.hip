@@ -883,8 +883,11 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
             const int x = beg + u;
             gk[u] = x < end ? sh.hkey[x] : -1;
         }
+        // agent-scope (L1-bypassing) loads: a label may be a merge of this block whose size this
+        // workgroup stored moments ago (top_level, the first half's deep_block) into a line its L1
+        // still holds from an earlier load — a plain load could return the line's old bytes
 #pragma unroll
-        for (int u = 0; u < per; ++u) gz[u] = w.SZ[lb + (gk[u] >= d.N ? gk[u] : 0)];
+        for (int u = 0; u < per; ++u) gz[u] = dofs_ld(w.SZ + lb + (gk[u] >= d.N ? gk[u] : 0));
 #pragma unroll
         for (int u = 0; u < per; ++u)
             if (gk[u] != -1) {
@@ -1048,7 +1051,7 @@ __device__ void top_level(const Ws& w, TopShared& sh, int f, int64_t s0, int cnt
             if (sh.hkey[x] != -1) {
                 sh.hval[x] = (short)base;
                 const int g = sh.hkey[x];
-                sh.SZ[base] = g < d.N ? 1 : w.SZ[lb + g];  // a pixel label is a leaf (size 1): no load
+                sh.SZ[base] = g < d.N ? 1 : dofs_ld(w.SZ + lb + g);  // a pixel: a leaf of size 1 (no load)
                 ++base;
             }
     }
@@ -2936,9 +2939,9 @@ struct HipBackend {
     }
     static constexpr bool kKrtLabelWords = false;  // the LDS KRT and the sweep keep their own words
     // small batches could take the top-down global depths (4K, one frame: KRT 111 → 12 ms; 1080p, 8
-    // frames: 386 vs 312 Mpix/s), but the first batch of a fresh context then sometimes leaves a replay
-    // path incomplete (1 in 6 at B = 8, 3 in 9 at B = 16, tools/flow_dump.py; never with the sweep): a
-    // read of a not yet written word somewhere in the DNC path, not found this round. Off until it is.
+    // frames: 386 vs 312 Mpix/s), but the first batch of a fresh context then sometimes gets a few node
+    // sizes one too large (1 in 6 at B = 8, tools/krt_race.py), which flips a heavy/light choice and
+    // leaves a replay path incomplete; never with the sweep. Off until that is found.
     static constexpr bool kDncAuto = false;
     // longest pointer chain the preorder's global jumping starts from: every word leaves its block
     // or goes to the block's top, so at most two words per block on any path
