@@ -1753,6 +1753,11 @@ __global__ __launch_bounds__(kAggT) void k_dnc_compress(Ws w, int64_t S, int ep)
         // only the workgroup's max rank of a component can be the component's max (its L-root):
         // own = the root for those candidates, -1 for the others (KDncLRootRelabel skips them)
         if (act) w.own[f * d.M + i] = hmx[slot] == (mtag | (int)i) ? r : -1;
+        // every lane has read its slot's maximum before any slot is cleared below (without this
+        // barrier a wave that is still on the line above can read a slot another wave has already
+        // cleared: its L-root then never writes the component's size and CS[r] leaks into the next
+        // depth — the DNC first-batch "size one too large" of round 3)
+        __syncthreads();
         for (int x = tid; x < kAggHT; x += kAggT) {
             const int k = hk[x];
             if (k < 0) continue;
