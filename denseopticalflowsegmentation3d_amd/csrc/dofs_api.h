@@ -229,11 +229,13 @@ struct Context {
         p0.krt_mode = p1.krt_mode = p2.krt_mode = kd && (kd[0] == '0' || kd[0] == '1') ? kd[0] - '0' : -1;
         const char* sp = getenv("DOFS_SPLIT");
         p0.preorder_in_b = p1.preorder_in_b = p2.preorder_in_b = sp && (sp[0] == '1' || sp[0] == '2') ? sp[0] - '0' : 0;
-        // stream priorities: DOFS_PRIO=2 (default) replay stage urgent — its workgroups are dispatched
-        // first when a CU frees up, since the replay rounds are the pipeline's critical chain;
-        // 1 = graph stage urgent, replay stage least (experiment); 0 = equal
+        // stream priorities: DOFS_PRIO=1 (default) graph stage urgent, replay stage least — its workgroups
+        // are dispatched first when a CU frees up, since the graph stage (Borůvka, sort, KRT, preorder)
+        // bounds the step; the long-path workers keep their own top-priority stream. 2 = replay stage
+        // urgent (the default while the replay ran in rounds and was the critical chain), 0 = equal.
+        // Round 3, B = 112, same box (Mpix/s): 1 → 1,559 / 1,561, 2 → 1,499 / 1,499, 0 → 1,253 / 1,255
         const char* pr = getenv("DOFS_PRIO");
-        const int prio = pr ? atoi(pr) : 2;
+        const int prio = pr ? atoi(pr) : 1;
         // DOFS_DUAL_A=1: two graph-stage streams, batches alternating — batch k + 1's graph stage starts
         // once batch k has read its input, so one batch's latency-bound sweeps (KRT, preorder) may overlap
         // the next one's bandwidth-bound kernels. Measured equal to one stream (B = 112, same box: 1,485 /

@@ -75,7 +75,18 @@ enum FlowStat {
     FS_SROUNDS = 11,   // flow_short calls
     FS_STICKS = 12,    // wall time inside flow_short, summed over waves
     FS_LSTEPS = 13,    // merges replayed by long paths
-    FS_N = 16
+    FS_T_ROOT = 14,    // last completion of a frame's root heavy path (top at preorder 0; max)
+    FS_RPARKS = 15,    // parks of root heavy paths
+    FS_RSTEPS = 16,    // merges replayed by root heavy paths
+    FS_RCHUNKS = 17,   // 64-step chunks of root heavy paths
+    // measurement build only (-DDOFS_FLOW_PROF): 100 MHz ticks of the long-path chunk loop, summed over
+    // waves — the steps (with the chunk's first LDS wait), the bbox scan and record stores, and the wait
+    // for the next chunk's resolve loads before they go to LDS
+    FS_P_STEPS = 18,
+    FS_P_TAIL = 19,
+    FS_P_NEXT = 20,
+    FS_KFAST = 21,     // long-path chunks run with a constant key (no step reaches the carried rank)
+    FS_N = 24
 };
 __device__ unsigned long long g_fs[FS_N * kFsStride];
 __device__ inline unsigned long long fs_now() { return __builtin_amdgcn_s_memrealtime(); }
@@ -261,7 +272,7 @@ __device__ inline int flow_resolve(const Ws& w, int64_t lb, int p, int top, OneR
 
 // A long path (task word t) on this wave, from its cursor: returns the task word of the parent path
 // that was parked on its top (to run next), or -1 (parked itself, or completed with nobody waiting).
-__device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut* ob) {
+__device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut* ob, int keyfast) {
     const Dims& d = w.d;
     const int g = t & kFlowIdMask;
     const int f = g / (int)d.N, j = g - f * (int)d.N;
@@ -287,11 +298,35 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
     B4 lbb;
     int meta = flow_resolve(w, lb, q - lane, top, &rec, &lbb);
     buf[cb][lane] = rec;
-    unsigned chunks = 0, steps = 0;  // anatomy, added once per call
+    unsigned curlk = rec.lk;  // this lane's step key in the current chunk (valid for lanes < n)
+    unsigned chunks = 0, steps = 0, kfast = 0;  // anatomy, added once per call
+#ifdef DOFS_FLOW_PROF
+    unsigned long long p_steps = 0, p_tail = 0, p_next = 0, p_t = wall_clock64();
+#define FLOW_PROF_MARK(acc)                                 \
+    do {                                                    \
+        const unsigned long long p_now = wall_clock64();   \
+        acc += p_now - p_t;                                 \
+        p_t = p_now;                                        \
+    } while (0)
+#else
+#define FLOW_PROF_MARK(acc) \
+    do {                    \
+    } while (0)
+#endif
     auto tally = [&]() {
         if (lane == 0) {
+#ifdef DOFS_FLOW_PROF
+            fs_add(FS_P_STEPS, p_steps);
+            fs_add(FS_P_TAIL, p_tail);
+            fs_add(FS_P_NEXT, p_next);
+#endif
             fs_add(FS_LCHUNKS, chunks);
             fs_add(FS_LSTEPS, steps);
+            fs_add(FS_KFAST, kfast);
+            if (top == 0) {
+                fs_add(FS_RCHUNKS, chunks);
+                fs_add(FS_RSTEPS, steps);
+            }
         }
     };
     for (;;) {
@@ -322,6 +357,46 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             ob[2 * k + h] = o;
         };
         auto lda = [&](int k) { return *reinterpret_cast<const uint4*>(&c[k]); };
+        // Constant-key chunks: union by rank (graph.cpp:177-182, 210-213) leaves the carried key K
+        // unchanged at a step whose light child has a lower rank (max(K, lk) = K). A lane checks its
+        // own step against K's rank; when no step of the chunk reaches it (the common case: after
+        // a path's first steps its light children are mostly pixels, rank 0), every step's key is K and
+        // the loop carries only the mean chain — one LDS read, five VALU and one LDS store per step
+        // instead of the ~16 instructions with the key update.
+        const unsigned krank = K & ~((1u << kRankShift) - 1);
+        if (keyfast && __ballot(lane < n && curlk >= krank) == 0) {
+            ++kfast;
+            auto stepf = [&](int k, OneHalf b) {
+                v = (float)((double)(v * b.fs + b.wb) * b.r);
+                OneOut o;
+                o.v = v;
+                o.k = K;
+                ob[2 * k + h] = o;
+            };
+            int k = 0;
+            OneHalf b0 = c[0].h[h], b1 = c[1].h[h], b2 = c[2].h[h], b3 = c[3].h[h];
+            for (; k + 8 <= n; k += 8) {
+                const int m = k + 4, m2 = (k + 8) & 63;
+                const OneHalf d0 = c[m].h[h], d1 = c[m + 1].h[h], d2 = c[m + 2].h[h], d3 = c[m + 3].h[h];
+                stepf(k, b0);
+                stepf(k + 1, b1);
+                stepf(k + 2, b2);
+                stepf(k + 3, b3);
+                b0 = c[m2].h[h], b1 = c[m2 + 1].h[h], b2 = c[m2 + 2].h[h], b3 = c[m2 + 3].h[h];
+                stepf(k + 4, d0);
+                stepf(k + 5, d1);
+                stepf(k + 6, d2);
+                stepf(k + 7, d3);
+            }
+            if (k + 4 <= n) {
+                stepf(k, b0);
+                stepf(k + 1, b1);
+                stepf(k + 2, b2);
+                stepf(k + 3, b3);
+                k += 4;
+            }
+            for (; k < n; ++k) stepf(k, c[k].h[h]);
+        } else {
         // two register sets, each reloaded right after its last use (4 steps ahead of its next use): no
         // loop-carried copies (the single-set form with next-group temporaries compiled to ~4 v_mov per step)
         int k = 0;
@@ -350,6 +425,8 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             k += 4;
         }
         for (; k < n; ++k) step(k, lda(k), c[k].h[h]);
+        }
+        FLOW_PROF_MARK(p_steps);
         B4 obb;
         {  // bbox: inclusive prefix join over the chunk (lane = step), then the carried box
             B4 x = lbb;
@@ -400,6 +477,7 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
                 if (t & kFlowLong) atomicAdd(ctl + FC_LDONE, 1);
                 fs_add(FS_LDONE, 1);
                 fs_max(FS_T_LONG, fs_now());
+                if (top == 0) fs_max(FS_T_ROOT, fs_now());
             }
             old = __shfl(old, 0, 64);
             tally();
@@ -424,7 +502,10 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             }
             parked = __shfl(parked, 0, 64);
             if (parked) {
-                if (lane == 0) fs_add(FS_LPARKS, 1);
+                if (lane == 0) {
+                    fs_add(FS_LPARKS, 1);
+                    if (top == 0) fs_add(FS_RPARKS, 1);
+                }
                 tally();
                 return -1;
             }
@@ -432,13 +513,20 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             __builtin_amdgcn_wave_barrier();
             meta = flow_resolve(w, lb, q - lane, top, &rec, &lbb, pb);
             buf[cb][lane] = rec;
+            curlk = rec.lk;
             continue;
         }
         q -= 64;
         cb ^= 1;
         meta = nmeta;
         lbb = nlbb;
+#ifdef DOFS_FLOW_PROF
+        FLOW_PROF_MARK(p_tail);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        FLOW_PROF_MARK(p_next);
+#endif
         buf[cb][lane] = nrec;
+        curlk = nrec.lk;
     }
 }
 
@@ -626,7 +714,7 @@ __device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int 
 // Measured (112 frames, 1080p, tools/flow_stats.py, serial): short paths done at 26.7 ms, the last
 // chain at 42.4 ms; same-box bench 1,518-1,540 Mpixels/s with 128 long and 2,048 short workers.
 template <bool kLong, int kW>
-__global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigned epoch) {
+__global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigned epoch, int keyfast) {
     __shared__ OneRec buf[kLong ? kW : 1][2][64];
     __shared__ OneOut ob[kLong ? kW : 1][128];
     const int lane = threadIdx.x & 63;
@@ -642,7 +730,7 @@ __global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigne
             const unsigned long long t1 = fs_now();
             while (t >= 0) {
                 if (lane == 0) fs_add(FS_LRUNS, 1);
-                const int nx = flow_long(w, ctl, t, buf[wv], ob[wv]);
+                const int nx = flow_long(w, ctl, t, buf[wv], ob[wv], keyfast);
                 if (nx >= 0 && !(nx & kFlowLong)) {  // a short waiter: a one-lane short round (and its waiters)
                     if (lane == 0) fs_add(FS_INJECT, 1);
                     flow_short(w, ctl, epoch, nx, false, &cb, &ce);

@@ -2943,11 +2943,10 @@ struct HipBackend {
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "blur launch");
     }
     static constexpr bool kKrtLabelWords = false;  // the LDS KRT and the sweep keep their own words
-    // small batches could take the top-down global depths (4K, one frame: KRT 111 → 12 ms; 1080p, 8
-    // frames: 386 vs 312 Mpix/s), but the first batch of a fresh context then sometimes gets a few node
-    // sizes one too large (1 in 6 at B = 8, tools/krt_race.py), which flips a heavy/light choice and
-    // leaves a replay path incomplete; never with the sweep. Off until that is found.
-    static constexpr bool kDncAuto = false;
+    // small batches take the top-down global depths (4K, one frame: KRT 111 → 12 ms; 1080p, 8 frames:
+    // 386 vs 312 Mpix/s). Round 3's first-batch size error of this path (1 in 6 fresh contexts) was the
+    // slot-table race in k_dnc_compress, fixed there; tests/test_gpu_krt_dnc.py holds the two modes equal.
+    static constexpr bool kDncAuto = true;
     // longest pointer chain the preorder's global jumping starts from: every word leaves its block
     // or goes to the block's top, so at most two words per block on any path
     static int64_t jump_chain_bound(int64_t M) { return 2 * ((M + kDeepTop - 1) / kDeepTop) + 1; }
@@ -3137,6 +3136,17 @@ struct HipBackend {
         }();
         return g;
     }
+    // constant-key chunks in the long-path loop (dofs_dataflow.h): the chain carries only the mean where
+    // no step of a 64-step chunk reaches the carried rank. DOFS_KEYFAST=0 / 1; default on (96 % of the
+    // chunks; one 4K frame's replay 93 → 72 ms; B = 112 with the graph stage urgent, same box: 1,559 /
+    // 1,561 vs 1,546 / 1,535 Mpix/s)
+    static int keyfast(const Dims&) {
+        static const int m = [] {
+            const char* e = getenv("DOFS_KEYFAST");
+            return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+        }();
+        return m >= 0 ? m : 1;
+    }
     static int flow_long_workers() {  // waves that run long paths (the rest of the grid runs short ones)
         static const int g = [] {
             const char* e = getenv("DOFS_FLOW_LONG");
@@ -3174,10 +3184,11 @@ struct HipBackend {
             const int gl = (flow_long_workers() + kFlowLongW - 1) / kFlowLongW;
             note(hipEventRecord(flow_ev[0], stream), "hipEventRecord");
             note(hipStreamWaitEvent(flow_stream, flow_ev[0], 0), "hipStreamWaitEvent");
+            const int kf = keyfast(w.d);
             hipLaunchKernelGGL((k_replay_flow<true, kFlowLongW>), dim3((unsigned)gl), dim3(64 * kFlowLongW), 0, flow_stream,
-                               w, flow_ctl, flow_epoch);
+                               w, flow_ctl, flow_epoch, kf);
             hipLaunchKernelGGL((k_replay_flow<false, kFlowShortW>), dim3((unsigned)gs), dim3(64 * kFlowShortW), 0, stream,
-                               w, flow_ctl, flow_epoch);
+                               w, flow_ctl, flow_epoch, kf);
             note(hipEventRecord(flow_ev[1], flow_stream), "hipEventRecord");
             note(hipStreamWaitEvent(stream, flow_ev[1], 0), "hipStreamWaitEvent");
         });
