@@ -2962,16 +2962,17 @@ struct HipBackend {
             launch(w.d.B, w.d.N, KSeqInitRec{reinterpret_cast<SeqRec*>(w.In), 2 * w.d.NL});
             // persistent workgroups: the frames' sweeps plus `extra` LDS-KRT workers (DOFS_FUSED_EXTRA),
             // at most one per CU. A workgroup holds a whole CU (151 KB of LDS, all VGPRs), so the
-            // other stream's replay cannot run beside it: by default 1/16 of the CUs stay free for it
-            // (round 3, dataflow replay, B = 96: 240 workgroups 1,449 Mpix/s, 224 1,425; round 2's
-            // round-based replay needed 1/8: 224 workgroups 982, 256 957, 160 909)
+            // other stream's replay cannot run beside it. With the graph stage urgent and the
+            // constant-key replay (round 3, B = 112, same box) every CU: 256 workgroups 1,593 / 1,586 /
+            // 1,584 / 1,587 Mpix/s against 240 (1/16 of the CUs left to the replay, the earlier default)
+            // 1,551 / 1,543 / 1,549 / 1,544; round 2's round-based replay needed 1/8 free: 224 982, 256 957
             static const int extra = [] {
                 const char* e = getenv("DOFS_FUSED_EXTRA");
                 return e ? atoi(e) : -1;
             }();
             int dev_cus = 256;
             (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, device);
-            const int cap = extra < 0 ? dev_cus - dev_cus / 16 : dev_cus;
+            const int cap = dev_cus;
             const int nwg = std::max(1, std::min(cap, extra < 0 ? cap : w.d.B + extra));
             timed("k_krt_fused", [&] {
                 hipLaunchKernelGGL(k_krt_fused, dim3((unsigned)nwg), dim3(kDeepT), 0, stream, w, w.ctr + C_PROG);
