@@ -15,3 +15,4 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --cpu-frames 0 --no-h2d
 B=112 bash tools/pmc_round.sh > gpurun_out/pmc_round.log 2>&1; rc=$?; tail -3 gpurun_out/pmc_round.log; [ $rc -eq 0 ] || exit $rc
 step bench_final 500 python bench.py --pmc gpurun_out/pmc/pmc_kernels.json
+step intraframe_model 300 python tools/bench_intraframe.py --model 4
