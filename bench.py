@@ -56,7 +56,9 @@ BYTES = {"k_boruvka_min4": (12, 16), "k_boruvka_pick4": 16, "k_boruvka_min": (24
          "k_replay_long": 64, "k_replay_flow": 64}
 PROBES = ("k_boruvka_min4", "k_boruvka_pick4", "k_krt_fused", "k_replay_flow", "k_replay_long")
 C_FLOWERR = 58         # counters (frame 0): the dataflow replay gave up a bounded wait
-ROOF_KERNEL = "k_boruvka_min4"
+INPUT_SETS = 3         # distinct resident input batches, rotated over the steps
+# measurement-only knobs of the library that make results invalid (they skip work): refused
+INVALID_KNOBS = ("DOFS_SKIP_B", "DOFS_SKIPMASK")
 
 
 def ceil_log2(n):
@@ -106,7 +108,7 @@ def parse(argv=None):
     ap.add_argument("--no-stages", action="store_true", help="skip the per-stage event timing pass")
     ap.add_argument("--no-h2d", action="store_true", help="skip the with-H2D (host input) pass")
     ap.add_argument("--probe", default=",".join(PROBES), help="kernels timed with device events (comma list)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03", "pmc_kernels.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r04", "pmc_kernels.json"),
                     help="PMC summary JSON (tools/pmc_kernels.py via tools/pmc_round.sh) for the roofline traffic; "
                          "used only when its lib_sha256 is the loaded library's")
     ap.add_argument("--cpu-worker", nargs=4, metavar=("OPT", "H", "W", "SEED"), help=argparse.SUPPRESS)
@@ -147,13 +149,21 @@ def _mem_avail_gb():
 
 def cpu_baseline(a):
     """`procs` concurrent single-thread processes (the reference is single-threaded; one frame per core),
-    capped by the box's CPU share (16 per GPU) and by ~1.5 GB of host RAM per 1080p frame; each runs
-    --cpu-frames synthetic frames of the bench workload. Runs before this process touches the GPU."""
+    one per host thread of this GPU's CPU share, capped by ~1.5 GB of host RAM per 1080p frame; each runs
+    --cpu-frames synthetic frames of the bench workload. Runs before this process touches the GPU.
+
+    The share: a one-GPU box of this pool is one GPU of an 8-GPU host whose `nproc` shows the whole
+    machine's hardware threads (256 on the EPYC 9575F hosts) but whose harness allots 16 of them per GPU
+    (its OMP_NUM_THREADS / MAX_JOBS); BASELINE.md's "nproc processes capped by RAM" on a dedicated host is
+    reported beside it as an extrapolation from the measured per-frame time (`nproc_extrapolated`), and so
+    is config 4's 512-frame job."""
     from oracle import binding as ob
     H, W = a.height, a.width
     share = len(os.sched_getaffinity(0))
     per_frame_gb = 1.5 * H * W / 2073600
-    procs = a.cpu_procs or max(1, min(16, share, int(_mem_avail_gb() * 0.5 / per_frame_gb)))
+    gpu_share = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)  # the harness's per-GPU CPU share
+    ram_cap = int(_mem_avail_gb() * 0.5 / per_frame_gb)
+    procs = a.cpu_procs or max(1, min(gpu_share, share, ram_cap))
     out = {"unit": "Mpixels/sec", "kind": "port", "cores": procs, "nproc": os.cpu_count(), "affinity": share,
            "cpu_model": _cpu_model()}
     for opt in a.cpu_opt.split(","):
@@ -178,10 +188,21 @@ def cpu_baseline(a):
                     "single_core_mpix_s": round(H * W / per[len(per) // 2] / 1e6, 4)}
     first = a.cpu_opt.split(",")[0]
     out["value"] = out[first]["value"]
-    out["sample"] = (f"{procs} concurrent processes x {a.cpu_frames} synthetic {W}x{H} frame(s) each (seeds "
-                     f"0..{procs * a.cpu_frames - 1}), faithful mode (std::multiset edge sort + std::set unions + "
-                     f"set-copy snapshots), one thread per process; value = {first} build; g++ "
-                     + " and ".join(f"-{o}: {out[o]['wall_s']} s wall" for o in a.cpu_opt.split(",")))
+    med = out[first]["s_per_frame"]["median"]
+    full = max(1, min(os.cpu_count() or 1, ram_cap))  # nproc processes, capped by RAM
+    out["gpu_cpu_share"] = gpu_share
+    out["nproc_extrapolated"] = {"procs": full, "value": round(full * H * W / med / 1e6, 3),
+                                 "note": f"{full} concurrent frames at the measured median {med} s per frame "
+                                         f"(nproc {os.cpu_count()}, RAM cap {ram_cap}); assumes no slowdown "
+                                         f"from memory-bandwidth contention, so an upper bound"}
+    out["job_512_frames_s"] = {"on_procs": round(-(-512 // procs) * med, 1),
+                               "on_nproc": round(-(-512 // full) * med, 1)}
+    out["sample"] = (f"{procs} concurrent processes (this GPU's CPU share) x {a.cpu_frames} synthetic {W}x{H} "
+                     f"frame(s) each (seeds 0..{procs * a.cpu_frames - 1}), faithful mode (std::multiset edge sort + "
+                     f"std::set unions + set-copy snapshots), one thread per process; value = {first} build; g++ "
+                     + " and ".join(f"-{o}: {out[o]['wall_s']} s wall" for o in a.cpu_opt.split(","))
+                     + f"; config 4's 512-frame job extrapolated: {out['job_512_frames_s']['on_procs']} s on these "
+                       f"{procs} processes, {out['job_512_frames_s']['on_nproc']} s on {full} (nproc, RAM-capped)")
     return out
 
 
@@ -217,6 +238,11 @@ def main(argv=None):
         opt, H, W, seed = a.cpu_worker
         cpu_worker(opt, int(H), int(W), int(seed))
         return 0
+    bad = [k for k in INVALID_KNOBS if os.environ.get(k, "") not in ("", "0")]
+    if bad:
+        print(f"bench.py: {', '.join(bad)} set: these skip work and invalidate every result; refusing to run",
+              file=sys.stderr)
+        return 2
     world = int(os.environ.get("WORLD_SIZE", "0"))
     if world == 0:
         if a.gpus > 1:
@@ -264,9 +290,15 @@ def main(argv=None):
         frames_per_step = a.frames
         B = chunks[0][1]
     else:
+        # INPUT_SETS distinct batches of fields, each resident in HBM, used in turn by consecutive steps: no
+        # step sees the inputs of the step before it (a stale-state bug cannot hide behind repeated inputs)
         B = a.batch
-        flows = torch.empty((B, H, W, 2), dtype=torch.float32, device=dev)
-        runtime.synth_flow_device(flows.data_ptr(), B, H, W, seed0=rank * B, stream=sh)
+        sets = []
+        for k in range(INPUT_SETS):
+            t = torch.empty((B, H, W, 2), dtype=torch.float32, device=dev)
+            runtime.synth_flow_device(t.data_ptr(), B, H, W, seed0=(rank * INPUT_SETS + k) * B, stream=sh)
+            sets.append(t)
+        flows = sets[0]
         chunks = [(0, B)]
         frames_per_step = world * B
 
@@ -276,8 +308,13 @@ def main(argv=None):
     pipe = Pipelined(fp, persp, inv, up, params=prm, stream=sh)
     flush = pipe.flush
 
+    nstep = [0]
+
     def step(src=None):
-        pipe.run_chunks(src if src is not None else flows, chunks)
+        if src is None:
+            src = flows if a.frames else sets[nstep[0] % INPUT_SETS]
+        nstep[0] += 1
+        pipe.run_chunks(src, chunks)
         if a.frames:  # one step = the whole job
             flush()
 
@@ -315,13 +352,22 @@ def main(argv=None):
     value = frames_per_step * a.steps * N / elapsed / 1e6
 
     # roofline: algorithmic bytes of each probed kernel's launches in the timed region over their
-    # device-event time (events recorded on the stream the kernel runs on); units from the last batch
-    # (every batch of the bench is the same workload shape)
-    counters = ctx.batch_counters(chunks[-1][1])
-    if counters[0, C_FLOWERR]:
-        raise RuntimeError("the dataflow replay gave up a bounded wait: results of the timed batches are invalid")
-    tiles = ctx.tile_pixels(chunks[-1][1])
-    recs = ctx.records(chunks[-1][1])
+    # device-event time (events recorded on the stream the kernel runs on). The units (processed Borůvka
+    # tiles, records, long-path merges) depend on the input: each input set's census is read from one
+    # extra, untimed batch of that set, and the timed region's units are the sum over its steps' sets.
+    timed_sets = [(a.warmup + j) % INPUT_SETS for j in range(a.steps)] if not a.frames else [0] * a.steps
+    census = {}
+    for k in sorted(set(timed_sets)):
+        if a.frames:
+            cnt = ctx.batch_counters(chunks[-1][1])
+        else:
+            pipe.run_chunks(sets[k], chunks)
+            flush()
+            torch.cuda.synchronize()
+            cnt = ctx.batch_counters(B)
+        if cnt[0, C_FLOWERR]:
+            raise RuntimeError("the dataflow replay gave up a bounded wait: results of the batches are invalid")
+        census[k] = (cnt, ctx.tile_pixels(chunks[-1][1]), ctx.records(chunks[-1][1]))
     pmc, pmc_note = {}, "no PMC summary"
     if a.pmc and os.path.exists(a.pmc):
         import hashlib
@@ -335,6 +381,33 @@ def main(argv=None):
         else:
             pmc_note = f"{os.path.relpath(a.pmc, ROOT)} is for another batch shape: traffic dropped"
     batches = a.steps * len(chunks)
+
+    def units(name, k):
+        """(algorithmic bytes of one batch of input set k, units description) for a probed kernel."""
+        cnt, tiles, recs = census[k]
+        if name == "k_boruvka_min4":
+            p0, _, _ = boruvka_min_units(tiles, cnt, N)
+            nrec = int(recs.sum())
+            return p0 * BYTES[name][0] + nrec * BYTES[name][1], {"pass0_px": p0, "records": nrec}
+        if name == "k_boruvka_pick4":
+            nrec = int(recs.sum())
+            return nrec * BYTES[name], {"records": nrec}
+        if name == "k_boruvka_min":
+            p0, p1, _ = boruvka_min_units(tiles, cnt, N)
+            return p0 * BYTES[name][0] + p1 * BYTES[name][1], {"pass0_px": p0, "pass1_px": p1}
+        if name in ("k_krt_fused", "k_replay_flow"):
+            return BYTES[name] * (N - 1) * B, {"merges": (N - 1) * B}
+        if name == "k_replay_long":
+            lm = int(cnt[:, C_LONGM].sum())
+            return BYTES[name] * lm, {"long_path_merges": lm}
+        return None, None
+
+    UNIT_TEXT = {"k_boruvka_min4": "12 per pixel of a processed tile + 16 per record written",
+                 "k_boruvka_pick4": "16 per record read",
+                 "k_boruvka_min": "24 (pass 0) / 16 (pass 1) per pixel of a processed tile",
+                 "k_krt_fused": f"{BYTES['k_krt_fused']} per merge",
+                 "k_replay_flow": f"{BYTES['k_replay_flow']} per merge (StepIn 32 B in, RepVal 32 B out)",
+                 "k_replay_long": f"{BYTES['k_replay_long']} per long-path merge"}
     kern = []
     for name, (ms, launches) in probes.items():
         if not launches:
@@ -343,33 +416,11 @@ def main(argv=None):
                  "avg_launch_us": round(ms / launches * 1e3, 2),
                  "share_of_step": round(ms / a.steps / (elapsed * 1e3 / a.steps), 4)}
         alg = None
-        if name == "k_boruvka_min4" and len(chunks) == 1:
-            p0, _, _ = boruvka_min_units(tiles, counters, N)
-            nrec = int(recs.sum())
-            alg = (p0 * BYTES[name][0] + nrec * BYTES[name][1]) * batches
-            entry["alg_bytes_per_unit"] = "12 per pixel of a processed tile + 16 per record written"
-            entry["units_per_batch"] = {"pass0_px": p0, "records": nrec}
-        elif name == "k_boruvka_pick4" and len(chunks) == 1:
-            nrec = int(recs.sum())
-            alg = nrec * BYTES[name] * batches
-            entry["alg_bytes_per_unit"] = "16 per record read"
-            entry["units_per_batch"] = {"records": nrec}
-        elif name == "k_boruvka_min" and len(chunks) == 1:
-            p0, p1, lpb = boruvka_min_units(tiles, counters, N)
-            assert launches == lpb * batches, (launches, lpb, batches)
-            alg = (p0 * BYTES[name][0] + p1 * BYTES[name][1]) * batches
-            entry["alg_bytes_per_unit"] = "24 (pass 0) / 16 (pass 1) per pixel of a processed tile"
-            entry["units_per_batch"] = {"pass0_px": p0, "pass1_px": p1}
-        elif name == "k_krt_fused" and len(chunks) == 1:
-            alg = BYTES[name] * (N - 1) * B * batches
-            entry["alg_bytes_per_unit"] = f"{BYTES[name]} per merge"
-        elif name == "k_replay_flow" and len(chunks) == 1:
-            alg = BYTES[name] * (N - 1) * B * batches
-            entry["alg_bytes_per_unit"] = f"{BYTES[name]} per merge"
-        elif name == "k_replay_long" and len(chunks) == 1:
-            alg = BYTES[name] * int(counters[:, C_LONGM].sum()) * batches
-            entry["alg_bytes_per_unit"] = f"{BYTES[name]} per long-path merge"
-            entry["units_per_batch"] = int(counters[:, C_LONGM].sum())
+        if len(chunks) == 1 and units(name, timed_sets[0])[0] is not None:
+            per_set = {k: units(name, k) for k in census}
+            alg = sum(per_set[k][0] for k in timed_sets)
+            entry["alg_bytes_per_unit"] = UNIT_TEXT[name]
+            entry["units_per_batch"] = per_set[timed_sets[-1]][1]
         if alg is not None:
             ach = alg / (ms / 1e3) / 1e9
             entry.update({"achieved": round(ach, 3), "frac": round(ach / HBM_PEAK_GBS, 6),
@@ -379,31 +430,39 @@ def main(argv=None):
                 entry["traffic"] = round(pk["hbm_bytes_per_launch"])
                 entry["traffic_over_alg"] = round(pk["hbm_bytes_per_launch"] / (alg / launches), 3)
                 entry["traffic_read_pattern"] = pk.get("read_pattern")
+                if pk.get("hbm_read_bounds"):  # raw FETCH_SIZE (random: 64 B per request) .. x2 (streaming)
+                    entry["traffic_bounds"] = [round(b + pk.get("write_size_raw_bytes", 0))
+                                               for b in pk["hbm_read_bounds"]]
+                if pk.get("read_bytes_by_request_size") is not None:
+                    entry["read_bytes_by_request_size"] = round(pk["read_bytes_by_request_size"])
         kern.append(entry)
     kern.sort(key=lambda e: -e["ms_per_batch"])
     roof = None
-    main_k = next((e for e in kern if e["kernel"] == ROOF_KERNEL and "achieved" in e), None)
+    # the headline is the dominant kernel: the probed kernel with the most device time per batch
+    main_k = next((e for e in kern if "achieved" in e), None)
     if main_k:
         roof = {"bound": "hbm", "achieved": main_k["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": main_k["frac"], "traffic": main_k.get("traffic"),
-                "traffic_source": pmc_note + ("; rocprofv3 FETCH_SIZE/WRITE_SIZE passes, tools/pmc_round.sh"
+                "traffic_source": pmc_note + ("; rocprofv3 --pmc passes, tools/pmc_round.sh"
                                               if main_k.get("traffic") else ""),
-                "kernel": ROOF_KERNEL,
+                "kernel": main_k["kernel"], "why": "the probed kernel with the most device time per batch",
+                "ms_per_batch": main_k["ms_per_batch"], "share_of_step": main_k["share_of_step"],
                 "launches": main_k["launches"], "avg_launch_us": main_k["avg_launch_us"],
                 "alg_bytes_per_launch": main_k["alg_bytes_per_launch"],
                 "alg_bytes_per_unit": main_k["alg_bytes_per_unit"],
-                "dominant": ({k: kern[0].get(k) for k in ("kernel", "ms_per_batch", "share_of_step", "achieved", "frac",
-                                                          "traffic", "traffic_over_alg")} if kern else None),
-                "top_kernels_by_time": kern[:3],
+                "secondary": [e for e in kern if e is not main_k],
                 "path_input_roofline_frac": round(frames_per_step * a.steps * N * 8 / world / elapsed / 1e9
                                                   / HBM_PEAK_GBS, 8)}
+        for k in ("traffic_over_alg", "traffic_bounds", "read_bytes_by_request_size", "traffic_read_pattern"):
+            if k in main_k:
+                roof[k] = main_k[k]
 
     # with host input: each batch's flow fields copied H2D from pinned host memory on the caller stream
     # before the call (two device buffers in turn), the PCIe-inclusive rate (never `value`)
     h2d = None
     if not a.no_h2d and not a.frames:
-        host = flows.cpu().pin_memory()
-        dbuf = [flows, torch.empty_like(flows)]
+        host = sets[0].cpu().pin_memory()
+        dbuf = [torch.empty_like(sets[0]), torch.empty_like(sets[0])]
         hs = max(3, a.steps // 2)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
@@ -440,6 +499,8 @@ def main(argv=None):
                "frames_per_sec": round(frames_per_step * a.steps / elapsed, 3),
                "parallelism": f"frame-parallel x{world}", "workspaces": ctx.batch_slots(),
                "workspace_mb_per_frame": round(ctx.workspace_bytes() / B / 1e6, 1),
+               "input_sets": 1 if a.frames else INPUT_SETS,
+               "dofs_env": {k: v for k, v in sorted(os.environ.items()) if k.startswith("DOFS_")},
                "snapshots_frame0": int(len(res.snapshots)),
                "candidates_frame0": int(res.stats["n_candidates"])}
         out = {
@@ -457,7 +518,8 @@ def main(argv=None):
             "scaling": "strong" if a.frames else "weak",
             "vs_baseline": None,
             "dtype": "f32+f64",
-            "data": "synthetic (on-device splitmix64 flow fields, SURVEY.md §8(d) spec)",
+            "data": ("synthetic (on-device splitmix64 flow fields, SURVEY.md §8(d) spec"
+                     + (")" if a.frames else f"; {INPUT_SETS} distinct resident batches used in turn by the steps)")),
             "config": cfg,
             "roofline": roof,
             "with_h2d": h2d,

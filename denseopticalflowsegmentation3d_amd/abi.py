@@ -139,8 +139,8 @@ class DofsBoxRecord(C.Structure, _NpMixin):
         ("slot", C.c_int32),
         ("cls", C.c_int32),
         ("size", C.c_int32),
-        ("score", C.c_float),
-        ("move", C.c_float),
+        ("score", C.c_double),
+        ("move", C.c_double),
         ("lower_face", (C.c_float * 2) * 4),
         ("upper_face", (C.c_float * 2) * 4),
     ]

@@ -54,11 +54,14 @@ enum FlowCtlIdx {
     FC_NS = FC_NL + 2,
     FC_QCAP = FC_NL + 3,            // queue slots: B * N (w.bw); tickets and pushes stay below it
     FC_NLPOOL = FC_NL + 4,          // initial long pool: B root-path entries, then the frames' other long paths
-    FC_HDR = 8 * kFlowLine,         // then pl[B + 1], pt[B + 1], ps[B + 1]
+    FC_FS = 8 * kFlowLine,          // the launch anatomy: FS_N u64 counters, one 256-byte line each (FlowStat)
+    FC_HDR = FC_FS + 24 * 64,       // then pl[B + 1], pt[B + 1], ps[B + 1]
 };
 constexpr int kFlowSpin = 1 << 22;  // polls of a queue slot before giving up (s_sleep between)
 
-// launch anatomy (a few atomics per task, not per step): read by dofs_debug_flow_stats (tools/flow_stats.py)
+// launch anatomy (a few atomics per task, not per step): per launch, in the context's control block
+// (FC_FS; so two contexts on one device never mix their counts), read by dofs_debug_flow_stats
+// (tools/flow_stats.py) after the launch
 constexpr int kFsStride = 32;  // u64 per stat: one 256-byte line each
 enum FlowStat {
     FS_T0 = 0,         // first wave start (100 MHz wall clock, min)
@@ -88,11 +91,14 @@ enum FlowStat {
     FS_KFAST = 21,     // long-path chunks run with a constant key (no step reaches the carried rank)
     FS_N = 24
 };
-__device__ unsigned long long g_fs[FS_N * kFsStride];
+static_assert(FS_N * kFsStride * 2 == FC_HDR - FC_FS, "FlowStat block size");
+__device__ inline unsigned long long* fs_at(int* ctl, int i) {
+    return reinterpret_cast<unsigned long long*>(ctl + FC_FS) + i * kFsStride;
+}
 __device__ inline unsigned long long fs_now() { return __builtin_amdgcn_s_memrealtime(); }
-__device__ inline void fs_add(int i, unsigned long long v) { atomicAdd(&g_fs[i * kFsStride], v); }
-__device__ inline void fs_min(int i, unsigned long long v) { atomicMin(&g_fs[i * kFsStride], v); }
-__device__ inline void fs_max(int i, unsigned long long v) { atomicMax(&g_fs[i * kFsStride], v); }
+__device__ inline void fs_add(int* ctl, int i, unsigned long long v) { atomicAdd(fs_at(ctl, i), v); }
+__device__ inline void fs_min(int* ctl, int i, unsigned long long v) { atomicMin(fs_at(ctl, i), v); }
+__device__ inline void fs_max(int* ctl, int i, unsigned long long v) { atomicMax(fs_at(ctl, i), v); }
 
 __device__ inline int f_ld(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ inline void f_st(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -218,7 +224,7 @@ __global__ void k_flow_prep(Ws w, int* ctl) {
     pt[B] = st;
     ps[B] = ss;
     for (int k = 0; k < FC_HDR; ++k) ctl[k] = 0;
-    for (int k = 0; k < FS_N; ++k) g_fs[k * kFsStride] = (k == FS_T0) ? ~0ull : 0ull;
+    *fs_at(ctl, FS_T0) = ~0ull;
     int nl = 0;
     for (int f = 0; f < B; ++f) nl += w.C(f)[C_LONG];
     ctl[FC_NL] = nl;
@@ -316,16 +322,16 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
     auto tally = [&]() {
         if (lane == 0) {
 #ifdef DOFS_FLOW_PROF
-            fs_add(FS_P_STEPS, p_steps);
-            fs_add(FS_P_TAIL, p_tail);
-            fs_add(FS_P_NEXT, p_next);
+            fs_add(ctl, FS_P_STEPS, p_steps);
+            fs_add(ctl, FS_P_TAIL, p_tail);
+            fs_add(ctl, FS_P_NEXT, p_next);
 #endif
-            fs_add(FS_LCHUNKS, chunks);
-            fs_add(FS_LSTEPS, steps);
-            fs_add(FS_KFAST, kfast);
+            fs_add(ctl, FS_LCHUNKS, chunks);
+            fs_add(ctl, FS_LSTEPS, steps);
+            fs_add(ctl, FS_KFAST, kfast);
             if (top == 0) {
-                fs_add(FS_RCHUNKS, chunks);
-                fs_add(FS_RSTEPS, steps);
+                fs_add(ctl, FS_RCHUNKS, chunks);
+                fs_add(ctl, FS_RSTEPS, steps);
             }
         }
     };
@@ -475,9 +481,9 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
                 f_st(curp, -1);
                 old = __hip_atomic_exchange(w.ready + lb + top, kFlowDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (t & kFlowLong) atomicAdd(ctl + FC_LDONE, 1);
-                fs_add(FS_LDONE, 1);
-                fs_max(FS_T_LONG, fs_now());
-                if (top == 0) fs_max(FS_T_ROOT, fs_now());
+                fs_add(ctl, FS_LDONE, 1);
+                fs_max(ctl, FS_T_LONG, fs_now());
+                if (top == 0) fs_max(ctl, FS_T_ROOT, fs_now());
             }
             old = __shfl(old, 0, 64);
             tally();
@@ -503,8 +509,8 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             parked = __shfl(parked, 0, 64);
             if (parked) {
                 if (lane == 0) {
-                    fs_add(FS_LPARKS, 1);
-                    if (top == 0) fs_add(FS_RPARKS, 1);
+                    fs_add(ctl, FS_LPARKS, 1);
+                    if (top == 0) fs_add(ctl, FS_RPARKS, 1);
                 }
                 tally();
                 return -1;
@@ -628,7 +634,7 @@ __device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch
             if (old < kFlowDone) {
                 if (old & kFlowLong) {
                     flow_push(w, ctl, epoch, old);
-                    fs_add(FS_PUSH, 1);
+                    fs_add(ctl, FS_PUSH, 1);
                 } else {
                     t = old;
                     fresh = true;
@@ -721,7 +727,7 @@ __global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigne
     const int wv = kLong ? (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
     const int nl = ctl[FC_NL];
     int cb = 0, ce = 0;  // this wave's claimed, not yet started initial short tasks
-    if (lane == 0) fs_min(FS_T0, fs_now());
+    if (lane == 0) fs_min(ctl, FS_T0, fs_now());
     if constexpr (kLong) {
         __builtin_amdgcn_s_setprio(3);  // the chains go first in their SIMD's arbitration
         for (int it = 0; it < (1 << 26); ++it) {
@@ -729,27 +735,27 @@ __global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigne
             if (t < 0) break;
             const unsigned long long t1 = fs_now();
             while (t >= 0) {
-                if (lane == 0) fs_add(FS_LRUNS, 1);
+                if (lane == 0) fs_add(ctl, FS_LRUNS, 1);
                 const int nx = flow_long(w, ctl, t, buf[wv], ob[wv], keyfast);
                 if (nx >= 0 && !(nx & kFlowLong)) {  // a short waiter: a one-lane short round (and its waiters)
-                    if (lane == 0) fs_add(FS_INJECT, 1);
+                    if (lane == 0) fs_add(ctl, FS_INJECT, 1);
                     flow_short(w, ctl, epoch, nx, false, &cb, &ce);
                     break;
                 }
                 t = nx;
             }
-            if (lane == 0) fs_add(FS_LTICKS, fs_now() - t1);
+            if (lane == 0) fs_add(ctl, FS_LTICKS, fs_now() - t1);
         }
     } else {
         const unsigned long long t1 = fs_now();
         flow_short(w, ctl, epoch, -1, true, &cb, &ce);
         if (lane == 0) {
-            fs_add(FS_SROUNDS, 1);
-            fs_add(FS_STICKS, fs_now() - t1);
-            fs_max(FS_T_SHORT, fs_now());
+            fs_add(ctl, FS_SROUNDS, 1);
+            fs_add(ctl, FS_STICKS, fs_now() - t1);
+            fs_max(ctl, FS_T_SHORT, fs_now());
         }
     }
-    if (lane == 0) fs_max(FS_T_EXIT, fs_now());
+    if (lane == 0) fs_max(ctl, FS_T_EXIT, fs_now());
 }
 constexpr int kFlowShortW = 8;  // waves per short-worker workgroup
 constexpr int kFlowLongW = 4;    // waves per long-worker workgroup (one per SIMD)

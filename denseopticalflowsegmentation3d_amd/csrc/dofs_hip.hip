@@ -1716,8 +1716,13 @@ __global__ __launch_bounds__(256) void k_boruvka_recs(Ws w, int r, RecBufs rb) {
 // lane per distinct root issues the two global atomics.
 // ---------------------------------------------------------------------------------------------
 constexpr int kAggT = 1024, kAggHT = 2048;
+// test knob (dofs_debug_dnc_skew): the odd waves of every workgroup sleep about `skew` x 64 cycles before
+// they read their slot's maximum, so the even waves reach the slot-table clear first — without the
+// barrier between the read and the clear, that order loses L-roots in every iteration (the round-3 race)
+__device__ int g_dnc_skew = 0;
 __global__ __launch_bounds__(kAggT) void k_dnc_compress(Ws w, int64_t S, int ep) {
     __shared__ int hk[kAggHT], hcs[kAggHT], hmx[kAggHT];
+    const int skew = g_dnc_skew;
     const Dims& d = w.d;
     const int f = blockIdx.y;
     const int64_t lb = f * d.NL;
@@ -1750,6 +1755,8 @@ __global__ __launch_bounds__(kAggT) void k_dnc_compress(Ws w, int64_t S, int ep)
             atomicMax(hmx + slot, mtag | (int)i);
         }
         __syncthreads();
+        if (skew && ((threadIdx.x >> 6) & 1))
+            for (int z = 0; z < skew; ++z) __builtin_amdgcn_s_sleep(1);
         // only the workgroup's max rank of a component can be the component's max (its L-root):
         // own = the root for those candidates, -1 for the others (KDncLRootRelabel skips them)
         if (act) w.own[f * d.M + i] = hmx[slot] == (mtag | (int)i) ? r : -1;
@@ -3377,14 +3384,6 @@ extern "C" int dofs_debug_krt_timing(double* out_us, int n) {
 }
 #endif
 
-// Measurement: the last dataflow replay launch's anatomy (dofs_dataflow.h FlowStat), after a sync.
-extern "C" int dofs_debug_flow_stats(unsigned long long* out, int n) {
-    unsigned long long v[dofs::FS_N * dofs::kFsStride] = {0};
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(dofs::g_fs), sizeof(v)) != hipSuccess) return -1;
-    for (int i = 0; i < n && i < dofs::FS_N; ++i) out[i] = v[i * dofs::kFsStride];
-    return dofs::FS_N;
-}
 
 // Test knob: the low key bits the batch MST sort leaves to the fix-up (dofs_sortfix.h), 0 .. 48
 // (0: the full 64-bit sort; 48: 16-bit keys, every weight class a mixed group: the fallback's test).
@@ -3397,6 +3396,30 @@ extern "C" int dofs_debug_sort_cut(int cut) {
 // Diagnosis only: fix-up on / off (the truncated order is not Kruskal's: results differ), and a copy of
 // the next packed batch's sorted (key, value) pairs — at most cap — into device buffers.
 extern "C" void dofs_debug_sort_fix(int on) { dofs::g_sort_fix = on != 0; }
+// Test knob: k_dnc_compress's wave skew (0 = off), see g_dnc_skew. Returns 0 or a HIP error code.
+extern "C" int dofs_debug_dnc_skew(int skew) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(dofs::g_dnc_skew), &skew, sizeof(int));
+}
+// Test entry: the fix-up (k_sortfix_local, then k_sortfix_merge when its flag is up) over a caller's n
+// device pairs already sorted stably by key bits [cut, 64) — keys u64, values u32 (distinct) — in place,
+// with d_k2 / d_v2 (n each) as the fallback's scratch and d_ctr (3 zeroed int32) receiving the counters
+// (moved pairs, fallback flag, barrier). Synchronous on the null stream; returns 0 or a HIP error code.
+extern "C" int dofs_debug_sortfix_run(void* d_keys, void* d_vals, void* d_k2, void* d_v2, int64_t n, int cut,
+                                      int* d_ctr) {
+    using namespace dofs;
+    if (n <= 0 || cut < 1 || cut > 48 || !d_keys || !d_vals || !d_k2 || !d_v2 || !d_ctr) return (int)hipErrorInvalidValue;
+    SortFix s{(unsigned long long*)d_keys, (unsigned*)d_vals, (unsigned long long*)d_k2, (unsigned*)d_v2, d_ctr, n, cut};
+    int lgs = 0;
+    while (((int64_t)1 << lgs) < n) ++lgs;
+    lgs += lgs & 1;
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    const unsigned gx = (unsigned)std::min<int64_t>((n + kFixBlock - 1) / kFixBlock, 8192);
+    hipLaunchKernelGGL(k_sortfix_local, dim3(gx), dim3(kFixBlock), 0, nullptr, s);
+    hipLaunchKernelGGL(k_sortfix_merge, dim3(2 * cus), dim3(kFixBlock), 0, nullptr, s, lgs);
+    const hipError_t e = hipDeviceSynchronize();
+    return e == hipSuccess ? (int)hipGetLastError() : (int)e;
+}
 extern "C" void dofs_debug_sort_dump(void* d_keys, void* d_vals, int64_t cap) {
     dofs::g_sort_dump[0] = d_keys;
     dofs::g_sort_dump[1] = d_vals;
@@ -3421,6 +3444,18 @@ extern "C" int dofs_debug_ws_ptrs(dofs_ctx* ctx, unsigned long long* out, long l
     dims[1] = w.d.N;
     dims[2] = w.d.NL;
     return DOFS_OK;
+}
+
+// Measurement: the context's last dataflow replay launch's anatomy (dofs_dataflow.h FlowStat, kept in the
+// context's control block), after draining the context. Returns FS_N or a negative error.
+extern "C" int dofs_debug_flow_stats(dofs_ctx* ctx, unsigned long long* out, int n) {
+    if (!ctx || !out || !ctx->be.flow_ctl) return -1;
+    ctx->drain();
+    unsigned long long v[dofs::FS_N * dofs::kFsStride] = {0};
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpy(v, ctx->be.flow_ctl + dofs::FC_FS, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    for (int i = 0; i < n && i < dofs::FS_N; ++i) out[i] = v[i * dofs::kFsStride];
+    return dofs::FS_N;
 }
 
 // ---- optical flow (upstream stage; HIP build only) ---------------------------------------------

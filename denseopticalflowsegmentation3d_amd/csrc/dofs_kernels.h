@@ -1440,8 +1440,8 @@ struct KSnapshot {
         rec.slot = (int)s;
         rec.cls = sn.sol.cls;
         rec.size = v.size;
-        rec.score = (float)sn.score;
-        rec.move = (float)sn.move;
+        rec.score = sn.score;
+        rec.move = sn.move;
         for (int t = 0; t < 4; ++t) {
             rec.lower_face[t][0] = sn.sol.lower_face[t][0];
             rec.lower_face[t][1] = sn.sol.lower_face[t][1];

@@ -62,8 +62,12 @@ struct Pipeline {
     // most kDncFrames frames on a backend that selects it), 0 sweep, 1 DNC (DOFS_KRT_DNC=0 / 1)
     int krt_mode = -1;
     static constexpr int kDncFrames = 8;
+    // Auto mode never forces a re-layout: a small (tail) batch on a workspace laid out for a large batch
+    // without the DNC's arrays runs the sweep instead (a re-layout would free and re-allocate the
+    // multi-GB workspace twice: down to the small shape, then up again for the next full batch).
     bool use_dnc(const Dims& d) const {
-        return krt_mode >= 0 ? krt_mode == 1 : (Backend::kDncAuto && d.B <= kDncFrames);
+        if (krt_mode >= 0) return krt_mode == 1;
+        return Backend::kDncAuto && d.B <= kDncFrames && (layout_words || !base || cap.B <= kDncFrames);
     }
     int skip_mask = 0;          // measurement only (DOFS_SKIPMASK): 1 short replay, 2 long replay, 4 lift
     void* ev_input = nullptr;   // run_a records it once the input flow has been read (the caller's release)

@@ -139,10 +139,11 @@ __global__ __launch_bounds__(kFixBlock) void k_sortfix_local(SortFix s) {
         if (!valid || fast || (!left_open && !right_open && !(mix & gmask))) continue;  // done, or exact ties
         if (!same_prev) {
             moved += fix_group_scalar(s, p, b);  // the group's first position: the scalar path
-        } else if (a != b) {  // a mixed pair of a scalar-path group: it must start within kFixScan
-            int64_t q = p - 1;
-            while (q >= 1 && p - q < kFixScan && (s.key[q - 1] >> s.cut) == T) --q;
-            if (q >= 1 && (s.key[q - 1] >> s.cut) == T) dofs_st(s.ctr + 1, 1);
+        } else if (a != b) {
+            // a mixed pair (p - 1, p) of a scalar-path group: its sorter covers [start, start + kFixScan),
+            // so the pair is sorted only if p - start < kFixScan. Groups are contiguous runs, so
+            // p - start >= kFixScan exactly when position p - kFixScan is still in the group: the fallback.
+            if (p >= kFixScan && (s.key[p - kFixScan] >> s.cut) == T) dofs_st(s.ctr + 1, 1);
         }
     }
     const int tot = wave_reduce(moved, [](int x, int y) { return x + y; });

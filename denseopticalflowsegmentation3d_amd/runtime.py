@@ -145,7 +145,7 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_overlay_batch_device.restype = C.c_int32
     L.dofs_overlay.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(C.c_uint8)]
     L.dofs_overlay.restype = C.c_int32
-    if L.dofs_abi_version() != 1:
+    if L.dofs_abi_version() != 2:
         raise RuntimeError("dofs ABI version mismatch")
     _LIBS[path] = L
     return L

@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define DOFS_ABI_VERSION 1
+#define DOFS_ABI_VERSION 2
 
 typedef enum dofs_status {
     DOFS_OK = 0,
@@ -151,14 +151,17 @@ typedef struct dofs_event {
     float mean[2];            /* Node::flow_value of the root */
 } dofs_event;
 
-/* Fixed-size 3D-box record for the frame-parallel gather (one per snapshot). */
+/* Fixed-size 3D-box record for the frame-parallel gather (one per snapshot, 96 bytes). score and move
+ * keep the reference's double (SegmentData::score, graph.hpp:30-31; the move norm, graph.cpp:349-354);
+ * the faces are Solution's float corners (lifting_3d.hpp, get_bottom_variants lifting_3d.cpp:412-438).
+ * ABI version 2: version 1 narrowed score and move to float (88 bytes). */
 typedef struct dofs_box_record {
     int32_t frame;
     int32_t slot;
     int32_t cls;
     int32_t size;
-    float score;
-    float move;
+    double score;
+    double move;
     float lower_face[4][2];
     float upper_face[4][2];
 } dofs_box_record;

@@ -64,3 +64,32 @@ def check_solution_close(a, b):
         assert np.all(np.abs(x - y) <= 1e-3 + 1e-5 * np.abs(x)), (k, x, y)
     for k in ("w_error", "h_error", "orient"):
         assert abs(float(a[k]) - float(b[k])) <= 1e-6, (k, a[k], b[k])
+
+
+def check_records(recs, snaps, frame=None, exact=False):
+    """Gathered box records (dofs_box_record, one per snapshot in slot order) against the oracle's
+    snapshots of the same frame (SegmentData, graph.cpp:348-356): slot, size, class exact; move exact
+    (a double norm of the replayed float mean, no transcendental); score (double) and the 3D box's
+    lower/upper face corners (get_bottom_variants, lifting_3d.cpp:412-438) bit-exact when `exact`
+    (host emulator, same libm), else within the stated tolerance of check_solution_close / check_exact
+    (GPU double atan2/sin/cos). `recs` may hold fewer records than snaps (truncated block)."""
+    k = min(len(snaps), len(recs))
+    r, s = recs[:k], snaps[:k]
+    assert np.array_equal(r["slot"], s["slot"]), "record slot"
+    assert np.array_equal(r["size"], s["size"]), "record size"
+    assert np.array_equal(r["cls"], s["sol"]["cls"]), "record cls"
+    if frame is not None:
+        assert np.array_equal(r["frame"], np.full(k, frame, np.int32)), "record frame"
+    assert _b(r["move"]) == _b(s["move"]), "record move"
+    for face in ("lower_face", "upper_face"):
+        x = np.asarray(s["sol"][face], np.float64)
+        y = np.asarray(r[face], np.float64)
+        if exact:
+            assert _b(np.asarray(r[face], np.float32)) == _b(np.asarray(s["sol"][face], np.float32)), face
+        else:
+            assert np.all(np.abs(x - y) <= 1e-3 + 1e-5 * np.abs(x)), (face, x, y)
+    if exact:
+        assert _b(r["score"]) == _b(s["score"]), "record score"
+    else:
+        assert np.all(np.abs(r["score"] - s["score"]) <= 1e-6), ("record score", r["score"], s["score"])
+    return k

@@ -34,20 +34,20 @@ def test_rccl_library_exports_every_declared_symbol():
     assert "dofs_gather_records" in names and "dofs_comm_init" in names
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.dofs_records_block_bytes(96, 64) == 4 * 96 + 88 * 96 * 64
+    assert lib.dofs_records_block_bytes(96, 64) == 4 * 96 + 96 * 96 * 64
 
 
 def test_abi_version_and_struct_layouts():
     from denseopticalflowsegmentation3d_amd import abi, runtime
     lib = runtime.load()
-    assert lib.dofs_abi_version() == 1
+    assert lib.dofs_abi_version() == 2
     p = abi.DofsParams()
     lib.dofs_default_params(ctypes.byref(p))
     ref = abi.default_params()
     assert bytes(p) == bytes(ref)
     # sizes fixed by the header (natural alignment, x86-64 and gfx950 alike)
     assert ctypes.sizeof(abi.DofsSolution) == 160 and ctypes.sizeof(abi.DofsSnapshot) == 208
-    assert ctypes.sizeof(abi.DofsEvent) == 56 and ctypes.sizeof(abi.DofsBoxRecord) == 88
+    assert ctypes.sizeof(abi.DofsEvent) == 56 and ctypes.sizeof(abi.DofsBoxRecord) == 96
     assert ctypes.sizeof(abi.DofsEdge) == 16
 
 

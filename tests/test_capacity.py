@@ -29,7 +29,7 @@ def _check(ctx, calib, dev_alloc, dev_ptr, to_host):
     ctx.set_snapshot_capacity(CAP)
     try:
         bid = _run(ctx, flows, calib, prm, dev_ptr)
-        blk = dev_alloc(np.zeros(4 * B + B * 4 * 88, np.uint8))
+        blk = dev_alloc(np.zeros(4 * B + B * 4 * RECORD_DTYPE.itemsize, np.uint8))
         # more records per frame than the workspace keeps: refused whatever the data (all ranks alike)
         with pytest.raises(RuntimeError, match=r"\(4\)"):
             ctx.records_copy(dev_ptr(blk), 4, stream=0, batch=bid)
@@ -38,7 +38,7 @@ def _check(ctx, calib, dev_alloc, dev_ptr, to_host):
         h = to_host(blk)
         counts = h[:4 * B].view(np.int32)
         assert list(counts) == [len(o.snapshots) for o in oracle]
-        recs = h[4 * B:4 * B + B * CAP * 88].view(RECORD_DTYPE).reshape(B, CAP)
+        recs = h[4 * B:4 * B + B * CAP * RECORD_DTYPE.itemsize].view(RECORD_DTYPE).reshape(B, CAP)
         for f in range(B):
             assert list(recs[f]["slot"]) == list(oracle[f].snapshots["slot"][:CAP])
             assert list(recs[f]["size"]) == list(oracle[f].snapshots["size"][:CAP])

@@ -91,8 +91,7 @@ def _emu_worker(rank, world, port, q, per=16, cap=0):
             n = records_nbytes(EB, per)
             counts = [int(c) for r in range(world) for c in g[r * n:r * n + 4 * EB].view(np.int32)]
             frames = decode_gathered(g, world, EB, per)
-            q.put(([(f["frame"].tolist(), f["slot"].tolist(), f["size"].tolist(), f["cls"].tolist(),
-                     f["score"].tolist()) for f in frames], counts))
+            q.put(([f.tobytes() for f in frames], counts))
         ctx.close()
     finally:
         dist.destroy_process_group()
@@ -119,28 +118,29 @@ def _run_emu_world2(per, cap):
 
 def _check_emu(got, calib, per):
     from oracle import binding as ob
-    from parity import params
+    from parity import check_records, params
     persp, inv, up = calib
     frames, counts = got
     assert len(frames) == 2 * EB
     nsnap, truncated = 0, 0
-    for gf, (frame, slot, size, cls, score) in enumerate(frames):
+    for gf, raw in enumerate(frames):
+        recs = np.frombuffer(raw, RECORD_DTYPE)
         o = ob.segment(ob.synth_flow(EH, EW, gf), persp, inv, up, params=params(EMIN, 8), mode=0)
         s = o.snapshots
         assert counts[gf] == len(s)  # the full count, also when the records were truncated
         truncated += len(s) > per
         s = s[:per]
-        nsnap += len(s)
-        assert slot == s["slot"].tolist() and size == s["size"].tolist() and cls == s["sol"]["cls"].tolist()
-        assert frame == [gf % EB] * len(s)  # frame index within the rank's batch
-        assert np.allclose(score, s["score"].astype(np.float32), rtol=0, atol=1e-6)
+        assert len(recs) == len(s)
+        # frame index within the rank's batch; every field of the record bit-exact (emulator: same libm)
+        nsnap += check_records(recs, s, gf % EB, exact=True)
     assert nsnap > 0
     return truncated
 
 
 def test_gather_real_pipeline_world2(calib):
     """Each gloo rank segments its frames through the product pipeline (host emulator, same kernel
-    bodies) and the gathered box records equal the oracle's snapshots of every frame, in frame order."""
+    bodies) and the gathered box records equal the oracle's snapshots of every frame, in frame order —
+    slot, size, class, move, score and the 3D box faces, bit for bit."""
     assert _check_emu(_run_emu_world2(EPER, 0), calib, EPER) == 0
 
 

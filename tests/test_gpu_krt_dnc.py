@@ -7,6 +7,11 @@ path counters and labels. Round 3 found a cross-wave race in `k_dnc_compress` th
 about one of six first batches of a fresh context; it is caught here by fresh contexts and distinct
 inputs per batch (a later batch on the same input would re-read the previous batch's sizes and hide
 it). Both modes are checked against the oracle at a small size as well.
+
+The race is also forced deterministically: with the wave-skew knob (dofs_debug_dnc_skew) the odd waves
+of every k_dnc_compress workgroup sleep before reading their slot's maximum, so the even waves reach the
+slot-table clear first in every iteration — exactly the interleaving that lost L-roots before the
+barrier between read and clear existed. The DNC KRT must still equal the sweep merge for merge.
 """
 import numpy as np
 import pytest
@@ -19,12 +24,16 @@ pytestmark = pytest.mark.gpu
 CTXS, BATCHES = 4, 3
 
 
-def _run(monkeypatch, mode, B, H, W, calib, seeds, prm=None):
+def _run(monkeypatch, mode, B, H, W, calib, seeds, prm=None, skew=0):
+    import ctypes as C
+
     import torch
     from denseopticalflowsegmentation3d_amd import runtime
     monkeypatch.setenv("DOFS_KRT_DNC", mode)
     persp, inv, up = calib
     ctx = runtime.Dofs(0)
+    ctx.lib.dofs_debug_dnc_skew.argtypes = [C.c_int]
+    assert ctx.lib.dofs_debug_dnc_skew(skew) == 0
     fl = torch.empty((B, H, W, 2), dtype=torch.float32, device="cuda")
     out = []
     try:
@@ -38,6 +47,7 @@ def _run(monkeypatch, mode, B, H, W, calib, seeds, prm=None):
             lab = ctx.fetch(B - 1, want_blur=False).labels.copy()
             out.append((c, ev, lab))
     finally:
+        ctx.lib.dofs_debug_dnc_skew(0)
         ctx.close()
     return out
 
@@ -71,3 +81,47 @@ def test_dnc_matches_oracle_small(monkeypatch, calib):
             assert np.asarray(ev[f][k]).tobytes() == np.asarray(o.events[k]).tobytes(), f"frame {f}: event field {k}"
         if f == B - 1:
             assert np.array_equal(lab, o.labels)
+
+
+def test_dnc_race_forced_by_wave_skew(monkeypatch, calib):
+    """The k_dnc_compress interleaving of the round-3 race, forced in every workgroup iteration."""
+    H, W, B = 540, 960, 4
+    seeds = [5000]
+    dnc = _run(monkeypatch, "1", B, H, W, calib, seeds, skew=64)
+    swp = _run(monkeypatch, "0", B, H, W, calib, seeds)
+    (c1, e1, l1), (c0, e0, l0) = dnc[0], swp[0]
+    assert int(c1[0, 58]) == 0 and int(c0[0, 58]) == 0
+    for f in range(B):
+        assert np.array_equal(e1[f], e0[f]), f"frame {f}: merge events differ under the wave skew"
+    assert np.array_equal(l1, l0)
+
+
+def test_tail_batch_keeps_large_workspace(calib):
+    """a small tail batch (<= 8 frames, the DNC KRT's auto range) on a workspace laid out for a
+    larger batch runs the sweep in place instead of re-laying the workspace out (no free + re-allocation
+    down and back up); its results equal the oracle's."""
+    import torch
+    from denseopticalflowsegmentation3d_amd import runtime
+    H, W = 180, 320
+    prm = params(300, 8)
+    persp, inv, up = calib
+    ctx = runtime.Dofs(0)
+    try:
+        fl = torch.empty((16, H, W, 2), dtype=torch.float32, device="cuda")
+        runtime.synth_flow_device(fl.data_ptr(), 16, H, W, 300)
+        sizes = []
+        for B in (16, 16, 16, 4, 4, 4, 16):  # every workspace sees the large shape, then a tail batch
+            ctx.segment_batch_device(fl.data_ptr(), B, H, W, persp, inv, up, params=prm)
+            torch.cuda.synchronize()
+            sizes.append(ctx.workspace_bytes())
+            if B == 4:
+                c = ctx.batch_counters(B)
+                assert int(c[0, 58]) == 0
+                for f in (0, 3):
+                    o = ob.segment(ob.synth_flow(H, W, 300 + f), persp, inv, up, params=prm, mode=0, events=True)
+                    ev = ctx.events(f)
+                    for k in EVENT_FIELDS:
+                        assert np.asarray(ev[k]).tobytes() == np.asarray(o.events[k]).tobytes(), (f, k)
+        assert len(set(sizes)) == 1, sizes  # no workspace was laid out again
+    finally:
+        ctx.close()

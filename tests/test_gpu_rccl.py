@@ -1,12 +1,13 @@
 """GPU: the C-ABI RCCL gather of box records (include/dofs_rccl.h, libdofs_rccl.so) on a one-rank
 communicator (ncclCommInitAll over device 0): the gathered block equals dofs_batch_records_copy's block
-byte for byte (ncclGather to root 0 and ncclAllGather), and decodes to the oracle's snapshots. Multi-rank
+byte for byte (ncclGather to root 0 and ncclAllGather), and decodes to the oracle's snapshots (3D box
+faces, move and score included). Multi-rank
 runs need one process per GPU; the exchange is the same collective with equal blocks per rank."""
 import numpy as np
 import pytest
 
 from oracle import binding as ob
-from parity import params
+from parity import check_records, params
 
 pytestmark = pytest.mark.gpu
 
@@ -45,4 +46,4 @@ def test_gather_records_one_rank(gpu, calib):
         o = ob.segment(ob.synth_flow(H, W, 7 + f), persp, inv, up, params=prm, mode=0)
         recs = per_frame[f]
         assert len(recs) == len(o.snapshots)
-        assert np.array_equal(recs["slot"], o.snapshots["slot"]) and np.array_equal(recs["size"], o.snapshots["size"])
+        check_records(recs, o.snapshots, f)  # slot/size/cls/move exact, score and 3D faces within tolerance

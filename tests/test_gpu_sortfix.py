@@ -58,3 +58,63 @@ def test_truncated_sort_matches_full(gpu, calib):
     assert seen[24][0] > 0 and seen[24][1] == 0  # mixed groups sorted by the local pass, no fallback
     assert seen[32][0] > seen[24][0]
     assert seen[48][1] == 1  # 16-bit keys: mixed groups longer than kFixScan, the fallback merge sort
+
+
+def _fixup(lib, keys, vals, cut):
+    """dofs_debug_sortfix_run over (keys, vals) given in truncated-key stable order; returns the pairs and
+    the counters (moved, fallback flag)."""
+    import torch
+    lib.dofs_debug_sortfix_run.argtypes = [C.c_void_p] * 4 + [C.c_int64, C.c_int, C.c_void_p]
+    lib.dofs_debug_sortfix_run.restype = C.c_int
+    n = len(keys)
+    dk = torch.from_numpy(keys.view(np.int64).copy()).cuda()
+    dv = torch.from_numpy(vals.view(np.int32).copy()).cuda()
+    k2, v2 = torch.empty_like(dk), torch.empty_like(dv)
+    ctr = torch.zeros(3, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    rc = lib.dofs_debug_sortfix_run(dk.data_ptr(), dv.data_ptr(), k2.data_ptr(), v2.data_ptr(), n, cut, ctr.data_ptr())
+    assert rc == 0, rc
+    return (dk.cpu().numpy().view(np.uint64), dv.cpu().numpy().view(np.uint32), ctr.cpu().numpy()[:2].tolist())
+
+
+def _truncated_stable(keys, vals, cut):
+    o = np.argsort(keys >> np.uint64(cut), kind="stable")
+    return keys[o], vals[o]
+
+
+@pytest.mark.parametrize("lead", [0, 1, 37, 64, 200])
+@pytest.mark.parametrize("ties", [255, 256, 257, 300])
+def test_sortfix_long_exact_tie_run_then_smaller_key(gpu, lead, ties):
+    """`ties` equal full keys, then one smaller key with the same truncated key. With ties >= 256
+    the only mixed pair lies past the scalar sorter's window [start, start + 256): the fallback must
+    catch it. `lead` pairs of a lower group shift the group's start inside the wave."""
+    cut = 24
+    K = np.uint64(0x3FF0_0000_1234_5678)
+    lo = np.arange(lead, dtype=np.uint64) + np.uint64(0x3FE0_0000_0000_0000)
+    keys = np.concatenate([lo, np.full(ties, K, np.uint64), np.array([K - np.uint64(1)], np.uint64)])
+    vals = np.arange(len(keys), dtype=np.uint32)
+    keys, vals = _truncated_stable(keys, vals, cut)
+    want = np.lexsort((vals, keys))
+    gk, gv, ctr = _fixup(gpu.lib, keys, vals, cut)
+    assert np.array_equal(gk, keys[want]) and np.array_equal(gv, vals[want]), (lead, ties, ctr)
+    assert ctr[1] == (1 if ties >= 256 else 0), ctr  # the local pass sorts a window of 256 positions
+
+
+def test_sortfix_random_groups(gpu):
+    """Random mixed groups of 1 .. 300 pairs (some longer than the window: the fallback) against numpy's
+    (key, value) order; exact-tie runs are left as they are (their values already ascend)."""
+    rng = np.random.default_rng(11)
+    cut = 24
+    parts = []
+    base = np.uint64(0x3FF0_0000_0000_0000)
+    for g in range(3000):
+        n = int(rng.choice([1, 2, 3, 7, 16, 17, 40, 64, 65, 255, 256, 257, 300], p=None))
+        t = base + (np.uint64(g) << np.uint64(cut))
+        parts.append(t + rng.integers(0, 4, n).astype(np.uint64))  # few distinct low bits: ties and mixes
+    keys = np.concatenate(parts)
+    # values ascend within each truncated group (the emission order the stable pair sort leaves)
+    vals = (np.arange(len(keys)) * 3 + 5).astype(np.uint32)
+    keys, vals = _truncated_stable(keys, vals, cut)
+    want = np.lexsort((vals, keys))
+    gk, gv, ctr = _fixup(gpu.lib, keys, vals, cut)
+    assert np.array_equal(gk, keys[want]) and np.array_equal(gv, vals[want]), ctr

@@ -60,7 +60,7 @@ def model(a):
                                                                m.data_ptr(), params=prm, stream=sh), a.steps))
     allowed = torch.cat(masks)
     add_cut_edges(allowed, bounds, prm.neighbor == 8)
-    rec = torch.empty(4 + 64 * 88, dtype=torch.uint8, device="cuda")
+    rec = torch.empty(4 + 64 * 96, dtype=torch.uint8, device="cuda")
 
     def masked():
         ctx.segment_masked_device(full.data_ptr(), H, W, allowed.data_ptr(), persp, inv, up, params=prm, stream=sh)
@@ -117,7 +117,7 @@ def main():
     runtime.synth_flow_device(full.data_ptr(), 1, H, W, seed0=0, stream=sh)
     r0, r1 = band_bounds(H, world, rank)
     band = full[0, r0:r1].contiguous()
-    rec = torch.empty(4 + 64 * 88, dtype=torch.uint8, device="cuda")
+    rec = torch.empty(4 + 64 * 96, dtype=torch.uint8, device="cuda")
     shard = IntraFrame(ctx, world, rank, prm)
 
     def step():

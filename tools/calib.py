@@ -1,6 +1,10 @@
 """FETCH_SIZE / WRITE_SIZE calibration on gfx950 (tools/fetch_calib.hip): counter bytes / known bytes.
 
-usage: python tools/calib.py FETCH_DIR WRITE_DIR > profiles/<round>/fetch_calib.json
+usage: python tools/calib.py FETCH_DIR WRITE_DIR [RDREQ_DIR] > profiles/<round>/fetch_calib.json
+
+RDREQ_DIR (optional): a pass of TCC_EA0_RDREQ_sum, TCC_EA0_RDREQ_32B_sum, TCC_EA0_RDREQ_64B_sum and
+TCC_EA0_RDREQ_128B_sum; the read bytes by request size, 32 R32 + 64 R64 + 128 R128, are compared with
+the known bytes as well ("sized_over_known"), the check that this measure needs no per-pattern factor.
 """
 import csv
 import glob
@@ -23,7 +27,10 @@ LABEL = {"rd<int>": "read 4 B/lane", "rd<unsigned long>": "read 8 B/lane",
          "scatter8": "random 8-B writes"}
 
 
-def per_kernel(d, counter):
+SIZED = {"TCC_EA0_RDREQ_32B_sum": 32, "TCC_EA0_RDREQ_64B_sum": 64, "TCC_EA0_RDREQ_128B_sum": 128}
+
+
+def per_kernel(d, counter, scale=1024):
     out = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
@@ -33,13 +40,19 @@ def per_kernel(d, counter):
             for k in KNOWN:
                 if name.startswith(("void " + k + "(", k + "(")):
                     out.setdefault(k, {}).setdefault(r["Dispatch_Id"], 0.0)
-                    out[k][r["Dispatch_Id"]] += float(r["Counter_Value"]) * 1024  # KB -> B
+                    out[k][r["Dispatch_Id"]] += float(r["Counter_Value"]) * scale  # KB -> B
     return {k: sum(v.values()) / len(v) for k, v in out.items()}
 
 
 def main():
     fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
     write = per_kernel(sys.argv[2], "WRITE_SIZE")
+    sized, reqs = {}, {}
+    if len(sys.argv) > 3:
+        for c, b in SIZED.items():
+            for k, v in per_kernel(sys.argv[3], c, scale=b).items():
+                sized[k] = sized.get(k, 0.0) + v
+        reqs = per_kernel(sys.argv[3], "TCC_EA0_RDREQ_sum", scale=1)
     res = {}
     for k, (rb, wb) in KNOWN.items():
         e = {"known_read_bytes": rb, "known_write_bytes": wb,
@@ -48,6 +61,10 @@ def main():
             e["fetch_over_known"] = round(fetch[k] / rb, 4)
         if wb and write.get(k) is not None:
             e["write_over_known"] = round(write[k] / wb, 4)
+        if rb and k in sized:
+            e["sized_read_bytes"] = sized[k]
+            e["sized_over_known"] = round(sized[k] / rb, 4)
+            e["read_requests"] = reqs.get(k)
         res[LABEL[k]] = e
     print(json.dumps(res, indent=1))
 

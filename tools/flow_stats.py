@@ -17,7 +17,7 @@ NB = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 H, W = int(os.environ.get("H", 1080)), int(os.environ.get("W", 1920))
 ctx = runtime.Dofs(0, lib=os.environ.get("DOFS_LIB") or None)  # DOFS_LIB: another build, for A/B
 L = ctx.lib
-L.dofs_debug_flow_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+L.dofs_debug_flow_stats.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
 persp, inv, up = runtime.calib()
 dev = torch.device("cuda", 0)
 flows = torch.empty((B, H, W, 2), dtype=torch.float32, device=dev)
@@ -29,7 +29,7 @@ for b in range(NB):
     ctx.segment_batch_device(flows.data_ptr(), B, H, W, persp, inv, up, stream=sh)
     torch.cuda.synchronize()
     out = (C.c_ulonglong * 24)()
-    L.dofs_debug_flow_stats(out, 24)
+    L.dofs_debug_flow_stats(ctx.ctx, out, 24)
     v = {n: int(out[i]) for i, n in enumerate(names)}
     t0 = v["t0"]
     res = {"ms_last_short_worker_done": (v["t_short_done"] - t0) / 1e5, "ms_last_long_done": (v["t_long_last"] - t0) / 1e5,

@@ -34,9 +34,9 @@ for b in range(NB):
         st = " " + " ".join(f"{k}={v:.1f}" for k, v in ms.items())
     c = ctx.batch_counters(B)
     import ctypes as C
-    ctx.lib.dofs_debug_flow_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    ctx.lib.dofs_debug_flow_stats.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
     fs = (C.c_ulonglong * 16)()
-    ctx.lib.dofs_debug_flow_stats(fs, 16)
+    ctx.lib.dofs_debug_flow_stats(ctx.ctx, fs, 16)
     flow = f" flowerr={int(c[0, 58])} short_done={(fs[1] - fs[0]) / 1e5:.1f} long_last={(fs[2] - fs[0]) / 1e5:.1f} exit={(fs[3] - fs[0]) / 1e5:.1f}"
     print(f"B={B} mode={os.environ.get('DOFS_KRT_DNC', 'auto')} batch {b}: {ts[-1]} ms{st}{flow}", flush=True)
 ctx.close()

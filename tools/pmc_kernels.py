@@ -13,7 +13,11 @@ coalesced reads of 4, 8 and 16 B per lane all count exactly half their bytes in 
 lines tallied at 64 B), so their HBM bytes are 2 x FETCH_SIZE; a random 4- or 16-B read counts 64 B
 (one request); WRITE_SIZE counts coalesced stores exactly and a random 8-B store as 32 B. So
 hbm_read_bytes = 2 x FETCH_SIZE for kernels whose reads are coalesced (pattern "stream"), and FETCH_SIZE
-(one 64-B request per access, a lower bound) for kernels dominated by random accesses ("random").
+(one 64-B request per access, a lower bound) for kernels dominated by random accesses ("random"), and
+both bounds for a "mixed" kernel (hbm_read_bounds = [FETCH_SIZE, 2 x FETCH_SIZE]; hbm_read_bytes = the
+upper one). A fifth pass, pmc_rdreq/ (TCC_EA0_RDREQ_{32B,64B,128B}_sum), counts the L2's memory-side read
+requests by size: read_bytes_by_request_size = 32 R32 + 64 R64 + 128 R128 needs no pattern factor
+(tools/calib.py checks it on the calibration kernels) and, when present, is the kernel's read bytes.
 """
 import csv
 import glob
@@ -30,7 +34,8 @@ PATTERN = {
     "KOrd": "stream",            # jump words by node; the ord[] scatter is random 4-B stores
     "k_krt_fused": "random",     # union-find records, label / seed stores
     "k_replay_long1": "stream",  # StepIn / RepVal records by preorder position (64-step chunks)
-    "k_replay_flow": "stream",   # StepIn / RepVal by preorder position (lanes: one path each; waves: 64-step chunks)
+    "k_replay_flow": "mixed",    # StepIn / RepVal by preorder position (waves: 64-step chunks, coalesced), short
+                                 # paths one per lane and light children's records gathered at random
     "KJump": "random",
     "KPathInit": "random",
     "KLift": "random",
@@ -79,7 +84,7 @@ def per_dispatch(rs, k):
 def main():
     out_dir, calib_path, kernels = sys.argv[1], sys.argv[2], sys.argv[3].split(",")
     calib = json.load(open(calib_path)) if os.path.exists(calib_path) else {}
-    passes = {p: rows(os.path.join(out_dir, p)) for p in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_tcc")}
+    passes = {p: rows(os.path.join(out_dir, p)) for p in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_tcc", "pmc_rdreq")}
     if not passes["pmc_fetch"]:  # tools/gpu_ab.sh layout: one directory per counter
         passes["pmc_fetch"] = rows(os.path.join(out_dir, "FETCH_SIZE"))
         passes["pmc_write"] = rows(os.path.join(out_dir, "WRITE_SIZE"))
@@ -94,10 +99,21 @@ def main():
             raw = f[0] * 1024  # KB -> B
             e["dispatches"] = f[1]
             e["fetch_size_raw_bytes"] = raw
-            e["hbm_read_bytes"] = 2 * raw if pat == "stream" else raw
+            e["hbm_read_bytes"] = 2 * raw if pat in ("stream", "mixed") else raw
+            if pat == "mixed":
+                e["hbm_read_bounds"] = [raw, 2 * raw]
+        rq = per_dispatch(passes["pmc_rdreq"], k)
+        if rq:
+            sized = sum(rq.get(c, (0.0, 0))[0] * b for c, b in
+                        (("TCC_EA0_RDREQ_32B_sum", 32), ("TCC_EA0_RDREQ_64B_sum", 64), ("TCC_EA0_RDREQ_128B_sum", 128)))
+            e["read_requests"] = {c: rq[c][0] for c in rq}
+            e["read_bytes_by_request_size"] = sized
+            if sized > 0:
+                e["hbm_read_bytes"] = sized
+                e["hbm_read_source"] = "TCC_EA0_RDREQ by request size"
         if w:
             e["write_size_raw_bytes"] = w[0] * 1024
-        if f and w:
+        if e.get("hbm_read_bytes") is not None and w:
             e["hbm_bytes_per_launch"] = e["hbm_read_bytes"] + e["write_size_raw_bytes"]
         e["calibration"] = {k2: v.get("fetch_over_known", v.get("write_over_known")) for k2, v in calib.items()}
         sq = per_dispatch(passes["pmc_sq"], k)
