@@ -18,7 +18,7 @@ if [ -z "${SKIP_BENCH:-}" ]; then
 step bench 600 python bench.py ${BENCH_ARGS:-}
 fi
 if [ -n "${ANATOMY:-}" ]; then
-DOFS_SERIAL=1 step flow1080 300 python tools/flow_stats.py 112 2
-DOFS_SERIAL=1 H=2160 W=3840 step flow4k 300 python tools/flow_stats.py 1 3
+step flow1080 300 env DOFS_SERIAL=1 python tools/flow_stats.py 112 2
+step flow4k 300 env DOFS_SERIAL=1 H=2160 W=3840 python tools/flow_stats.py 1 3
 fi
 exit 0
