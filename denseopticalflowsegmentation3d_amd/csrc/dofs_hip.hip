@@ -1141,10 +1141,16 @@ __device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, in
         if (h >= x0 && h < x0 + cnt) {
             sh.lw[h - x0] = jump_pack(t, 1);
             sh.lit[h - x0] = 0;
-        }  // (a child outside the block: k_pre_sweep pushes its position and flag)
+        } else if (w.jscatter && h >= d.N) {  // a merge child outside the block: its word and flag here
+            w.J[lb + h] = jump_pack((int)(x0 + t), 1);
+            w.lite[lb + h] = 0;
+        }  // (else k_pre_sweep pushes its position and flag)
         if (l >= x0 && l < x0 + cnt) {
             sh.lw[l - x0] = jump_pack(t, offl);
             sh.lit[l - x0] = 1;
+        } else if (w.jscatter && l >= d.N) {
+            w.J[lb + l] = jump_pack((int)(x0 + t), offl);
+            w.lite[lb + l] = 1;
         }
     }
     __syncthreads();
@@ -1175,13 +1181,20 @@ __device__ void deep_parent(const Ws& w, ParentShared& sh, int f, int64_t s0, in
         }
         if (!__syncthreads_or(moved)) break;
     }
+    const int64_t root = d.N + d.M - 1;
     for (int t = tid; t < cnt; t += kDeepT) {
         const unsigned long long v = sh.lw[t];
         const int p = jump_anc(v);
-        // a block top (parent outside the block) is marked -2: k_pre_sweep reads its pushed position
-        w.J[lb + x0 + t] = p >= 0 ? jump_pack((int)(x0 + p), jump_sum(v)) : jump_pack(-2, 0);
         const unsigned char c = sh.lit[t];
         if (c != 0xFF) w.lite[lb + x0 + t] = c;
+        if (p >= 0) {
+            w.J[lb + x0 + t] = jump_pack((int)(x0 + p), jump_sum(v));
+        } else if (!w.jscatter) {  // a block top (parent outside the block) is marked -2: k_pre_sweep
+            w.J[lb + x0 + t] = jump_pack(-2, 0);  // reads its pushed position
+        } else if (x0 + t == root) {  // jumping: the root is converged at position 0 and a path top; the
+            w.J[lb + x0 + t] = jump_pack(-1, 0);  // other tops' words come from their parents' blocks
+            w.lite[lb + x0 + t] = 1;
+        }
     }
 }
 static_assert(kDeepTop % kDeepT == 0, "parent epilogue shape");
@@ -2604,6 +2617,42 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w) {
     }
 }
 
+// K4 for small batches (Ws::jscatter): chip-wide pointer jumping instead of the per-frame sweep. After the
+// LDS KRT's epilogue a merge's word points to its block-top ancestor inside the block (offset sum), and a
+// block top's word to its parent outside the block (heavy +1, light +2 size(heavy)); the root's is (-1, 0).
+// Only the tops jump (the in-block words are final snapshots of the (top, sum) relation, so a top may hop
+// over any of them): a chain alternates in-block and outside words, at most 2 per block, and two hops per
+// launch on the freshest words at least triple every distance (KJump's invariant, dofs_kernels.h).
+struct KJumpTop {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t k) const {
+        const Dims& d = w.d;
+        const int64_t lb = f * d.NL, x = d.N + k;
+        unsigned long long v = dofs_ld64(w.J + lb + x);
+        int a = jump_anc(v);
+        if (a < 0 || (a - d.N) / kDeepTop == k / kDeepTop) return;  // converged, or not a block top
+        for (int h = 0; h < 2 && a >= 0; ++h) {
+            const unsigned long long u = dofs_ld64(w.J + lb + a);
+            v = jump_pack(jump_anc(u), jump_sum(v) + jump_sum(u));
+            a = jump_anc(v);
+        }
+        dofs_st64(w.J + lb + x, v);
+    }
+};
+// then every merge's position: a top's converged sum, or its in-block sum plus its top's
+struct KOrdMerge {
+    Ws w;
+    DOFS_HD void operator()(int f, int64_t k) const {
+        const Dims& d = w.d;
+        const int64_t lb = f * d.NL, x = d.N + k;
+        const unsigned long long v = w.J[lb + x];
+        const int a = jump_anc(v);
+        const int q = jump_sum(v) + (a >= 0 ? jump_sum(w.J[lb + a]) : 0);
+        w.pre[lb + x] = q;
+        w.ord[lb + q] = (int)x;
+    }
+};
+
 // the leaves' ord[] entries from their parents' positions (after k_pre_sweep): one lane per merge
 struct KLeafPos {
     Ws w;
@@ -3020,11 +3069,27 @@ struct HipBackend {
     // K4 merge positions by the top-down sweep (k_pre_sweep) instead of KJump (which the emulator
     // keeps): it also writes the block tops' path-top flags, which the LDS KRT's epilogue leaves out
     bool pre_sweep(const Ws& w) {
-        timed("k_pre_sweep", [&] { hipLaunchKernelGGL(k_pre_sweep, dim3((unsigned)w.d.B), dim3(kPreT), 0, stream, w); });
-        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_pre_sweep launch");
+        if (w.jscatter) {  // small batches: chip-wide jumping over the block tops (KJumpTop, KOrdMerge)
+            int launches = 0;
+            const int64_t chain = std::min<int64_t>(w.d.M, jump_chain_bound(w.d.M));
+            for (int64_t span = 1; span < chain; span *= 3) ++launches;
+            for (int t = 0; t < launches; ++t) launch(w.d.B, w.d.M, KJumpTop{w});
+            launch(w.d.B, w.d.M, KOrdMerge{w});
+        } else {
+            timed("k_pre_sweep", [&] { hipLaunchKernelGGL(k_pre_sweep, dim3((unsigned)w.d.B), dim3(kPreT), 0, stream, w); });
+            if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_pre_sweep launch");
+        }
         launch(w.d.B, w.d.M, KLeafPos{w});
         return true;
     }
+    // K4 by jumping (Ws::jscatter) for batches of at most `pre_jump_frames` frames (DOFS_PRE_JUMP = the
+    // frame bound; 0 = always the sweep): the sweep is one workgroup per frame, so a lone 4K frame walks its
+    // ~2,000 KRT blocks on one CU while the rest of the chip idles
+    static int pre_jump_frames() {  // read per batch (tests switch it within one process)
+        const char* e = getenv("DOFS_PRE_JUMP");
+        return e ? atoi(e) : 8;
+    }
+    static bool pre_jump(const Dims& d) { return d.B <= pre_jump_frames(); }
     void boruvka_relabel(const Ws& w, int r) {
         if (r >= 1 && rec_path(w) && relabel_tiles()) {  // round 0 runs before the tile flags exist
             rec_launch(w, r, k_boruvka_relabel_t, "k_boruvka_relabelt");

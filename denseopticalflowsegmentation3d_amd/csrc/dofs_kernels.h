@@ -128,6 +128,8 @@ struct Ws {
     double score_threshold;
     double overlay_min_score;
     int long_path;  // heavy paths at least this long run on the wave-cooperative replay
+    int jscatter;   // HIP: the LDS KRT's epilogue writes its block's outside children's jump words and
+                    // path-top flags (the chip-wide jumping preorder of small batches), else k_pre_sweep
     int64_t mreal;  // merges of the caller's graph (scored); later ones only complete a forest (< M)
     double min_convexity[3];
 

@@ -378,6 +378,7 @@ struct Pipeline {
         const int B = d.B;
         const int64_t N = d.N, M = d.M, NL = d.NL;
         be.mark(3);
+        w.jscatter = Backend::pre_jump(d) ? 1 : 0;
         const bool dnc = use_dnc(d);
         KEdgeInit ei{w, dnc};
         ei.given = given;
