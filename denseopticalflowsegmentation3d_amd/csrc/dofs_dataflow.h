@@ -82,9 +82,9 @@ enum FlowStat {
     FS_RPARKS = 15,    // parks of root heavy paths
     FS_RSTEPS = 16,    // merges replayed by root heavy paths
     FS_RCHUNKS = 17,   // 64-step chunks of root heavy paths
-    // measurement build only (-DDOFS_FLOW_PROF): 100 MHz ticks of the long-path chunk loop, summed over
-    // waves — the steps (with the chunk's first LDS wait), the bbox scan and record stores, and the wait
-    // for the next chunk's resolve loads before they go to LDS
+    // measurement build only (-DDOFS_FLOW_PROF, `make prof`): 100 MHz ticks of the long-path chunk loop,
+    // summed over waves — the steps alone, the tail (bbox scan, record stores, the hand-over of a
+    // finished or blocked chunk), and the next chunk's resolve (its global loads and the waits on them)
     FS_P_STEPS = 18,
     FS_P_TAIL = 19,
     FS_P_NEXT = 20,
@@ -349,6 +349,7 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
         steps += n;
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this chunk's LDS records have landed
         __builtin_amdgcn_wave_barrier();
+        FLOW_PROF_MARK(p_next);  // the next chunk's resolve (its global loads and their waits)
         const OneRec* c = buf[cb];
         auto step = [&](int k, uint4 a, OneHalf b) {  // a = {lk, bm, lkp}, b = {r, wb, fs}
             v = (float)((double)(v * b.fs + b.wb) * b.r);
@@ -370,38 +371,59 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
         // the loop carries only the mean chain — one LDS read, five VALU and one LDS store per step
         // instead of the ~16 instructions with the key update.
         const unsigned krank = K & ~((1u << kRankShift) - 1);
-        if (keyfast && __ballot(lane < n && curlk >= krank) == 0) {
+        const bool fastc = keyfast && __ballot(lane < n && curlk >= krank) == 0;
+        if (fastc) {
             ++kfast;
-            auto stepf = [&](int k, OneHalf b) {
+            // The mean chain alone: per step one ds_read_b128 of the lane's half record, the five chain
+            // ops, and the value (no key: it is K for the whole chunk) into the chunk's output slot. The
+            // records run through three 4-step register sets: a set is reloaded 4 to 8 steps ahead of
+            // its use (~90-170 cycles against the ~50-cycle LDS latency), and the sched barriers keep
+            // the compiler from sinking those loads next to their uses (round 3's ISA had them issued
+            // one to three steps ahead: the LDS latency was exposed twice per 8 steps).
+            float* obv = reinterpret_cast<float*>(ob) + 2 * h;  // .v of ob[2 k + h] at obv[4 k]
+            const OneHalf* ch = &c[0].h[h];
+            auto ld = [&](int k) { return *reinterpret_cast<const OneHalf*>(reinterpret_cast<const char*>(ch) + k * (int)sizeof(OneRec)); };
+            auto stepf = [&](int k, const OneHalf& b) {
                 v = (float)((double)(v * b.fs + b.wb) * b.r);
-                OneOut o;
-                o.v = v;
-                o.k = K;
-                ob[2 * k + h] = o;
+                obv[4 * k] = v;
             };
+            // 8 steps per iteration in two 4-step register sets, each loaded 4 steps (~90 cycles) ahead of
+            // its use; the sched barriers pin the loads there (round 3's ISA had the compiler sink them to
+            // one to three steps ahead of their use: the LDS latency was exposed twice per 8 steps). The
+            // sets are not rotated across iterations (a rotating ring compiled to v_mov_b64 copies, and a
+            // fully unrolled chunk to AGPR spills)
+            OneHalf b0 = ld(0), b1 = ld(1), b2 = ld(2), b3 = ld(3);
             int k = 0;
-            OneHalf b0 = c[0].h[h], b1 = c[1].h[h], b2 = c[2].h[h], b3 = c[3].h[h];
             for (; k + 8 <= n; k += 8) {
-                const int m = k + 4, m2 = (k + 8) & 63;
-                const OneHalf d0 = c[m].h[h], d1 = c[m + 1].h[h], d2 = c[m + 2].h[h], d3 = c[m + 3].h[h];
+                const OneHalf d0 = ld(k + 4), d1 = ld(k + 5), d2 = ld(k + 6), d3 = ld(k + 7);
+                __builtin_amdgcn_sched_barrier(0);
                 stepf(k, b0);
                 stepf(k + 1, b1);
                 stepf(k + 2, b2);
                 stepf(k + 3, b3);
-                b0 = c[m2].h[h], b1 = c[m2 + 1].h[h], b2 = c[m2 + 2].h[h], b3 = c[m2 + 3].h[h];
+                __builtin_amdgcn_sched_barrier(0);
+                b0 = ld(k + 8), b1 = ld(k + 9), b2 = ld(k + 10), b3 = ld(k + 11);
+                __builtin_amdgcn_sched_barrier(0);
                 stepf(k + 4, d0);
                 stepf(k + 5, d1);
                 stepf(k + 6, d2);
                 stepf(k + 7, d3);
+                __builtin_amdgcn_sched_barrier(0);
             }
             if (k + 4 <= n) {
+                const OneHalf d0 = ld(k + 4), d1 = ld(k + 5), d2 = ld(k + 6);
                 stepf(k, b0);
                 stepf(k + 1, b1);
                 stepf(k + 2, b2);
                 stepf(k + 3, b3);
-                k += 4;
+                if (k + 4 < n) stepf(k + 4, d0);
+                if (k + 5 < n) stepf(k + 5, d1);
+                if (k + 6 < n) stepf(k + 6, d2);
+            } else {
+                if (k < n) stepf(k, b0);
+                if (k + 1 < n) stepf(k + 1, b1);
+                if (k + 2 < n) stepf(k + 2, b2);
             }
-            for (; k < n; ++k) stepf(k, c[k].h[h]);
         } else {
         // two register sets, each reloaded right after its last use (4 steps ahead of its next use): no
         // loop-carried copies (the single-set form with next-group temporaries compiled to ~4 v_mov per step)
@@ -457,7 +479,8 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
         __builtin_amdgcn_wave_barrier();
         if (lane < n) {
             const OneOut sx = ob[2 * lane], sy = ob[2 * lane + 1];
-            const int rank = (int)(sx.k >> kRankShift), root = (int)(sx.k & ((1u << kRankShift) - 1));
+            const unsigned kk = fastc ? K : sx.k;  // a constant-key chunk stores only the values
+            const int rank = (int)(kk >> kRankShift), root = (int)(kk & ((1u << kRankShift) - 1));
             RepVal* dst = w.Rv + lb + q - lane;
             if (lane == n - 1 && (finished || n < 64)) {  // the top's record (parent path) or a parked state
                 rv_publish(dst, sx.v, sy.v, rank, root, obb);
@@ -526,11 +549,7 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
         cb ^= 1;
         meta = nmeta;
         lbb = nlbb;
-#ifdef DOFS_FLOW_PROF
         FLOW_PROF_MARK(p_tail);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        FLOW_PROF_MARK(p_next);
-#endif
         buf[cb][lane] = nrec;
         curlk = nrec.lk;
     }

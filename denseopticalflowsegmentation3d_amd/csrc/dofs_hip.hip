@@ -2620,9 +2620,13 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w) {
 // K4 for small batches (Ws::jscatter): chip-wide pointer jumping instead of the per-frame sweep. After the
 // LDS KRT's epilogue a merge's word points to its block-top ancestor inside the block (offset sum), and a
 // block top's word to its parent outside the block (heavy +1, light +2 size(heavy)); the root's is (-1, 0).
-// Only the tops jump (the in-block words are final snapshots of the (top, sum) relation, so a top may hop
-// over any of them): a chain alternates in-block and outside words, at most 2 per block, and two hops per
-// launch on the freshest words at least triple every distance (KJump's invariant, dofs_kernels.h).
+// Only the tops jump: the in-block words are final (top, sum) snapshots, so a hop over a non-top lands on
+// its block's top and costs nothing in the tree of tops, while a hop over a top follows that top's current
+// word. Two hops over tops per launch, on the freshest words, at least triple every distance in the tree
+// of tops (KJump's invariant, dofs_kernels.h), whose depth is at most the number of blocks.
+DOFS_HD inline bool jump_in_block(const Dims& d, int a, int64_t x) {  // a (a merge node) in x's KRT block
+    return (a - d.N) / kDeepTop == (x - d.N) / kDeepTop;
+}
 struct KJumpTop {
     Ws w;
     DOFS_HD void operator()(int f, int64_t k) const {
@@ -2630,24 +2634,33 @@ struct KJumpTop {
         const int64_t lb = f * d.NL, x = d.N + k;
         unsigned long long v = dofs_ld64(w.J + lb + x);
         int a = jump_anc(v);
-        if (a < 0 || (a - d.N) / kDeepTop == k / kDeepTop) return;  // converged, or not a block top
-        for (int h = 0; h < 2 && a >= 0; ++h) {
+        if (a < 0 || jump_in_block(d, a, x)) return;  // converged, or not a block top
+        for (int h = 0; h < 2 && a >= 0;) {
             const unsigned long long u = dofs_ld64(w.J + lb + a);
-            v = jump_pack(jump_anc(u), jump_sum(v) + jump_sum(u));
-            a = jump_anc(v);
+            const int na = jump_anc(u);
+            if (na < 0 || !jump_in_block(d, na, a)) ++h;  // a is a top (a non-top points into its block)
+            v = jump_pack(na, jump_sum(v) + jump_sum(u));
+            a = na;
         }
         dofs_st64(w.J + lb + x, v);
     }
 };
-// then every merge's position: a top's converged sum, or its in-block sum plus its top's
+// then every merge's position: the sum of the offsets up to the root — a top's converged word, or an
+// in-block word plus its top's. Every word is a valid (ancestor, sum) snapshot, so a word that is not
+// converged is walked to the root here (never after enough KJumpTop launches: a guard, not a path).
 struct KOrdMerge {
     Ws w;
     DOFS_HD void operator()(int f, int64_t k) const {
         const Dims& d = w.d;
         const int64_t lb = f * d.NL, x = d.N + k;
         const unsigned long long v = w.J[lb + x];
-        const int a = jump_anc(v);
-        const int q = jump_sum(v) + (a >= 0 ? jump_sum(w.J[lb + a]) : 0);
+        int a = jump_anc(v);
+        int q = jump_sum(v);
+        while (a >= 0) {
+            const unsigned long long u = w.J[lb + a];
+            q += jump_sum(u);
+            a = jump_anc(u);
+        }
         w.pre[lb + x] = q;
         w.ord[lb + q] = (int)x;
     }
@@ -3070,9 +3083,9 @@ struct HipBackend {
     // keeps): it also writes the block tops' path-top flags, which the LDS KRT's epilogue leaves out
     bool pre_sweep(const Ws& w) {
         if (w.jscatter) {  // small batches: chip-wide jumping over the block tops (KJumpTop, KOrdMerge)
-            int launches = 0;
-            const int64_t chain = std::min<int64_t>(w.d.M, jump_chain_bound(w.d.M));
-            for (int64_t span = 1; span < chain; span *= 3) ++launches;
+            int launches = 0;  // the tree of tops is at most one top per block deep
+            const int64_t depth = (w.d.M + kDeepTop - 1) / kDeepTop + 1;
+            for (int64_t span = 1; span < depth; span *= 3) ++launches;
             for (int t = 0; t < launches; ++t) launch(w.d.B, w.d.M, KJumpTop{w});
             launch(w.d.B, w.d.M, KOrdMerge{w});
         } else {
