@@ -89,6 +89,7 @@ enum FlowStat {
     FS_P_TAIL = 19,
     FS_P_NEXT = 20,
     FS_KFAST = 21,     // long-path chunks run with a constant key (no step reaches the carried rank)
+    FS_RESTARTS = 22,  // pipelined resolve: stage fills (a run's first chunk, a re-resolve after a park)
     FS_N = 24
 };
 static_assert(FS_N * kFsStride * 2 == FC_HDR - FC_FS, "FlowStat block size");
@@ -276,8 +277,78 @@ __device__ inline int flow_resolve(const Ws& w, int64_t lb, int p, int top, OneR
     return meta;
 }
 
+// The pipelined resolve of a long path's chunks (flow_long<true>). Resolving a chunk is three dependent
+// global round trips — its StepIn records, then the state words of its dynamic light children, then the
+// records of those that are done (rv_fetch only after the state word was seen done: the publisher wrote
+// the record before the state word) — and the synchronous form paid all three at the top of every
+// chunk, before its 64 steps (about three times the steps' own time). Here chunk q - 64 d of the lane's
+// path runs stage 4 - d while chunk q is stepped: d = 3 loads the StepIn records, d = 2 the state words,
+// d = 1 the records, and chunk q - 64 is built into LDS from them at the next chunk's start. Each stage's
+// loads have one chunk's steps to arrive; a restart (a task's first chunk, or a re-resolve after a park
+// that found its child done) fills the stages synchronously.
+struct FlowPipe {
+    StepIn in1, in2, in3;  // this lane's StepIn in chunks q - 64, q - 128, q - 192
+    int rdy1, rdy2;        // their light children's state words (kFlowDone where not dynamic)
+    RepVal rv1;            // the light child's record (chunk q - 64, dynamic and done)
+};
+// Branch-free loads: a lane that needs none reads a line the wave reads anyway (its path top's), so no
+// loaded register is merged with a constant at a branch join (the merge made the compiler wait for the
+// load right after issuing it).
+__device__ inline StepIn pipe_in(const Ws& w, int64_t lb, int p, int top) {
+    return w.In[lb + (p >= top ? p : top)];  // (p < top: meta is ignored, pipe_build checks p)
+}
+__device__ inline int pipe_rdy(const Ws& w, int64_t lb, const StepIn& in, int p, int top) {
+    const bool dyn = p >= top && (in.meta & kStepDyn);
+    return f_ld(w.ready + lb + (dyn ? in.lb : top));
+}
+__device__ inline RepVal pipe_rv(const Ws& w, int64_t lb, const StepIn& in, int rdy, int p, int top) {
+    const bool need = p >= top && (in.meta & kStepDyn) && rdy == kFlowDone;
+    return rv_fetch(w.Rv + lb + (need ? in.lb : top));  // read before the state word was seen done: unused
+}
+// flow_resolve from the pipeline's loaded values (same record, same meta)
+__device__ inline int pipe_build(const StepIn& in, int rdy, const RepVal& lv, int p, int top, OneRec* o, B4* lbb) {
+    lbb->x0 = lbb->y0 = 0x7fff;
+    lbb->x1 = lbb->y1 = -1;
+    if (p < top) return 0;
+    int meta = in.meta;
+    int lrank = 0, lroot = in.lb;
+    if (in.meta & kStepDyn) {
+        // blocked (the chunk ends here; the park re-checks the state). The record is used only where the
+        // state word it was loaded after read done (pipe_rv); elsewhere the load read another line.
+        if (rdy != kFlowDone) return meta;
+        o->h[0].wb = lv.mx * (float)in.la;
+        o->h[1].wb = lv.my * (float)in.la;
+        lrank = lv.rank;
+        lroot = lv.root;
+        *lbb = lv.bb;
+    } else {
+        o->h[0].wb = in.wbx;
+        o->h[1].wb = in.wby;
+        lbb->x0 = lbb->x1 = (int16_t)(in.la & 0xffff);
+        lbb->y0 = lbb->y1 = (int16_t)(in.la >> 16);
+    }
+    meta |= kLongOk;
+    o->h[0].fs = o->h[1].fs = in.fs;
+    o->h[0].r = o->h[1].r = in.r;
+    o->pad = 0;
+    o->lk = rk_pack(lrank, lroot);
+    o->lkp = o->lk + (1u << kRankShift);
+    o->bm = (meta & kStepB) ? ~0u : 0u;
+    return meta;
+}
+// fill the stages for chunks q - 64 .. q - 192 (synchronous: three round trips)
+__device__ inline void pipe_restart(const Ws& w, int64_t lb, int q, int top, int lane, FlowPipe& P) {
+    P.in1 = pipe_in(w, lb, q - 64 - lane, top);
+    P.in2 = pipe_in(w, lb, q - 128 - lane, top);
+    P.in3 = pipe_in(w, lb, q - 192 - lane, top);
+    P.rdy1 = pipe_rdy(w, lb, P.in1, q - 64 - lane, top);
+    P.rdy2 = pipe_rdy(w, lb, P.in2, q - 128 - lane, top);
+    P.rv1 = pipe_rv(w, lb, P.in1, P.rdy1, q - 64 - lane, top);
+}
+
 // A long path (task word t) on this wave, from its cursor: returns the task word of the parent path
 // that was parked on its top (to run next), or -1 (parked itself, or completed with nobody waiting).
+template <bool kPipe>
 __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut* ob, int keyfast) {
     const Dims& d = w.d;
     const int g = t & kFlowIdMask;
@@ -305,7 +376,9 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
     int meta = flow_resolve(w, lb, q - lane, top, &rec, &lbb);
     buf[cb][lane] = rec;
     unsigned curlk = rec.lk;  // this lane's step key in the current chunk (valid for lanes < n)
-    unsigned chunks = 0, steps = 0, kfast = 0;  // anatomy, added once per call
+    unsigned chunks = 0, steps = 0, kfast = 0, restarts = 1;  // anatomy, added once per call
+    FlowPipe P;
+    if constexpr (kPipe) pipe_restart(w, lb, q, top, lane, P);
 #ifdef DOFS_FLOW_PROF
     unsigned long long p_steps = 0, p_tail = 0, p_next = 0, p_t = wall_clock64();
 #define FLOW_PROF_MARK(acc)                                 \
@@ -329,6 +402,7 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             fs_add(ctl, FS_LCHUNKS, chunks);
             fs_add(ctl, FS_LSTEPS, steps);
             fs_add(ctl, FS_KFAST, kfast);
+            fs_add(ctl, FS_RESTARTS, restarts);
             if (top == 0) {
                 fs_add(ctl, FS_RCHUNKS, chunks);
                 fs_add(ctl, FS_RSTEPS, steps);
@@ -338,7 +412,18 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
     for (;;) {
         OneRec nrec;
         B4 nlbb;
-        const int nmeta = flow_resolve(w, lb, q - 64 - lane, top, &nrec, &nlbb);
+        int nmeta;
+        RepVal rv2;
+        int rdy3 = kFlowDone;
+        StepIn in4;
+        if constexpr (kPipe) {
+            nmeta = pipe_build(P.in1, P.rdy1, P.rv1, q - 64 - lane, top, &nrec, &nlbb);
+            rv2 = pipe_rv(w, lb, P.in2, P.rdy2, q - 128 - lane, top);  // issued now, used a chunk later
+            rdy3 = pipe_rdy(w, lb, P.in3, q - 192 - lane, top);
+            in4 = pipe_in(w, lb, q - 256 - lane, top);
+        } else {
+            nmeta = flow_resolve(w, lb, q - 64 - lane, top, &nrec, &nlbb);
+        }
         const unsigned long long blocked = __ballot(!(meta & kLongOk));
         const unsigned long long tops = __ballot((meta & kLongOk) && (meta & kStepTop));
         const int fb = blocked ? __ffsll((long long)blocked) - 1 : 64;
@@ -543,12 +628,24 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             meta = flow_resolve(w, lb, q - lane, top, &rec, &lbb, pb);
             buf[cb][lane] = rec;
             curlk = rec.lk;
+            if constexpr (kPipe) {  // the stages were for the old cursor
+                pipe_restart(w, lb, q, top, lane, P);
+                ++restarts;
+            }
             continue;
         }
         q -= 64;
         cb ^= 1;
         meta = nmeta;
         lbb = nlbb;
+        if constexpr (kPipe) {
+            P.in1 = P.in2;
+            P.rdy1 = P.rdy2;
+            P.rv1 = rv2;
+            P.in2 = P.in3;
+            P.rdy2 = rdy3;
+            P.in3 = in4;
+        }
         FLOW_PROF_MARK(p_tail);
         buf[cb][lane] = nrec;
         curlk = nrec.lk;
@@ -739,7 +836,7 @@ __device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int 
 // Measured (112 frames, 1080p, tools/flow_stats.py, serial): short paths done at 26.7 ms, the last
 // chain at 42.4 ms; same-box bench 1,518-1,540 Mpixels/s with 128 long and 2,048 short workers.
 template <bool kLong, int kW>
-__global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigned epoch, int keyfast) {
+__global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigned epoch, int keyfast, int pipe) {
     __shared__ OneRec buf[kLong ? kW : 1][2][64];
     __shared__ OneOut ob[kLong ? kW : 1][128];
     const int lane = threadIdx.x & 63;
@@ -755,7 +852,8 @@ __global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigne
             const unsigned long long t1 = fs_now();
             while (t >= 0) {
                 if (lane == 0) fs_add(ctl, FS_LRUNS, 1);
-                const int nx = flow_long(w, ctl, t, buf[wv], ob[wv], keyfast);
+                const int nx = pipe ? flow_long<true>(w, ctl, t, buf[wv], ob[wv], keyfast)
+                                    : flow_long<false>(w, ctl, t, buf[wv], ob[wv], keyfast);
                 if (nx >= 0 && !(nx & kFlowLong)) {  // a short waiter: a one-lane short round (and its waiters)
                     if (lane == 0) fs_add(ctl, FS_INJECT, 1);
                     flow_short(w, ctl, epoch, nx, false, &cb, &ce);

@@ -3233,6 +3233,14 @@ struct HipBackend {
         }();
         return m >= 0 ? m : 1;
     }
+    // pipelined resolve of the long paths' chunks (dofs_dataflow.h FlowPipe): DOFS_FLOW_PIPE=0 / 1, default 1
+    static int flow_pipe() {
+        static const int m = [] {
+            const char* e = getenv("DOFS_FLOW_PIPE");
+            return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : 1;
+        }();
+        return m;
+    }
     static int flow_long_workers() {  // waves that run long paths (the rest of the grid runs short ones)
         static const int g = [] {
             const char* e = getenv("DOFS_FLOW_LONG");
@@ -3272,9 +3280,9 @@ struct HipBackend {
             note(hipStreamWaitEvent(flow_stream, flow_ev[0], 0), "hipStreamWaitEvent");
             const int kf = keyfast(w.d);
             hipLaunchKernelGGL((k_replay_flow<true, kFlowLongW>), dim3((unsigned)gl), dim3(64 * kFlowLongW), 0, flow_stream,
-                               w, flow_ctl, flow_epoch, kf);
+                               w, flow_ctl, flow_epoch, kf, flow_pipe());
             hipLaunchKernelGGL((k_replay_flow<false, kFlowShortW>), dim3((unsigned)gs), dim3(64 * kFlowShortW), 0, stream,
-                               w, flow_ctl, flow_epoch, kf);
+                               w, flow_ctl, flow_epoch, kf, 0);
             note(hipEventRecord(flow_ev[1], flow_stream), "hipEventRecord");
             note(hipStreamWaitEvent(stream, flow_ev[1], 0), "hipStreamWaitEvent");
         });

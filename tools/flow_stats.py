@@ -24,7 +24,7 @@ flows = torch.empty((B, H, W, 2), dtype=torch.float32, device=dev)
 sh = torch.cuda.current_stream(dev).cuda_stream
 runtime.synth_flow_device(flows.data_ptr(), B, H, W, 0, stream=sh)
 names = ["t0", "t_short_done", "t_long_last", "t_exit", "long_runs", "long_parks", "long_chunks", "pushes", "injects",
-         "long_done", "long_ticks", "short_rounds", "short_ticks", "long_steps", "t_root", "root_parks", "root_steps", "root_chunks", "p_steps", "p_tail", "p_next", "kfast_chunks"]
+         "long_done", "long_ticks", "short_rounds", "short_ticks", "long_steps", "t_root", "root_parks", "root_steps", "root_chunks", "p_steps", "p_tail", "p_next", "kfast_chunks", "restarts"]
 for b in range(NB):
     ctx.segment_batch_device(flows.data_ptr(), B, H, W, persp, inv, up, stream=sh)
     torch.cuda.synchronize()
@@ -37,7 +37,8 @@ for b in range(NB):
            "wave_ms_in_short": v["short_ticks"] / 1e5,
            "prof_ms": {k: v[k] / 1e5 for k in ("p_steps", "p_tail", "p_next")}}
     res.update({k: v[k] for k in ("long_runs", "long_parks", "long_chunks", "pushes", "injects", "long_done",
-                                  "short_rounds", "long_steps", "root_parks", "root_steps", "root_chunks", "kfast_chunks")})
+                                  "short_rounds", "long_steps", "root_parks", "root_steps", "root_chunks", "kfast_chunks",
+                                  "restarts")})
     print(json.dumps(res), flush=True)
 ctr = ctx.batch_counters(B)
 print(json.dumps({"paths": int(ctr[:, 0].sum()), "long": int(ctr[:, 7].sum()), "short": int(ctr[:, 6].sum()),

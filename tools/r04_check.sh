@@ -17,12 +17,16 @@ fi
 if [ -z "${SKIP_BENCH:-}" ]; then
 step bench 600 python bench.py ${BENCH_ARGS:-}
 fi
+if [ -n "${VARIANTS:-}" ]; then  # same-box A/B of library / environment variants (tools/ab_env.sh)
+timeout -k 10 900 bash tools/ab_env.sh || exit 1
+fi
 if [ -n "${ANATOMY:-}" ]; then
 P=denseopticalflowsegmentation3d_amd/_build/prof/libdofs_hip.so
 step flow1080 300 env DOFS_SERIAL=1 python tools/flow_stats.py 112 2
 step flow4k 300 env DOFS_SERIAL=1 H=2160 W=3840 python tools/flow_stats.py 1 3
 step flow1080_prof 300 env DOFS_SERIAL=1 DOFS_LIB=$P python tools/flow_stats.py 112 2
 step flow4k_prof 300 env DOFS_SERIAL=1 DOFS_LIB=$P H=2160 W=3840 python tools/flow_stats.py 1 3
+step flow4k_prof_nopipe 300 env DOFS_FLOW_PIPE=0 DOFS_SERIAL=1 DOFS_LIB=$P H=2160 W=3840 python tools/flow_stats.py 1 3
 step intraframe 300 python tools/bench_intraframe.py --model 4
 fi
 exit 0
