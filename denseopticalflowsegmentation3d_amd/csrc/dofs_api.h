@@ -554,6 +554,10 @@ int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity
     be.d2h(rv.data(), w.Rv + fo, sizeof(RepVal) * (size_t)d.NL);
     be.d2h(sz.data(), w.SZ + fo + d.N, 4 * (size_t)d.M);
     be.sync();
+    for (int64_t i = 0; i < M; ++i) {  // (the KRT sweep's singleton flags, Ws::single)
+        eu[(size_t)i] &= kEndMask;
+        evv[(size_t)i] &= kEndMask;
+    }
     if (!keys)
         for (int64_t i = 0; i < M; ++i) {  // KMstEmit's edge_weight: float differences, double squares
             const F2 a = bl[(size_t)eu[i]], b = bl[(size_t)evv[i]];

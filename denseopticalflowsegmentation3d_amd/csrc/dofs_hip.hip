@@ -2017,9 +2017,13 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
             e[2 * k + 1] = t < cnt ? EV[s + t] : 0;
         }
 #pragma unroll
-        for (int k = 0; k < K2; ++k) {
+        for (int k = 0; k < K2; ++k) {  // a single pixel (its first merge, Ws::single) needs no find
+            const bool one = (e[k] >> kSingleBit) & 1;
+            e[k] &= kEndMask;
             c[k] = e[k];
-            pend[k] = act2[k];
+            pend[k] = act2[k] && !one;
+            rtl[k] = -1;
+            rts[k] = 1;
         }
 #ifdef DOFS_KRT_TIMING
         {  // the slowest thread's find rounds (two dependent loads each) in phase A
@@ -3016,6 +3020,7 @@ struct HipBackend {
     // 386 vs 312 Mpix/s). Round 3's first-batch size error of this path (1 in 6 fresh contexts) was the
     // slot-table race in k_dnc_compress, fixed there; tests/test_gpu_krt_dnc.py holds the two modes equal.
     static constexpr bool kDncAuto = true;
+    static constexpr bool kSingleFlags = true;  // KMstEmit / KEdgeInit mark single-pixel endpoints (Ws::single)
     // longest pointer chain the preorder's global jumping starts from: every word leaves its block
     // or goes to the block's top, so at most two words per block on any path
     static int64_t jump_chain_bound(int64_t M) { return 2 * ((M + kDeepTop - 1) / kDeepTop) + 1; }

@@ -130,6 +130,9 @@ struct Ws {
     int long_path;  // heavy paths at least this long run on the wave-cooperative replay
     int jscatter;   // HIP: the LDS KRT's epilogue writes its block's outside children's jump words and
                     // path-top flags (the chip-wide jumping preorder of small batches), else k_pre_sweep
+    int single;     // HIP: EU / EV carry bit kSingleBit — the endpoint is a single pixel at this merge (the
+                    // merge is its minimum incident edge, so its first in Kruskal order): the KRT sweep
+                    // takes its label without a find
     int64_t mreal;  // merges of the caller's graph (scored); later ones only complete a forest (< M)
     double min_convexity[3];
 
@@ -366,6 +369,7 @@ DOFS_UNROLL
         unsigned long long best = ~0ull;
         unsigned bidx = kNoEdge;
         int64_t far = p;
+        int jb = 0xFF;
 DOFS_UNROLL
         for (int j = 0; j < 8; ++j) {
             if (!ok[j] || !((allow_bits >> j) & 1)) continue;
@@ -378,8 +382,12 @@ DOFS_UNROLL
                 best = wb;
                 bidx = idx;
                 far = q[j];
+                jb = j;
             }
         }
+        // the pixel's minimum incident edge as its slot 0..7 (0xFF: none), in the leaf part of lite (free:
+        // path-top flags are written and read for merge nodes only) until KMstEmit reads it
+        if (w.single) w.lite[f * d.NL + p] = (unsigned char)jb;
         const int64_t o = f * d.N + p;
         w.bw[o] = ~0ull;
         w.bi[o] = kNoEdge;
@@ -548,6 +556,11 @@ struct KMstCount {
     }
 };
 
+// singleton flags (Ws::single): in the sorted values' two top bits (KMstEmit; the sort fix-up compares
+// values below them), then in EU / EV bit kSingleBit (KEdgeInit; pixel ids are < 2^26)
+constexpr unsigned kValSingleS = 1u << 30, kValSingleE = 1u << 31;
+constexpr int kSingleBit = 30;
+constexpr int kEndMask = (1 << kSingleBit) - 1;
 struct KMstEmit {
     Ws w;
     int fshift;  // > 0: the frame id rides above the emission index (one batch-wide frame sort, HIP)
@@ -562,13 +575,22 @@ struct KMstEmit {
         F2 bq[4];
         DOFS_UNROLL
         for (int k = 0; k < 4; ++k) bq[k] = b[(bits >> k) & 1 ? edge_end(d, p, k) : p];
+        unsigned ms = 0xFF, mq[4] = {0xFF, 0xFF, 0xFF, 0xFF};  // minimum-edge slots of p and of the far ends
+        if (w.single) {
+            const unsigned char* lt = w.lite + f * d.NL;
+            ms = lt[p];
+            DOFS_UNROLL
+            for (int k = 0; k < 4; ++k) mq[k] = (bits >> k) & 1 ? lt[edge_end(d, p, k)] : 0xFF;
+        }
         DOFS_UNROLL
         for (int k = 0; k < 4; ++k) {
             if (!(bits & (1 << k))) continue;
             if (j < d.M) {
                 const double dx = bp.x - bq[k].x, dy = bp.y - bq[k].y;  // edge_weight(b, p, q)
                 w.key_in[f * d.M + j] = dbits(sqrt(dx * dx + dy * dy));
-                w.val_in[f * d.M + j] = (unsigned)(4 * p + k) | (fshift ? (unsigned)f << fshift : 0u);
+                // p's first merge is its minimum edge (slot k); the far end receives this edge in its slot 4 + k
+                const unsigned sg = (ms == (unsigned)k ? kValSingleS : 0u) | (mq[k] == (unsigned)(4 + k) ? kValSingleE : 0u);
+                w.val_in[f * d.M + j] = (unsigned)(4 * p + k) | (fshift ? (unsigned)f << fshift : 0u) | sg;
             }
             ++j;
         }
@@ -589,11 +611,14 @@ struct KEdgeInit {  // endpoints by rank; labels = the endpoints (global-kernel 
             p = w.EU[o];
             q = w.EV[o];
         } else {
-            const unsigned idx = w.val_out[o] & vmask;
+            const unsigned val = w.val_out[o];
+            const unsigned idx = val & vmask;
             p = idx >> 2;
             q = edge_end(d, p, idx & 3);
-            w.EU[o] = (int)p;
-            w.EV[o] = (int)q;
+            const int su = w.single && (val & kValSingleS) ? 1 << kSingleBit : 0;
+            const int sv = w.single && (val & kValSingleE) ? 1 << kSingleBit : 0;
+            w.EU[o] = (int)p | su;
+            w.EV[o] = (int)q | sv;
         }
         if (!labels) return;  // the sweep writes every merge's block-start labels
         w.lu[o] = (int)p;

@@ -264,6 +264,7 @@ struct Pipeline {
     // dims_for(1, rows, W, nbr8).
     void run_band(const F2* flow_rows, int row0, int rows, int H, int r0, int r1, unsigned char* mask) {
         const int nbr8 = w.d.nbr8;
+        w.single = 0;
         Ws wr = w;
         wr.d = dims_for(1, rows, w.d.W, nbr8);
         wr.flow = flow_rows;
@@ -290,6 +291,13 @@ struct Pipeline {
         w.mreal = M;
         w.flow = flow;
         w.flow_fstride = fstride;
+        {  // singleton flags ride in the two top value bits: only when the index and frame bits leave them
+            const int vb = ceil_log2(4 * N);
+            int fb = 0;
+            if (be.mst_packed(std::max<int64_t>(M, 1), B, vb))
+                while ((1 << fb) < B) ++fb;
+            w.single = Backend::kSingleFlags && vb + fb <= 30 ? 1 : 0;
+        }
         be.memset(w.ctr, 0, sizeof(int) * (size_t)B * kCounters);
 
         be.mark(0);
@@ -331,6 +339,7 @@ struct Pipeline {
         if (E >= (int64_t)0x7FFFFFFF) return -1;  // positions and the scan are 32-bit
         w.flow = flow;
         w.flow_fstride = N;
+        w.single = 0;  // the caller's edge list: no minimum-edge slots
         be.memset(w.ctr, 0, sizeof(int) * kCounters);
         be.mark(0);
         be.launch(1, N, KCopyFlow{w});

@@ -44,8 +44,10 @@ struct SortFix {
     int cut;
 };
 
+// values compare below their two top bits (the KRT sweep's singleton flags, dofs_kernels.h kValSingle*: the
+// frame and emission index, distinct for all pairs, sit below them)
 __device__ inline bool fix_less(unsigned long long ka, unsigned va, unsigned long long kb, unsigned vb) {
-    return ka < kb || (ka == kb && va < vb);
+    return ka < kb || (ka == kb && (va & 0x3FFFFFFFu) < (vb & 0x3FFFFFFFu));
 }
 
 // the scalar path of one group [p, ...) from its first position: at most kFixScan positions, in place
