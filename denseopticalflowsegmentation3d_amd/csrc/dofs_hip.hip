@@ -2555,9 +2555,10 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w) {
     struct Node {  // a merge's static inputs (final until swept)
         unsigned long long v, hl;
         int a, b;
-        unsigned char lB;
+        unsigned char lB, lt;  // light side, path-top flag (the epilogue's, for a merge under an in-block parent)
     };
     Node nd[kPreK];
+    F2 lf[kPreK];  // the light child's blurred flow when it is a pixel (its StepIn, KPathInit's step_in)
     auto load = [&](int64_t blk, Node (&o)[kPreK]) {
         const int64_t s0 = blk * kDeepTop;
         const int cnt = (int)((d.M - s0) < kDeepTop ? (d.M - s0) : kDeepTop);
@@ -2570,10 +2571,25 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w) {
                 o[k].a = w.lu[eb + s0 + t];
                 o[k].b = w.lv[eb + s0 + t];
                 o[k].lB = w.hlB[eb + s0 + t];
+                o[k].lt = w.lite[lb + d.N + s0 + t];
             }
         }
     };
-    if (nblk > 0) load(nblk - 1, nd);
+    const F2* bl = w.blur + f * d.N;
+    auto gather = [&](int64_t blk) {  // issued a block ahead of its use (after the block's inputs arrived)
+        const int64_t s0 = blk * kDeepTop;
+        const int cnt = (int)((d.M - s0) < kDeepTop ? (d.M - s0) : kDeepTop);
+#pragma unroll
+        for (int k = 0; k < kPreK; ++k) {
+            const int t = tid + k * kPreT;
+            const int l = nd[k].lB ? nd[k].b : nd[k].a;
+            if (t < cnt && l < d.N) lf[k] = bl[l];
+        }
+    };
+    if (nblk > 0) {
+        load(nblk - 1, nd);
+        gather(nblk - 1);
+    }
     for (int64_t blk = nblk - 1; blk >= 0; --blk) {
         const int64_t s0 = blk * kDeepTop, x0 = d.N + s0;
         const int cnt = (int)((d.M - s0) < kDeepTop ? (d.M - s0) : kDeepTop);
@@ -2612,11 +2628,23 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w) {
             const int h = nd[k].lB ? nd[k].a : nd[k].b, l = nd[k].lB ? nd[k].b : nd[k].a;
             if (h < x0 && h >= d.N) pre[h] = pos[k] + 1;
             if (l < x0 && l >= d.N) pre[l] = (pos[k] + 2 * sh) | kPushLight;
+            // the merge's replay inputs at its position (KPathInit's step_in, the same record; random
+            // 32-B stores, fire and forget): a top's path-top flag is its push's, a merge under an
+            // in-block parent has its flag from the KRT epilogue
+            const bool ptop = top[k] ? (x == root || (pushed[k] & kPushLight)) : nd[k].lt != 0;
+            StepIn in;
+            if (l < d.N) {
+                in = step_in_leaf(nd[k].hl, ptop, nd[k].lB, l, lf[k], d.W);
+            } else {
+                in = step_in(w, f, pos[k], ptop, l, nd[k].lB, nd[k].hl);  // (a merge light child: no load)
+            }
+            w.In[lb + pos[k]] = in;
         }
         __syncthreads();  // the pushes are read by the blocks below
         if (blk > 0) {
 #pragma unroll
             for (int k = 0; k < kPreK; ++k) nd[k] = nx[k];
+            gather(blk - 1);
         }
     }
 }
@@ -3097,6 +3125,7 @@ struct HipBackend {
             timed("k_pre_sweep", [&] { hipLaunchKernelGGL(k_pre_sweep, dim3((unsigned)w.d.B), dim3(kPreT), 0, stream, w); });
             if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_pre_sweep launch");
         }
+        pre_steps_done = !w.jscatter;  // the sweep wrote every StepIn (KPathInit registers the paths only)
         launch(w.d.B, w.d.M, KLeafPos{w});
         return true;
     }
@@ -3108,6 +3137,8 @@ struct HipBackend {
         return e ? atoi(e) : 8;
     }
     static bool pre_jump(const Dims& d) { return d.B <= pre_jump_frames(); }
+    bool pre_steps_done = false;  // the last pre_sweep wrote the StepIn records (k_pre_sweep)
+    static bool pre_steps(const HipBackend& b) { return b.pre_steps_done; }
     void boruvka_relabel(const Ws& w, int r) {
         if (r >= 1 && rec_path(w) && relabel_tiles()) {  // round 0 runs before the tile flags exist
             rec_launch(w, r, k_boruvka_relabel_t, "k_boruvka_relabelt");

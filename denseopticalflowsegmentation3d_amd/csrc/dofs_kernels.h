@@ -130,6 +130,7 @@ struct Ws {
     int long_path;  // heavy paths at least this long run on the wave-cooperative replay
     int jscatter;   // HIP: the LDS KRT's epilogue writes its block's outside children's jump words and
                     // path-top flags (the chip-wide jumping preorder of small batches), else k_pre_sweep
+    int pre_steps;  // HIP: k_pre_sweep wrote every merge's StepIn (KPathInit then registers the paths only)
     int single;     // HIP: EU / EV carry bit kSingleBit — the endpoint is a single pixel at this merge (the
                     // merge is its minimum incident edge, so its first in Kruskal order): the KRT sweep
                     // takes its label without a find
@@ -1127,6 +1128,44 @@ constexpr int kPendLong = kIntMax - 1;  // long path, not complete
 constexpr int kParkBase = kIntMax - 2;  // long path stopped in round r: kParkBase - r
 
 
+// The replay's inputs of the merge at preorder position q (Forest::merge, graph.cpp:170-218): heavy and
+// light child sizes hl (sh | sl << 32), the light child lt (its side lB), whether q tops a heavy path
+DOFS_HD inline StepIn step_in(const Ws& w, int f, int q, bool top, int lt, int lB, unsigned long long hl) {
+    const Dims& d = w.d;
+    const int sh = (int)(unsigned)(hl & 0xffffffffu), sl = (int)(unsigned)(hl >> 32);
+    StepIn in;
+    in.fs = (float)sh;
+    in.r = 1. / (double)(sh + sl);  // size(x)
+    in.meta = (lB ? kStepB : 0) | (top ? kStepTop : 0);
+    if (lt < d.N) {
+        const F2 v = w.blur[f * d.N + lt];
+        in.wbx = v.x * (float)1;
+        in.wby = v.y * (float)1;
+        in.la = (lt % d.W) | ((lt / d.W) << 16);
+        in.lb = lt;
+    } else {
+        in.meta |= kStepDyn;
+        in.wbx = in.wby = 0.f;
+        in.la = sl;
+        in.lb = q + 2 * sh;  // heavy-first preorder: the light child follows the heavy subtree
+    }
+    return in;
+}
+
+// step_in for a pixel light child whose blurred flow lf is already loaded (the preorder sweep's gather)
+DOFS_HD inline StepIn step_in_leaf(unsigned long long hl, bool top, int lB, int lt, F2 lf, int W) {
+    const int sh = (int)(unsigned)(hl & 0xffffffffu), sl = (int)(unsigned)(hl >> 32);
+    StepIn in;
+    in.fs = (float)sh;
+    in.r = 1. / (double)(sh + sl);
+    in.meta = (lB ? kStepB : 0) | (top ? kStepTop : 0);
+    in.wbx = lf.x * (float)1;
+    in.wby = lf.y * (float)1;
+    in.la = (lt % W) | ((lt / W) << 16);
+    in.lb = lt;
+    return in;
+}
+
 struct KPathInit {  // one lane per merge node x = N + k; path ids and lists through the list taker
     Ws w;
     const int* pre;
@@ -1141,27 +1180,12 @@ struct KPathInit {  // one lane per merge node x = N + k; path ids and lists thr
         if (valid) {
             q = pre[lb + x];
             top = w.lite[lb + x] != 0;
-            int lt, lB;
-            heavy_child(w, f, (int)x, &lt, &lB);
-            const unsigned long long hl = w.hls[f * d.M + k];  // children's sizes (the KRT's parent pass)
-            const int sh = (int)(unsigned)(hl & 0xffffffffu), sl = (int)(unsigned)(hl >> 32);
-            StepIn in;
-            in.fs = (float)sh;
-            in.r = 1. / (double)(sh + sl);  // size(x)
-            in.meta = (lB ? kStepB : 0) | (top ? kStepTop : 0);
-            if (lt < d.N) {
-                const F2 v = w.blur[f * d.N + lt];
-                in.wbx = v.x * (float)1;
-                in.wby = v.y * (float)1;
-                in.la = (lt % d.W) | ((lt / d.W) << 16);
-                in.lb = lt;
-            } else {
-                in.meta |= kStepDyn;
-                in.wbx = in.wby = 0.f;
-                in.la = sl;
-                in.lb = q + 2 * sh;  // heavy-first preorder: the light child follows the heavy subtree
+            if (!w.pre_steps) {  // (else the preorder sweep wrote it, k_pre_sweep: the same record)
+                int lt, lB;
+                heavy_child(w, f, (int)x, &lt, &lB);
+                const unsigned long long hl = w.hls[f * d.M + k];  // children's sizes (the KRT's parent pass)
+                w.In[lb + q] = step_in(w, f, q, top, lt, lB, hl);
             }
-            w.In[lb + q] = in;
             if (top) {  // heavy path [q, bottom): its bottom leaf is the first leaf after q in preorder
                 qb = w.lposr[f * d.N + w.lscan[lb + q]];
                 islong = qb - q >= w.long_path;

@@ -440,7 +440,10 @@ struct Pipeline {
         be.scan_excl_leaf(w.ord, w.lscan, NL, B, N);
         be.launch(B, NL, KLeafOrder{w, pre});
     }
-    void path_init() { be.launch(w.d.B, w.d.M, KPathInit{w, w.pre}); }
+    void path_init() {
+        w.pre_steps = Backend::pre_steps(be) ? 1 : 0;
+        be.launch(w.d.B, w.d.M, KPathInit{w, w.pre});
+    }
 
     // Phase B (replay + scoring): the order-dependent replay is latency-bound (a few waves per
     // frame), so the HIP backend overlaps it with the next batch's phase A on a second stream.

@@ -238,6 +238,8 @@ struct HostBackend {
     bool pre_sweep(const Ws&) { return false; }  // KJump (the emulator's KRT has no block epilogue)
     static bool pre_jump(const Dims&) { return false; }  // (KDncParent writes every word itself)
     static constexpr bool kSingleFlags = false;  // its sweep model reads EU / EV as plain endpoints
+    template <class B>
+    static bool pre_steps(const B&) { return false; }  // KPathInit writes the StepIn records
     void sort_mst(Ws& w, int64_t n, int nf, int value_bits, bool) {
         sort_pairs(w.key_in, w.key_out, w.val_in, w.val_out, n, nf, value_bits);
     }
