@@ -1322,7 +1322,7 @@ __global__ __launch_bounds__(256) void k_boruvka_min(Ws w, int r, int pass, unsi
                     // edge_weight(b, s, e) with s the emitting pixel: float differences, double squares
                     const F2 bs = j < 4 ? bp : bq[j], be = j < 4 ? bq[j] : bp;
                     const double dx = bs.x - be.x, dy = bs.y - be.y;
-                    const unsigned long long wb = dbits(sqrt(dx * dx + dy * dy));
+                    const unsigned long long wb = dbits(sqrt(sq_len(dx, dy)));
                     const unsigned idx = (unsigned)(4 * (j < 4 ? p : q[j]) + (j & 3));
                     if (wb < best || (wb == best && idx < bidx)) {
                         best = wb;
@@ -1538,7 +1538,7 @@ __global__ __launch_bounds__(256) void k_boruvka_min4(Ws w, int r, RecBufs rb) {
             for (int j = 0; j < 8; ++j) {
                 const F2 bs = j < 4 ? f0 : fq[j], be = j < 4 ? fq[j] : f0;
                 const double dx = bs.x - be.x, dy = bs.y - be.y;
-                sqb[j] = (ok[j] && cq[j] != c0) ? dbits(dx * dx + dy * dy) : ~0ull;
+                sqb[j] = (ok[j] && cq[j] != c0) ? dbits(sq_len(dx, dy)) : ~0ull;
                 msq = sqb[j] < msq ? sqb[j] : msq;
             }
             unsigned long long best = ~0ull;

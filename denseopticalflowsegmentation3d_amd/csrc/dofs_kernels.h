@@ -161,11 +161,15 @@ DOFS_HD inline int64_t edge_end(const Dims& d, int64_t p, int k) {
         default: return p + d.W - 1;
     }
 }
+// dx * dx + dy * dy for dx, dy converted from floats, bit for bit with one rounding less to issue: a
+// float's square is exact in double (24 + 24 significant bits <= 53, no overflow or underflow for any
+// float), so fma(dx, dx, dy * dy) rounds the same exact sum the separate multiply and add round once
+DOFS_HD inline double sq_len(double dx, double dy) { return fma(dx, dx, dy * dy); }
 // diff (segment.cpp:20-32): float subtraction, double squares/sum/sqrt (correctly rounded).
 DOFS_HD inline double edge_weight(const F2* b, int64_t p, int64_t q) {
     double dx = b[p].x - b[q].x;
     double dy = b[p].y - b[q].y;
-    return sqrt(dx * dx + dy * dy);
+    return sqrt(sq_len(dx, dy));
 }
 DOFS_HD inline unsigned long long dbits(double w) {
     union {
@@ -377,7 +381,7 @@ DOFS_UNROLL
             // edge_weight(b, s, e) with s the emitting pixel: float differences, double squares
             const F2 bs = j < 4 ? bp : bq[j], be = j < 4 ? bq[j] : bp;
             const double dx = bs.x - be.x, dy = bs.y - be.y;
-            const unsigned long long wb = dbits(sqrt(dx * dx + dy * dy));
+            const unsigned long long wb = dbits(sqrt(sq_len(dx, dy)));
             const unsigned idx = (unsigned)(4 * (j < 4 ? p : q[j]) + (j & 3));
             if (wb < best || (wb == best && idx < bidx)) {
                 best = wb;
@@ -588,7 +592,7 @@ struct KMstEmit {
             if (!(bits & (1 << k))) continue;
             if (j < d.M) {
                 const double dx = bp.x - bq[k].x, dy = bp.y - bq[k].y;  // edge_weight(b, p, q)
-                w.key_in[f * d.M + j] = dbits(sqrt(dx * dx + dy * dy));
+                w.key_in[f * d.M + j] = dbits(sqrt(sq_len(dx, dy)));
                 // p's first merge is its minimum edge (slot k); the far end receives this edge in its slot 4 + k
                 const unsigned sg = (ms == (unsigned)k ? kValSingleS : 0u) | (mq[k] == (unsigned)(4 + k) ? kValSingleE : 0u);
                 w.val_in[f * d.M + j] = (unsigned)(4 * p + k) | (fshift ? (unsigned)f << fshift : 0u) | sg;

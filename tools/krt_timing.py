@@ -1,6 +1,7 @@
 """KRT phase anatomy from a measurement build (-DDOFS_KRT_TIMING, exports dofs_debug_krt_timing):
 runs batches of synthetic 1080p frames and prints the wall time per phase, summed over workgroups and
-per 4096-merge block. usage: DOFS_LIB=_ab/T/libdofs_hip.so python tools/krt_timing.py [B] [batches]"""
+per 4096-merge block. usage: DOFS_LIB=denseopticalflowsegmentation3d_amd/_build/krt/libdofs_hip.so python tools/krt_timing.py [B] [batches]
+(the measurement build: make -C denseopticalflowsegmentation3d_amd/csrc krt)"""
 import ctypes as C
 import json
 import os
@@ -32,7 +33,7 @@ torch.cuda.synchronize()
 ctx.records_device()
 L.dofs_debug_krt_timing(out, 16)
 blocks = NB * B * ((H * W - 1 + 4095) // 4096)
-names = ["sweep A finds", "sweep B unions", "sweep C roots+hash", "sweep D stores", "sweep top level (L half, R relabel)", "top level",
+names = ["sweep A finds", "sweep B root hash", "sweep C R-half unions + sizes", "sweep D stores", "sweep C L-half unions + top level", "top level",
          "deep block 1", "deep block 2", "parent epilogue", "deep depths S>=256", "deep depths S<256",
          "LDS worker wait"]
 res = {n: {"total_ms": round(out[i] / 1e3, 2), "us_per_block": round(out[i] / blocks, 2)}
