@@ -371,23 +371,38 @@ DOFS_UNROLL
             allow_bits = al[p] & 0xfu;
             for (int j = 4; j < 8; ++j) allow_bits |= ((al[q[j]] >> (j - 4)) & 1u) << j;
         }
+        // the lexicographic minimum (weight, index): edge_weight(b, s, e) = sqrt(sq) with s the emitting
+        // pixel (float differences, double squares). sqrt is monotone and correctly rounded, so the
+        // minimum weight is sqrt of the minimum sq, and only edges whose sq lies within 2^-48 (relative)
+        // of it can tie with it (a weight's rounding interval is 2^-52 wide): one sqrt per pixel, not
+        // eight (as k_boruvka_min4 does in the later rounds)
+        unsigned long long sqb[8];
+        unsigned long long msq = ~0ull;  // bits of non-negative doubles order like the values
+DOFS_UNROLL
+        for (int j = 0; j < 8; ++j) {
+            const F2 bs = j < 4 ? bp : bq[j], be = j < 4 ? bq[j] : bp;
+            const double dx = bs.x - be.x, dy = bs.y - be.y;
+            sqb[j] = (ok[j] && ((allow_bits >> j) & 1)) ? dbits(sq_len(dx, dy)) : ~0ull;
+            msq = sqb[j] < msq ? sqb[j] : msq;
+        }
         unsigned long long best = ~0ull;
         unsigned bidx = kNoEdge;
         int64_t far = p;
         int jb = 0xFF;
+        if (msq != ~0ull) {
+            const double mv = bitsd(msq);
+            best = dbits(sqrt(mv));
+            const unsigned long long thr = dbits(mv * 1.0000000000000036);  // (1 + 2^-48) mv
 DOFS_UNROLL
-        for (int j = 0; j < 8; ++j) {
-            if (!ok[j] || !((allow_bits >> j) & 1)) continue;
-            // edge_weight(b, s, e) with s the emitting pixel: float differences, double squares
-            const F2 bs = j < 4 ? bp : bq[j], be = j < 4 ? bq[j] : bp;
-            const double dx = bs.x - be.x, dy = bs.y - be.y;
-            const unsigned long long wb = dbits(sqrt(sq_len(dx, dy)));
-            const unsigned idx = (unsigned)(4 * (j < 4 ? p : q[j]) + (j & 3));
-            if (wb < best || (wb == best && idx < bidx)) {
-                best = wb;
-                bidx = idx;
-                far = q[j];
-                jb = j;
+            for (int j = 0; j < 8; ++j) {
+                if (sqb[j] > thr) continue;  // also the non-candidates (~0)
+                const bool tie = sqb[j] == msq || dbits(sqrt(bitsd(sqb[j]))) == best;
+                const unsigned idx = (unsigned)(4 * (j < 4 ? p : q[j]) + (j & 3));
+                if (tie && idx < bidx) {
+                    bidx = idx;
+                    far = q[j];
+                    jb = j;
+                }
             }
         }
         // the pixel's minimum incident edge as its slot 0..7 (0xFF: none), in the leaf part of lite (free:
