@@ -465,12 +465,23 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             // its use (~90-170 cycles against the ~50-cycle LDS latency), and the sched barriers keep
             // the compiler from sinking those loads next to their uses (round 3's ISA had them issued
             // one to three steps ahead: the LDS latency was exposed twice per 8 steps).
-            float* obv = reinterpret_cast<float*>(ob) + 2 * h;  // .v of ob[2 k + h] at obv[4 k]
+            // values only, as two rows of 64 floats in ob's storage (x row, y row): four steps' values
+            // are contiguous, one ds_write_b128 per 4 steps
+            float* fvh = reinterpret_cast<float*>(ob) + 64 * h;
             const OneHalf* ch = &c[0].h[h];
             auto ld = [&](int k) { return *reinterpret_cast<const OneHalf*>(reinterpret_cast<const char*>(ch) + k * (int)sizeof(OneRec)); };
-            auto stepf = [&](int k, const OneHalf& b) {
+            auto chain = [&](const OneHalf& b) {
                 v = (float)((double)(v * b.fs + b.wb) * b.r);
-                obv[4 * k] = v;
+                return v;
+            };
+            auto stepf = [&](int k, const OneHalf& b) { fvh[k] = chain(b); };
+            auto step4 = [&](int k, const OneHalf& a0, const OneHalf& a1, const OneHalf& a2, const OneHalf& a3) {
+                float4 o;
+                o.x = chain(a0);
+                o.y = chain(a1);
+                o.z = chain(a2);
+                o.w = chain(a3);
+                *reinterpret_cast<float4*>(fvh + k) = o;
             };
             // 8 steps per iteration in two 4-step register sets, each loaded 4 steps (~90 cycles) ahead of
             // its use; the sched barriers pin the loads there (round 3's ISA had the compiler sink them to
@@ -482,25 +493,16 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             for (; k + 8 <= n; k += 8) {
                 const OneHalf d0 = ld(k + 4), d1 = ld(k + 5), d2 = ld(k + 6), d3 = ld(k + 7);
                 __builtin_amdgcn_sched_barrier(0);
-                stepf(k, b0);
-                stepf(k + 1, b1);
-                stepf(k + 2, b2);
-                stepf(k + 3, b3);
+                step4(k, b0, b1, b2, b3);
                 __builtin_amdgcn_sched_barrier(0);
                 b0 = ld(k + 8), b1 = ld(k + 9), b2 = ld(k + 10), b3 = ld(k + 11);
                 __builtin_amdgcn_sched_barrier(0);
-                stepf(k + 4, d0);
-                stepf(k + 5, d1);
-                stepf(k + 6, d2);
-                stepf(k + 7, d3);
+                step4(k + 4, d0, d1, d2, d3);
                 __builtin_amdgcn_sched_barrier(0);
             }
             if (k + 4 <= n) {
                 const OneHalf d0 = ld(k + 4), d1 = ld(k + 5), d2 = ld(k + 6);
-                stepf(k, b0);
-                stepf(k + 1, b1);
-                stepf(k + 2, b2);
-                stepf(k + 3, b3);
+                step4(k, b0, b1, b2, b3);
                 if (k + 4 < n) stepf(k + 4, d0);
                 if (k + 5 < n) stepf(k + 5, d1);
                 if (k + 6 < n) stepf(k + 6, d2);
@@ -563,16 +565,19 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
         __builtin_amdgcn_s_waitcnt(0xc07f);  // the chunk's output records are in LDS
         __builtin_amdgcn_wave_barrier();
         if (lane < n) {
+            // a constant-key chunk stored only the values (two rows), its key is the carried one
+            const float* fv = reinterpret_cast<const float*>(ob);
             const OneOut sx = ob[2 * lane], sy = ob[2 * lane + 1];
-            const unsigned kk = fastc ? K : sx.k;  // a constant-key chunk stores only the values
+            const float vx = fastc ? fv[lane] : sx.v, vy = fastc ? fv[64 + lane] : sy.v;
+            const unsigned kk = fastc ? K : sx.k;
             const int rank = (int)(kk >> kRankShift), root = (int)(kk & ((1u << kRankShift) - 1));
             RepVal* dst = w.Rv + lb + q - lane;
             if (lane == n - 1 && (finished || n < 64)) {  // the top's record (parent path) or a parked state
-                rv_publish(dst, sx.v, sy.v, rank, root, obb);
+                rv_publish(dst, vx, vy, rank, root, obb);
             } else {
                 RepVal o;
-                o.mx = sx.v;
-                o.my = sy.v;
+                o.mx = vx;
+                o.my = vy;
                 o.rank = rank;
                 o.root = root;
                 o.bb = obb;
@@ -838,7 +843,7 @@ __device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int 
 template <bool kLong, int kW>
 __global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigned epoch, int keyfast, int pipe) {
     __shared__ OneRec buf[kLong ? kW : 1][2][64];
-    __shared__ OneOut ob[kLong ? kW : 1][128];
+    __shared__ __attribute__((aligned(16))) OneOut ob[kLong ? kW : 1][128];
     const int lane = threadIdx.x & 63;
     const int wv = kLong ? (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
     const int nl = ctl[FC_NL];
