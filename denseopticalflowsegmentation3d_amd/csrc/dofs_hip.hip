@@ -2541,7 +2541,7 @@ __global__ __launch_bounds__(kDeepT) void k_krt_fused(Ws w, int* progress) {
 constexpr int kPreT = 1024, kPreK = kDeepTop / kPreT;
 static_assert(kPreK * kPreT == kDeepTop, "preorder sweep shape");
 constexpr int kPushLight = (int)0x80000000u;
-__global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w) {
+__global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w, int steps) {
     __shared__ int lpos[kDeepTop];
     const Dims& d = w.d;
     const int f = blockIdx.x;
@@ -2588,7 +2588,7 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w) {
     };
     if (nblk > 0) {
         load(nblk - 1, nd);
-        gather(nblk - 1);
+        if (steps) gather(nblk - 1);
     }
     for (int64_t blk = nblk - 1; blk >= 0; --blk) {
         const int64_t s0 = blk * kDeepTop, x0 = d.N + s0;
@@ -2631,20 +2631,22 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w) {
             // the merge's replay inputs at its position (KPathInit's step_in, the same record; random
             // 32-B stores, fire and forget): a top's path-top flag is its push's, a merge under an
             // in-block parent has its flag from the KRT epilogue
-            const bool ptop = top[k] ? (x == root || (pushed[k] & kPushLight)) : nd[k].lt != 0;
-            StepIn in;
-            if (l < d.N) {
-                in = step_in_leaf(nd[k].hl, ptop, nd[k].lB, l, lf[k], d.W);
-            } else {
-                in = step_in(w, f, pos[k], ptop, l, nd[k].lB, nd[k].hl);  // (a merge light child: no load)
+            if (steps) {
+                const bool ptop = top[k] ? (x == root || (pushed[k] & kPushLight)) : nd[k].lt != 0;
+                StepIn in;
+                if (l < d.N) {
+                    in = step_in_leaf(nd[k].hl, ptop, nd[k].lB, l, lf[k], d.W);
+                } else {
+                    in = step_in(w, f, pos[k], ptop, l, nd[k].lB, nd[k].hl);  // (a merge light child: no load)
+                }
+                w.In[lb + pos[k]] = in;
             }
-            w.In[lb + pos[k]] = in;
         }
         __syncthreads();  // the pushes are read by the blocks below
         if (blk > 0) {
 #pragma unroll
             for (int k = 0; k < kPreK; ++k) nd[k] = nx[k];
-            gather(blk - 1);
+            if (steps) gather(blk - 1);
         }
     }
 }
@@ -3122,10 +3124,12 @@ struct HipBackend {
             for (int t = 0; t < launches; ++t) launch(w.d.B, w.d.M, KJumpTop{w});
             launch(w.d.B, w.d.M, KOrdMerge{w});
         } else {
-            timed("k_pre_sweep", [&] { hipLaunchKernelGGL(k_pre_sweep, dim3((unsigned)w.d.B), dim3(kPreT), 0, stream, w); });
+            timed("k_pre_sweep", [&] {
+                hipLaunchKernelGGL(k_pre_sweep, dim3((unsigned)w.d.B), dim3(kPreT), 0, stream, w, pre_steps_on() ? 1 : 0);
+            });
             if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_pre_sweep launch");
         }
-        pre_steps_done = !w.jscatter;  // the sweep wrote every StepIn (KPathInit registers the paths only)
+        pre_steps_done = !w.jscatter && pre_steps_on();  // the sweep wrote every StepIn (KPathInit: paths only)
         launch(w.d.B, w.d.M, KLeafPos{w});
         return true;
     }
@@ -3138,6 +3142,11 @@ struct HipBackend {
     }
     static bool pre_jump(const Dims& d) { return d.B <= pre_jump_frames(); }
     bool pre_steps_done = false;  // the last pre_sweep wrote the StepIn records (k_pre_sweep)
+    // DOFS_PRE_STEPS=0: KPathInit writes the StepIn records instead of the preorder sweep (read per batch)
+    static bool pre_steps_on() {
+        const char* e = getenv("DOFS_PRE_STEPS");
+        return !(e && e[0] == '0');
+    }
     static bool pre_steps(const HipBackend& b) { return b.pre_steps_done; }
     void boruvka_relabel(const Ws& w, int r) {
         if (r >= 1 && rec_path(w) && relabel_tiles()) {  // round 0 runs before the tile flags exist

@@ -29,4 +29,7 @@ step flow4k_prof 300 env DOFS_SERIAL=1 DOFS_LIB=$P H=2160 W=3840 python tools/fl
 step flow4k_prof_nopipe 300 env DOFS_FLOW_PIPE=0 DOFS_SERIAL=1 DOFS_LIB=$P H=2160 W=3840 python tools/flow_stats.py 1 3
 step intraframe 300 python tools/bench_intraframe.py --model 4
 fi
+if [ -n "${KRT:-}" ]; then
+step krt_timing 300 env DOFS_LIB=denseopticalflowsegmentation3d_amd/_build/krt/libdofs_hip.so python tools/krt_timing.py 112 2
+fi
 exit 0
