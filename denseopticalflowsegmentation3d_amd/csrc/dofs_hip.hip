@@ -7,6 +7,7 @@
 // so a stale L1/L2 line can never be re-read forever (MI355X_MICROARCH.md §inter-workgroup visibility).
 #include <hip/hip_runtime.h>
 #include <type_traits>
+#include <utility>
 #include <hipcub/hipcub.hpp>
 
 #include <stdlib.h>
@@ -827,6 +828,32 @@ struct DeepShared {
     int wsum[kDeepT / 64];
 };
 
+// deep_block's 16-merge window pass: step J (merge J of the window) for every lane of each 16-lane row
+struct WinLanes {
+    int ca, cb, za, zb;  // the lane's endpoint labels and their component sizes
+    int p, L0;           // the lane's position in its window, the window's first merge label
+};
+template <int J>
+__device__ inline void win_step(WinLanes& v) {
+    constexpr int pat = 0x10 | (J << 5);  // ds_swizzle bitmask mode: lane (lane & 0x10) | J of each 32-lane half
+    const int sa = __builtin_amdgcn_ds_swizzle(v.ca, pat), sb = __builtin_amdgcn_ds_swizzle(v.cb, pat);
+    const int nz = __builtin_amdgcn_ds_swizzle(v.za, pat) + __builtin_amdgcn_ds_swizzle(v.zb, pat);
+    if (J < v.p) {
+        if (v.ca == sa || v.ca == sb) {
+            v.ca = v.L0 + J;
+            v.za = nz;
+        }
+        if (v.cb == sa || v.cb == sb) {
+            v.cb = v.L0 + J;
+            v.zb = nz;
+        }
+    }
+}
+template <int... J>
+__device__ inline void win_steps(WinLanes& v, std::integer_sequence<int, J...>) {
+    (win_step<J>(v), ...);
+}
+
 // all depths of one block [s0, s0 + cnt) (cnt <= kDeepS) of frame f, in LDS
 __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int cnt) {
     const Dims& d = w.d;
@@ -919,7 +946,8 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
         else
             lds_wait();
     };
-    for (int S = kDeepS; S >= 2; S >>= 1) {
+    const int s_last = w.deep_wave ? 32 : 2;  // the last depth of the LDS union-find form
+    for (int S = kDeepS; S >= s_last; S >>= 1) {
         const int half = S >> 1;
         // union (L edges of sub-blocks whose R half exists)
         for (int t = tid; t < cnt; t += kDeepT) {
@@ -977,6 +1005,35 @@ __device__ void deep_block(const Ws& w, DeepShared& sh, int f, int64_t s0, int c
         }
         depth_sync(S);
         KT(S >= 256 ? 9 : 10);  // the upper depths (S >= 256) and the lower ones
+    }
+    if (w.deep_wave) {
+        // The depths S <= 16 as one pass over each 16-merge window (one row of 16 lanes; thread tid holds
+        // merges tid and tid + kDeepT). After depth 32 a window's labels are the components' labels at
+        // the window start and belong to no other window. In rank order j, merge j joins the components
+        // whose labels its lane holds; every later lane of the window whose endpoint carries one of those
+        // two labels takes merge j's label and the sum of the two sizes. A lane stops updating at its own
+        // step, so after the pass it holds its merge's children (labels and sizes): the KRT children the
+        // four depths compute, without their unions and barriers. Row broadcasts by ds_swizzle (the LDS
+        // crossbar, no memory access): a wave-wide readlane loop over 64 lanes was VALU-bound (measured
+        // slower than the depths it replaced).
+        const int lane = tid & 63, p = lane & 15;
+#pragma unroll
+        for (int u = 0; u < kDeepS / kDeepT; ++u) {
+            const int t = tid + u * kDeepT;
+            const bool valid = t < cnt;
+            int ca = valid ? sh.lu[t] : -1, cb = valid ? sh.lv[t] : -1;
+            int za = valid ? sh.SZ[ca] : 0, zb = valid ? sh.SZ[cb] : 0;
+            WinLanes v{ca, cb, za, zb, p, kDeepK + t - p};  // merge j of the window: label L0 + j
+            win_steps(v, std::make_integer_sequence<int, 15>{});
+            ca = v.ca, cb = v.cb, za = v.za, zb = v.zb;
+            if (valid) {
+                sh.lu[t] = (short)ca;
+                sh.lv[t] = (short)cb;
+                sh.SZ[kDeepK + t] = za + zb;
+            }
+        }
+        lds_wait();  // a window's labels and sizes are read by its own wave only
+        KT(10);
     }
     // final labels (the edge's KRT children) as global ids: a local id below kDeepK was never
     // relabeled, so it is still the edge's own input label
@@ -2541,7 +2598,10 @@ __global__ __launch_bounds__(kDeepT) void k_krt_fused(Ws w, int* progress) {
 constexpr int kPreT = 1024, kPreK = kDeepTop / kPreT;
 static_assert(kPreK * kPreT == kDeepTop, "preorder sweep shape");
 constexpr int kPushLight = (int)0x80000000u;
-__global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w, int steps) {
+// steps: also the StepIn records (DOFS_PRE_STEPS); ordw: also the merges' ord[] entries (else KLeafPos
+// writes them, chip-wide after the sweep: random 4-byte stores from one CU are bound by its waves'
+// outstanding-store slots, not by bandwidth)
+__global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w, int steps, int ordw) {
     __shared__ int lpos[kDeepTop];
     const Dims& d = w.d;
     const int f = blockIdx.x;
@@ -2621,7 +2681,7 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w, int steps) {
             const int64_t x = x0 + t;
             if (!top[k]) pos[k] = jump_sum(nd[k].v) + lpos[jump_anc(nd[k].v) - x0];
             pre[x] = pos[k];  // (the converged word is not needed: nothing reads J after this pass)
-            ord[pos[k]] = (int)x;
+            if (ordw) ord[pos[k]] = (int)x;
             // push the merge children outside the block (tops of earlier blocks) their positions;
             // the leaves get theirs from KLeafPos, in parallel after the sweep
             const int sh = (int)(unsigned)(nd[k].hl & 0xffffffffu);
@@ -2703,12 +2763,15 @@ struct KOrdMerge {
 // the leaves' ord[] entries from their parents' positions (after k_pre_sweep): one lane per merge
 struct KLeafPos {
     Ws w;
+    bool merge_ord;  // also the merge's own ord[] entry (k_pre_sweep left them out)
     DOFS_HD void operator()(int f, int64_t k) const {
         const Dims& d = w.d;
         const int64_t lb = f * d.NL, e = f * d.M + k;
         const int a = w.lu[e], b = w.lv[e];
-        if (a >= d.N && b >= d.N) return;
+        if (!merge_ord && a >= d.N && b >= d.N) return;
         const int q = w.pre[lb + d.N + k];
+        if (merge_ord) w.ord[lb + q] = (int)(d.N + k);
+        if (a >= d.N && b >= d.N) return;
         const int sh = (int)(unsigned)(w.hls[e] & 0xffffffffu);
         const bool lB = w.hlB[e] != 0;
         const int h = lB ? a : b, l = lB ? b : a;
@@ -3078,8 +3141,10 @@ struct HipBackend {
             (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, device);
             const int cap = dev_cus;
             const int nwg = std::max(1, std::min(cap, extra < 0 ? cap : w.d.B + extra));
+            Ws wk = w;
+            wk.deep_wave = deep_wave_on() ? 1 : 0;
             timed("k_krt_fused", [&] {
-                hipLaunchKernelGGL(k_krt_fused, dim3((unsigned)nwg), dim3(kDeepT), 0, stream, w, w.ctr + C_PROG);
+                hipLaunchKernelGGL(k_krt_fused, dim3((unsigned)nwg), dim3(kDeepT), 0, stream, wk, w.ctr + C_PROG);
             });
             if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_krt_fused launch");
             fused_done = true;
@@ -3102,10 +3167,18 @@ struct HipBackend {
         const unsigned nb = (unsigned)((w.d.M + kDeepTop - 1) / kDeepTop);
         const int top = swept_top ? 0 : 1;  // DOFS_KRT_DNC: the global depths stop above the block
         swept_top = false;
+        Ws wk = w;
+        wk.deep_wave = deep_wave_on() ? 1 : 0;
         timed("k_dnc_deep", [&] {
-            hipLaunchKernelGGL(k_dnc_deep, dim3(nb, (unsigned)w.d.B), dim3(kDeepT), 0, stream, w, top);
+            hipLaunchKernelGGL(k_dnc_deep, dim3(nb, (unsigned)w.d.B), dim3(kDeepT), 0, stream, wk, top);
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_dnc_deep launch");
+    }
+    // DOFS_DEEP_WAVE=0: the LDS KRT's depths below 32 merges by the union-find depths instead of the
+    // one-pass window form (read per batch, for A/B runs on one library)
+    static bool deep_wave_on() {
+        const char* e = getenv("DOFS_DEEP_WAVE");
+        return !(e && e[0] == '0');
     }
     void boruvka_hook(const Ws& w, int r) {
         if (rec_path(w)) {
@@ -3125,12 +3198,13 @@ struct HipBackend {
             launch(w.d.B, w.d.M, KOrdMerge{w});
         } else {
             timed("k_pre_sweep", [&] {
-                hipLaunchKernelGGL(k_pre_sweep, dim3((unsigned)w.d.B), dim3(kPreT), 0, stream, w, pre_steps_on() ? 1 : 0);
+                hipLaunchKernelGGL(k_pre_sweep, dim3((unsigned)w.d.B), dim3(kPreT), 0, stream, w, pre_steps_on() ? 1 : 0,
+                                   pre_ord_on() ? 1 : 0);
             });
             if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_pre_sweep launch");
         }
         pre_steps_done = !w.jscatter && pre_steps_on();  // the sweep wrote every StepIn (KPathInit: paths only)
-        launch(w.d.B, w.d.M, KLeafPos{w});
+        launch(w.d.B, w.d.M, KLeafPos{w, !w.jscatter && !pre_ord_on()});
         return true;
     }
     // K4 by jumping (Ws::jscatter) for batches of at most `pre_jump_frames` frames (DOFS_PRE_JUMP = the
@@ -3142,12 +3216,19 @@ struct HipBackend {
     }
     static bool pre_jump(const Dims& d) { return d.B <= pre_jump_frames(); }
     bool pre_steps_done = false;  // the last pre_sweep wrote the StepIn records (k_pre_sweep)
-    // DOFS_PRE_STEPS=0: KPathInit writes the StepIn records instead of the preorder sweep (read per batch)
+    // DOFS_PRE_STEPS=1: the preorder sweep writes the StepIn records instead of KPathInit (read per batch).
+    // Off by default: B = 112, one library, same box, three runs each: sweep-written 1,584 / 1,591 /
+    // 1,588 Mpix/s (preorder stage 25.3 ms), KPathInit-written 1,591 / 1,592 / 1,591 (24.7 ms)
     static bool pre_steps_on() {
         const char* e = getenv("DOFS_PRE_STEPS");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }
     static bool pre_steps(const HipBackend& b) { return b.pre_steps_done; }
+    // DOFS_PRE_ORD=1: the preorder sweep writes the merges' ord[] entries (else KLeafPos; read per batch)
+    static bool pre_ord_on() {
+        const char* e = getenv("DOFS_PRE_ORD");
+        return e && e[0] == '1';
+    }
     void boruvka_relabel(const Ws& w, int r) {
         if (r >= 1 && rec_path(w) && relabel_tiles()) {  // round 0 runs before the tile flags exist
             rec_launch(w, r, k_boruvka_relabel_t, "k_boruvka_relabelt");

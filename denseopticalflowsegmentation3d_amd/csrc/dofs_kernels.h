@@ -131,6 +131,7 @@ struct Ws {
     int jscatter;   // HIP: the LDS KRT's epilogue writes its block's outside children's jump words and
                     // path-top flags (the chip-wide jumping preorder of small batches), else k_pre_sweep
     int pre_steps;  // HIP: k_pre_sweep wrote every merge's StepIn (KPathInit then registers the paths only)
+    int deep_wave;  // HIP: the LDS KRT's depths below 32 merges by one register pass per 16-merge window
     int single;     // HIP: EU / EV carry bit kSingleBit — the endpoint is a single pixel at this merge (the
                     // merge is its minimum incident edge, so its first in Kruskal order): the KRT sweep
                     // takes its label without a find
