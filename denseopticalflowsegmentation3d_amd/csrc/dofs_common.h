@@ -80,7 +80,8 @@ enum Counter {
     C_LONGM = 57,    // merges on long heavy paths (replayed by the wave-per-path kernel)
     C_FLOWERR = 58,  // frame 0 only: the dataflow replay gave up a bounded wait (results invalid)
     C_ROOTL = 59,    // 1 + position in list_long of the frame's root heavy path (0: the root path is short)
-    C_SORTFIX = 60   // frame 0 only, 3 counters: pairs the MST sort fix-up moved, its fallback flag, barrier
+    C_SORTFIX = 60,  // frame 0 only, 3 counters: pairs the MST sort fix-up moved, its fallback flag, barrier
+    C_BMAX = 63      // the frame's largest |blurred flow component| (float bits, atomicMax by the HIP blur)
 };
 
 constexpr uint32_t kNoEdge = 0xFFFFFFFFu;

@@ -803,7 +803,7 @@ __device__ inline int lds_union(int* P, const int* SZ, int a, int b) {
 // Measurement build only (-DDOFS_KRT_TIMING): thread 0 of each KRT workgroup adds the wall-clock time
 // (100 MHz counter) of each phase to g_kt[i] (read by dofs_debug_krt_timing; tools/krt_timing.py).
 #ifdef DOFS_KRT_TIMING
-__device__ unsigned long long g_kt[16];
+__device__ unsigned long long g_kt[20];
 #define KT_DECL unsigned long long kt_last = wall_clock64();
 #define KT(i)                                                  \
     do {                                                       \
@@ -2290,12 +2290,14 @@ __device__ __forceinline__ int uf_find_ro_halve(int* P, int x) {
         x = gp;
     }
 }
+// self: the chains run in comp itself (after k_boruvka_tile0: a pixel's root or a tile exit, an ancestor)
+template <bool kSelf = false>
 __global__ __launch_bounds__(256) void k_boruvka_relabel4(Ws w, int r) {
     const int f = blockIdx.y;
     if (!w.C(f)[C_ACT + r]) return;
     const int64_t N = w.d.N;
     int* comp = w.comp + f * N;
-    int* uf = w.uf + f * N;
+    int* uf = kSelf ? comp : w.uf + f * N;
     const Span4 sp = span4(comp, N);
     const int64_t step = (int64_t)gridDim.x * blockDim.x;
     const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2314,6 +2316,100 @@ __global__ __launch_bounds__(256) void k_boruvka_relabel4(Ws w, int r) {
         const int c = comp[p];
         const int root = uf_find_ro_halve(uf, c);
         if (root != c) comp[p] = root;
+    }
+}
+
+// Round 0's KBoruvkaPairs and the first half of its relabel, per 64 x 32 tile (DOFS_TILE0, default;
+// k_boruvka_relabel4 over comp finishes). KBoruvkaFirst left each pixel's pointer along its minimum edge
+// in uf: a forest whose only cycles are the mutual pairs, each rooted at its smaller pixel. The tile and a
+// 4-pixel halo are staged in LDS as cell pointers (a pointer goes to one of the eight neighbours, so only
+// a halo cell can point out of the region: then the cell keeps the target pixel, encoded negative). The
+// pairs are rooted (a pair leaving the region is checked in uf), then every cell finds its root or exit in
+// LDS with path halving — the min-edge chains are long, and a walk without compression costs the square
+// of a chain's length. A tile pixel's comp becomes its root, or the pixel its chain leaves the region by
+// (an ancestor): k_boruvka_relabel4 on comp then follows those tile hops to the roots. The pair's smaller
+// pixel roots itself in uf (the later rounds start their finds from the roots).
+constexpr int kT0X = 64, kT0Y = 32, kT0H = 4, kT0RX = kT0X + 2 * kT0H, kT0RY = kT0Y + 2 * kT0H;
+constexpr int kT0C = kT0RX * kT0RY, kT0T = 256, kT0K = (kT0C + kT0T - 1) / kT0T;  // cells per thread
+__global__ __launch_bounds__(kT0T) void k_boruvka_tile0(Ws w) {
+    __shared__ int U[kT0C];
+    const Dims& d = w.d;
+    const int f = blockIdx.y;
+    if (!w.C(f)[C_ACT + 0]) return;
+    const int W = d.W, H = d.H;
+    int* uf = w.uf + f * d.N;
+    int* comp = w.comp + f * d.N;
+    const int tx = (W + kT0X - 1) / kT0X, ty = (H + kT0Y - 1) / kT0Y;
+    const int tid = threadIdx.x;
+    for (int64_t bi = blockIdx.x; bi < (int64_t)tx * ty; bi += gridDim.x) {
+        const int bx = (int)(bi % tx) * kT0X - kT0H, by = (int)(bi / tx) * kT0Y - kT0H;  // region origin
+        // cell pointers: the target cell, the cell itself (no edge), -1 (outside the frame), or -(2 + target
+        // pixel) when the target lies outside the region
+#pragma unroll
+        for (int k = 0; k < kT0K; ++k) {
+            const int e = tid + k * kT0T;
+            if (e >= kT0C) break;
+            const int cx = e % kT0RX, cy = e / kT0RX, gx = bx + cx, gy = by + cy;
+            int v = -1;
+            if (gx >= 0 && gx < W && gy >= 0 && gy < H) {
+                const int g = gy * W + gx, t = uf[g];
+                const int dl = t - g, dy = dl > 1 ? 1 : (dl < -1 ? -1 : 0), dx = dl - dy * W;
+                const int nx = cx + dx, ny = cy + dy;
+                v = (nx >= 0 && nx < kT0RX && ny >= 0 && ny < kT0RY) ? ny * kT0RX + nx : -(2 + t);
+            }
+            U[e] = v;
+        }
+        __syncthreads();
+        // the pairs: the smaller pixel of a mutual pair becomes a root (decided on the staged pointers)
+        bool root[kT0K];
+#pragma unroll
+        for (int k = 0; k < kT0K; ++k) {
+            const int e = tid + k * kT0T;
+            root[k] = false;
+            if (e >= kT0C) continue;
+            const int v = U[e];
+            const int g = (by + e / kT0RX) * W + bx + e % kT0RX;
+            if (v >= 0 && v != e) {
+                const int t = (by + v / kT0RX) * W + bx + v % kT0RX;
+                root[k] = U[v] == e && g < t;
+            } else if (v <= -2) {
+                const int t = -(v + 2);
+                root[k] = g < t && uf[t] == g;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kT0K; ++k) {
+            const int e = tid + k * kT0T;
+            if (!root[k]) continue;
+            U[e] = e;
+            const int cx = e % kT0RX, cy = e / kT0RX;
+            if (cx >= kT0H && cx < kT0H + kT0X && cy >= kT0H && cy < kT0H + kT0Y)  // the tile's own pixel
+                uf[(by + cy) * W + bx + cx] = (by + cy) * W + bx + cx;
+        }
+        __syncthreads();
+        // finds in LDS with path halving (concurrent halving stores only ever point to an ancestor)
+        for (int e = tid; e < kT0C; e += kT0T) {
+            int x = e;
+            for (;;) {
+                const int y = U[x];
+                if (y < 0 || y == x) break;
+                const int z = U[y];
+                if (z < 0 || z == y) {
+                    x = y;
+                    break;
+                }
+                U[x] = z;
+                x = z;
+            }
+            const int cx = e % kT0RX, cy = e / kT0RX;
+            if (cx < kT0H || cx >= kT0H + kT0X || cy < kT0H || cy >= kT0H + kT0Y) continue;  // halo
+            const int gx = bx + cx, gy = by + cy;
+            if (gx >= W || gy >= H) continue;
+            const int y = U[x];  // x: the root cell, or the cell whose pointer leaves the region
+            comp[gy * W + gx] = y == x ? (by + x / kT0RX) * W + bx + x % kT0RX : -(y + 2);
+        }
+        __syncthreads();
     }
 }
 
@@ -2403,6 +2499,11 @@ __global__ __launch_bounds__(kBlurSeg) void k_blur_row(Ws w) {
     }
 }
 constexpr int kColW = 64, kColH = 64, kColT = 256;
+// one atomic per wave: the frame's largest |blurred component| (nonnegative float bits order as ints)
+__device__ inline void blur_max_out(const Ws& w, int f, int mb) {
+    mb = wave_reduce(mb, [](int x, int y) { return x > y ? x : y; });
+    if (wave_lane() == 0 && mb > 0) atomicMax(w.C(f) + C_BMAX, mb);
+}
 __global__ __launch_bounds__(kColT) void k_blur_col(Ws w) {
     __shared__ F2 buf[(kColH + 2 * kBlurR) * kColW];
     const int W = w.d.W, H = w.d.H;
@@ -2411,6 +2512,7 @@ __global__ __launch_bounds__(kColT) void k_blur_col(Ws w) {
     const int r = w.bn / 2;
     const F2* src = w.tmp + f * w.d.N;
     const int cx = threadIdx.x % kColW, cg = threadIdx.x / kColW;  // column, row group
+    int mb = 0;  // the largest |component| written (float bits): the frame's C_BMAX (key32_etop)
     for (int64_t bi = blockIdx.x; bi < (int64_t)tx * ty; bi += gridDim.x) {
         const int x0 = (int)(bi % tx) * kColW, y0 = (int)(bi / tx) * kColH;
         const int x = x0 + cx;
@@ -2434,10 +2536,12 @@ __global__ __launch_bounds__(kColT) void k_blur_col(Ws w) {
                 o.x = sx;
                 o.y = sy;
                 w.blur[f * w.d.N + (int64_t)y * W + x] = o;
+                mb = max(mb, max(__float_as_int(fabsf(sx)), __float_as_int(fabsf(sy))));
             }
         }
         __syncthreads();
     }
+    blur_max_out(w, f, mb);
 }
 
 // K1 in one pass (the blur radius of the reference's sigma = 3: 25 taps): per 64 x 32 output tile the
@@ -2461,6 +2565,7 @@ __global__ __launch_bounds__(kFbT) void k_blur_fused(Ws w) {
 #pragma unroll
     for (int t = 0; t <= 2 * kFbR; ++t) k[t] = w.bk[t];
     constexpr int kLd = (kFbRH * kFbIW + kFbT - 1) / kFbT;  // staged elements per lane
+    int mb = 0;  // the largest |component| written (float bits): the frame's C_BMAX (key32_etop)
     for (int64_t bi = blockIdx.x; bi < (int64_t)tx * ty; bi += gridDim.x) {
         const int x0 = (int)(bi % tx) * kFbW, y0 = (int)(bi / tx) * kFbH;
         // every lane's loads issued before any is stored (one memory wait per tile); reflect-101 by
@@ -2525,12 +2630,16 @@ __global__ __launch_bounds__(kFbT) void k_blur_fused(Ws w) {
                     F2 out;
                     out.x = sx;
                     out.y = sy;
-                    if (y < H) dst[(int64_t)y * W + x] = out;
+                    if (y < H) {
+                        dst[(int64_t)y * W + x] = out;
+                        mb = max(mb, max(__float_as_int(fabsf(sx)), __float_as_int(fabsf(sy))));
+                    }
                 }
             }
         }
         __syncthreads();
     }
+    blur_max_out(w, f, mb);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2650,6 +2759,7 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w, int steps, int ordw) 
         load(nblk - 1, nd);
         if (steps) gather(nblk - 1);
     }
+    KT_DECL
     for (int64_t blk = nblk - 1; blk >= 0; --blk) {
         const int64_t s0 = blk * kDeepTop, x0 = d.N + s0;
         const int cnt = (int)((d.M - s0) < kDeepTop ? (d.M - s0) : kDeepTop);
@@ -2674,6 +2784,7 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w, int steps, int ordw) 
             w.lite[lb + x0 + t] = x0 + t == root || (pushed[k] & kPushLight) ? 1 : 0;
         }
         lds_barrier();
+        KT(14);
 #pragma unroll
         for (int k = 0; k < kPreK; ++k) {
             const int t = tid + k * kPreT;
@@ -2702,12 +2813,14 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w, int steps, int ordw) 
                 w.In[lb + pos[k]] = in;
             }
         }
+        KT(15);
         __syncthreads();  // the pushes are read by the blocks below
         if (blk > 0) {
 #pragma unroll
             for (int k = 0; k < kPreK; ++k) nd[k] = nx[k];
             if (steps) gather(blk - 1);
         }
+        KT(16);
     }
 }
 
@@ -2761,17 +2874,18 @@ struct KOrdMerge {
 };
 
 // the leaves' ord[] entries from their parents' positions (after k_pre_sweep): one lane per merge
+// (a merge's own ord[] entry only has to say "a merge": ord is read for leaf pixels and tested >= N —
+// KLeafOrder, the leaf scan, the replay's path starts — so the merges' positions get one coalesced fill,
+// kOrdMerge, instead of a random store each)
+constexpr int kOrdMerge = 0x7FFFFFFF;
 struct KLeafPos {
     Ws w;
-    bool merge_ord;  // also the merge's own ord[] entry (k_pre_sweep left them out)
     DOFS_HD void operator()(int f, int64_t k) const {
         const Dims& d = w.d;
         const int64_t lb = f * d.NL, e = f * d.M + k;
         const int a = w.lu[e], b = w.lv[e];
-        if (!merge_ord && a >= d.N && b >= d.N) return;
-        const int q = w.pre[lb + d.N + k];
-        if (merge_ord) w.ord[lb + q] = (int)(d.N + k);
         if (a >= d.N && b >= d.N) return;
+        const int q = w.pre[lb + d.N + k];
         const int sh = (int)(unsigned)(w.hls[e] & 0xffffffffu);
         const bool lB = w.hlB[e] != 0;
         const int h = lB ? a : b, l = lB ? b : a;
@@ -3204,7 +3318,10 @@ struct HipBackend {
             if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_pre_sweep launch");
         }
         pre_steps_done = !w.jscatter && pre_steps_on();  // the sweep wrote every StepIn (KPathInit: paths only)
-        launch(w.d.B, w.d.M, KLeafPos{w, !w.jscatter && !pre_ord_on()});
+        if (!w.jscatter && !pre_ord_on())  // the merges' ord entries: the merge mark, one fill (KLeafPos)
+            note(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.ord), kOrdMerge, (size_t)w.d.B * w.d.NL, stream),
+                 "hipMemsetD32Async");
+        launch(w.d.B, w.d.M, KLeafPos{w});
         return true;
     }
     // K4 by jumping (Ws::jscatter) for batches of at most `pre_jump_frames` frames (DOFS_PRE_JUMP = the
@@ -3234,8 +3351,28 @@ struct HipBackend {
             rec_launch(w, r, k_boruvka_relabel_t, "k_boruvka_relabelt");
             return;
         }
-        pixel4(w, r, k_boruvka_relabel4, "KBoruvkaRelabelFind");
+        if (r == 0 && tile0_on() && w.d.W >= 3) {  // KBoruvkaPairs + the relabel's in-tile part, then tile hops
+            const int64_t tiles = (int64_t)((w.d.W + kT0X - 1) / kT0X) * ((w.d.H + kT0Y - 1) / kT0Y);
+            const int64_t cap = std::max<int64_t>(1, (grid_cap() > 0 ? grid_cap() : 8192) / w.d.B);
+            timed("k_boruvka_tile0", [&] {
+                hipLaunchKernelGGL(k_boruvka_tile0, dim3((unsigned)std::min(tiles, cap), (unsigned)w.d.B), dim3(kT0T), 0,
+                                   stream, w);
+            });
+            if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_boruvka_tile0 launch");
+            pixel4(w, r, k_boruvka_relabel4<true>, "KBoruvkaRelabelFind");
+            return;
+        }
+        pixel4(w, r, k_boruvka_relabel4<false>, "KBoruvkaRelabelFind");
     }
+    // DOFS_TILE0=0: round 0 by KBoruvkaPairs + k_boruvka_relabel4 over uf (else k_boruvka_tile0 + hops)
+    static bool tile0_on() {
+        static const bool on = [] {
+            const char* e = getenv("DOFS_TILE0");
+            return !(e && e[0] == '0');
+        }();
+        return on;
+    }
+    static bool pairs_in_relabel(const Ws& w) { return tile0_on() && w.d.W >= 3; }
     static bool relabel_tiles() {  // DOFS_RELABEL_TILES=0: every pixel every round (k_boruvka_relabel4)
         static const bool on = [] {
             const char* e = getenv("DOFS_RELABEL_TILES");
@@ -3531,6 +3668,7 @@ struct HipBackend {
     }
     // Kruskal order of each frame's MST edges into w.val_out (values of frame f at [f n, (f + 1) n)).
     // Packed: w.EU (written later by KEdgeInit) is the scratch between the two passes.
+    static int sort_k32() { return g_sort_k32; }  // KMstEmit's 32-bit keys for the packed sort (0: 64-bit)
     void sort_mst(Ws& w, int64_t n, int nf, int value_bits, bool packed) {
         if (!packed) {
             sort_pairs(w.key_in, w.key_out, w.val_in, w.val_out, n, nf, value_bits);
@@ -3538,6 +3676,28 @@ struct HipBackend {
         }
         const int fb = frame_bits(nf);
         const int tot = (int)(n * nf);
+        if (g_sort_k32 > 0) {  // 32-bit keys (dofs_sortfix.h): four digits of (u32, u32) pairs, then the fix-up
+            const unsigned* k32_in = reinterpret_cast<const unsigned*>(w.key_in);
+            unsigned* k32_out = reinterpret_cast<unsigned*>(w.key_out);
+            unsigned* vmid = reinterpret_cast<unsigned*>(w.EU);
+            size_t b1 = 0, b2 = 0;
+            note(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, k32_in, k32_out, w.val_in, vmid, tot, 0, 32, stream),
+                 "sort size");
+            note(hipcub::DeviceRadixSort::SortKeys(nullptr, b2, vmid, w.val_out, tot, value_bits, value_bits + fb, stream),
+                 "sort size");
+            void* t = temp(std::max(b1, b2));
+            note(hipcub::DeviceRadixSort::SortPairs(t, b1, k32_in, k32_out, w.val_in, vmid, tot, 0, 32, stream), "sort");
+            if (g_sort_fix) sort_fixup32(w, vmid, tot, value_bits);
+            if (g_sort_dump[0]) {  // diagnosis: 32-bit keys (4 bytes each) and values after the fix-up
+                const size_t m = (size_t)std::min<int64_t>(tot, g_sort_dump_cap);
+                note(hipMemcpyAsync(g_sort_dump[0], k32_out, 4 * m, hipMemcpyDeviceToDevice, stream), "dump");
+                note(hipMemcpyAsync(g_sort_dump[1], vmid, 4 * m, hipMemcpyDeviceToDevice, stream), "dump");
+                g_sort_dump[0] = g_sort_dump[1] = nullptr;
+            }
+            note(hipcub::DeviceRadixSort::SortKeys(t, b2, vmid, w.val_out, tot, value_bits, value_bits + fb, stream),
+                 "sort frames");
+            return;
+        }
         const int cut = g_sort_cut;
         unsigned* vmid = reinterpret_cast<unsigned*>(w.EU);
         size_t b1 = 0, b2 = 0;
@@ -3561,6 +3721,27 @@ struct HipBackend {
         }
         note(hipcub::DeviceRadixSort::SortKeys(t, b2, vmid, w.val_out, tot, value_bits, value_bits + fb, stream),
              "sort frames");
+    }
+    // dofs_sortfix.h, 32-bit keys: the mixed groups sorted by (recomputed full key, value); key_in / val_in
+    // (dead after the pair sort) the scratch, key_out's storage the fallback's full keys
+    void sort_fixup32(Ws& w, unsigned* vmid, int64_t tot, int vb) {
+        SortFix32 s{reinterpret_cast<const unsigned*>(w.key_out), vmid, w.key_out, w.key_in, w.val_in, w.blur, w.d,
+                    vb, w.single ? 0x3FFFFFFFu : ~0u, w.ctr + C_SORTFIX, tot};
+        const int64_t cap = grid_cap() > 0 ? grid_cap() : 8192;
+        const unsigned gx = (unsigned)std::min<int64_t>((tot + kFixBlock - 1) / kFixBlock, cap);
+        int lgs = 0;
+        while (((int64_t)1 << lgs) < tot) ++lgs;
+        lgs += lgs & 1;  // an even number of merge passes ends in (k64, vmid)
+        timed("k_sortfix", [&] {
+            hipLaunchKernelGGL(k_sortfix32_local, dim3(gx), dim3(kFixBlock), 0, stream, s);
+            int cus = 256;
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+            // the fallback (both return at once unless the flag is up): full keys, then the merge sort
+            hipLaunchKernelGGL(k_sortfix32_keys, dim3(2 * cus), dim3(kFixBlock), 0, stream, s);
+            hipLaunchKernelGGL(k_sortfix_merge, dim3(2 * cus), dim3(kFixBlock), 0, stream,
+                               SortFix{w.key_out, vmid, w.key_in, w.val_in, w.ctr + C_SORTFIX, tot, 1}, lgs);
+        });
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "sort fix-up launch");
     }
     // dofs_sortfix.h: the groups of equal truncated keys sorted by the full key (val_out, written by the
     // frame pass next, holds the lists; key_in / val_in, dead after the pair sort, the scratch)
@@ -3587,12 +3768,12 @@ struct HipBackend {
 #ifdef DOFS_KRT_TIMING
 // Measurement build only: the KRT phase times accumulated since the last call (microseconds), then reset.
 extern "C" int dofs_debug_krt_timing(double* out_us, int n) {
-    unsigned long long v[16] = {0};
+    unsigned long long v[20] = {0};
     if (hipMemcpyFromSymbol(v, HIP_SYMBOL(dofs::g_kt), sizeof(v)) != hipSuccess) return -1;
-    const unsigned long long z[16] = {0};
+    const unsigned long long z[20] = {0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(dofs::g_kt), z, sizeof(z));
-    for (int i = 0; i < n && i < 16; ++i) out_us[i] = (double)v[i] / 100.0;  // 100 MHz wall clock
-    return 16;
+    for (int i = 0; i < n && i < 20; ++i) out_us[i] = (double)v[i] / 100.0;  // 100 MHz wall clock
+    return 20;
 }
 #endif
 
@@ -3603,6 +3784,14 @@ extern "C" int dofs_debug_krt_timing(double* out_us, int n) {
 extern "C" int dofs_debug_sort_cut(int cut) {
     const int old = dofs::g_sort_cut;
     if (cut >= 0 && cut <= 48) dofs::g_sort_cut = cut;
+    return old;
+}
+// Test knob: the mantissa bits of the packed sort's 32-bit keys (dofs_sortfix.h), 4 .. 30, or 0 for the
+// 64-bit keys (then dofs_debug_sort_cut applies); m < 0 only reads it. Returns the previous value.
+// Few bits make long mixed groups: the fallback's test.
+extern "C" int dofs_debug_sort_k32(int m) {
+    const int old = dofs::g_sort_k32;
+    if (m == 0 || (m >= 4 && m <= 30)) dofs::g_sort_k32 = m;
     return old;
 }
 // Diagnosis only: fix-up on / off (the truncated order is not Kruskal's: results differ), and a copy of

@@ -180,6 +180,23 @@ DOFS_HD inline unsigned long long dbits(double w) {
     c.d = w;
     return c.u;
 }
+// The 32-bit Kruskal sort key of a weight key (HIP batch sort, dofs_sortfix.h): m mantissa bits below a
+// (32 - m)-bit exponent offset inside the window of 2^(32 - m) binades that ends at etop, the biased
+// double exponent bound of every weight of the frame. Monotone non-decreasing in the 64-bit key read as
+// unsigned: below the window (zero included) 0; above it, or a set sign bit, the largest key.
+DOFS_HD inline unsigned key32_of(unsigned long long k, int etop, int m) {
+    if (k >> 63) return 0xFFFFFFFFu;
+    const int e = (int)((k >> 52) & 0x7FF), lo = etop - ((1 << (32 - m)) - 1);
+    if (e > etop) return 0xFFFFFFFFu;
+    if (e < lo) return 0u;
+    return ((unsigned)(e - lo) << m) | (unsigned)((k >> (52 - m)) & ((1ull << m) - 1));
+}
+// etop from a frame's largest |blurred component| M (float bits, C_BMAX): |dx|, |dy| <= 2M after the float
+// subtraction, so a weight is at most 2 sqrt(2) M < 4 M: its double exponent is at most M's + 2
+DOFS_HD inline int key32_etop(int mbits) {
+    const int fe = (mbits >> 23) & 0xFF;
+    return (fe > 0 ? fe : 1) - 127 + 1023 + 2;
+}
 DOFS_HD inline double bitsd(unsigned long long u) {
     union {
         double d;
@@ -585,10 +602,12 @@ constexpr int kEndMask = (1 << kSingleBit) - 1;
 struct KMstEmit {
     Ws w;
     int fshift;  // > 0: the frame id rides above the emission index (one batch-wide frame sort, HIP)
+    int k32m = 0;  // > 0: 32-bit keys (key32_of, this many mantissa bits) into key_in's first half (HIP)
     DOFS_HD void operator()(int f, int64_t p) const {
         const Dims& d = w.d;
         const int bits = (int)mst_bits(w.mstbits[f * d.N + p]);
         if (!bits) return;
+        const int etop = k32m ? key32_etop(w.C(f)[C_BMAX]) : 0;
         int64_t j = w.off[f * d.N + p];
         const F2* b = w.blur + f * d.N;
         // the flow of p and of its MST edges' far ends read together (an unused slot re-reads p)
@@ -608,7 +627,11 @@ struct KMstEmit {
             if (!(bits & (1 << k))) continue;
             if (j < d.M) {
                 const double dx = bp.x - bq[k].x, dy = bp.y - bq[k].y;  // edge_weight(b, p, q)
-                w.key_in[f * d.M + j] = dbits(sqrt(sq_len(dx, dy)));
+                const unsigned long long key = dbits(sqrt(sq_len(dx, dy)));
+                if (k32m)
+                    reinterpret_cast<unsigned*>(w.key_in)[f * d.M + j] = key32_of(key, etop, k32m);
+                else
+                    w.key_in[f * d.M + j] = key;
                 // p's first merge is its minimum edge (slot k); the far end receives this edge in its slot 4 + k
                 const unsigned sg = (ms == (unsigned)k ? kValSingleS : 0u) | (mq[k] == (unsigned)(4 + k) ? kValSingleE : 0u);
                 w.val_in[f * d.M + j] = (unsigned)(4 * p + k) | (fshift ? (unsigned)f << fshift : 0u) | sg;

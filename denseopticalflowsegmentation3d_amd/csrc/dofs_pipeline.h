@@ -247,7 +247,7 @@ struct Pipeline {
         for (int r = 0; r < R; ++r) {
             if (r == 0) {  // every pixel hooks along its minimum edge (a forest of pointers)
                 be.launch(B, N, KBoruvkaFirst{w});
-                be.launch(B, N, KBoruvkaPairs{w});
+                if (!be.pairs_in_relabel(w)) be.launch(B, N, KBoruvkaPairs{w});  // (HIP: k_boruvka_tile0)
             } else {
                 be.boruvka_min(w, r, 0);  // KBoruvkaMinW (HIP: workgroup-aggregated per tile)
                 be.boruvka_min(w, r, 1);  // KBoruvkaMinI
@@ -321,7 +321,9 @@ struct Pipeline {
         // the whole batch at once the frame id rides above the index bits and key_out is not per frame
         const int vb = ceil_log2(4 * N);
         const bool packed = be.mst_packed(M, B, vb);
-        be.launch(B, N, KMstEmit{w, packed ? vb : 0});
+        KMstEmit em{w, packed ? vb : 0};
+        em.k32m = packed ? Backend::sort_k32() : 0;  // 32-bit sort keys (HIP batch sort, dofs_sortfix.h)
+        be.launch(B, N, em);
         be.sort_mst(w, M, B, vb, packed);
         keys_by_frame = !packed;
         vmask = vb >= 32 ? ~0u : (1u << vb) - 1u;

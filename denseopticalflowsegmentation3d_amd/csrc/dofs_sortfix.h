@@ -204,3 +204,163 @@ __global__ __launch_bounds__(kFixBlock) void k_sortfix_merge(SortFix s, int lgs)
         __syncthreads();
     }
 }
+
+// ---------------------------------------------------------------------------------------------
+// The default batch sort: 32-bit keys (key32_of, dofs_kernels.h) — a window of 2^(32 - m) binades below
+// the frame's weight bound (from its largest blurred component, C_BMAX) with m = 27 mantissa bits, the
+// precision of cut 24 in half the key bytes: four 8-bit digits of (u32 key, u32 value) pairs instead of
+// five of (u64, u32). key32_of is monotone, so the stable pair sort is exact except inside mixed groups
+// (equal 32-bit keys, different weights), which the fix-up below sorts by (full key, value) as above.
+// The full keys are not stored: a pair's weight is recomputed from its value (frame, pixel p, edge slot
+// k) and the blurred field, by the expression KMstEmit used (edge_weight), for the tied positions only.
+// A group's 32-bit keys are equal, so only values move. Weights below the window (zero included) share
+// key 0 and weights above it (none for finite flows) the largest key: a long mixed group there takes
+// the fallback — slower, never wrong.
+// host: mantissa bits of the 32-bit keys (0: the 64-bit keys and g_sort_cut); DOFS_SORT_K32 sets the
+// start value (A/B runs on one library)
+inline int g_sort_k32 = [] {
+    const char* e = getenv("DOFS_SORT_K32");
+    const int m = e ? atoi(e) : 27;
+    return m == 0 || (m >= 4 && m <= 30) ? m : 27;
+}();
+
+struct SortFix32 {
+    const unsigned* key;      // sorted 32-bit keys (key_out's first half; never permuted)
+    unsigned* val;            // their values (the packed sort's middle buffer), permuted in place
+    unsigned long long* k64;  // the fallback's full keys (key_out's storage, 8 bytes per pair)
+    unsigned long long* k2;   // scratch (key_in's storage): the scalar path's keys, the fallback's ping-pong
+    unsigned* v2;
+    const F2* blur;  // the batch's blurred fields (frame stride d.N)
+    Dims d;
+    int vb;       // value bits: the frame id above, the emission index 4 p + k below
+    unsigned vm;  // the frame and index bits of a value (below the singleton flags when Ws::single)
+    int* ctr;     // as SortFix::ctr
+    int64_t n;
+};
+
+// A group is a run of equal 32-bit keys of one frame: the pair sort is stable and its input frame-major, so
+// a run of equal keys holds each frame's pairs contiguously, and only the order within a frame matters
+// (the frame pass that follows separates the frames stably). Most ties of a 112-frame batch are across
+// frames (the frames share weight values) and need no full key.
+__device__ inline unsigned fix_frame(const SortFix32& s, unsigned v) { return (v & s.vm) >> s.vb; }
+
+// the full 64-bit key of a value (KMstEmit's weight of the MST edge (p, slot k) of its frame)
+__device__ inline unsigned long long fix_full(const SortFix32& s, unsigned v) {
+    v &= s.vm;
+    const int64_t f = v >> s.vb;
+    const unsigned idx = v & ((1u << s.vb) - 1u);
+    const int64_t p = idx >> 2;
+    return dbits(edge_weight(s.blur + f * s.d.N, p, edge_end(s.d, p, (int)(idx & 3))));
+}
+
+// the scalar path of one tied group [p, ...) whose first full key is b: its full keys go to k2 (the group's
+// range only), then an insertion sort of (k2, val) — at most kFixScan positions, in place
+__device__ inline int fix32_group_scalar(const SortFix32& s, int64_t p, unsigned T, unsigned F, unsigned long long b) {
+    int64_t e = p + 1;
+    bool mixed = false;
+    s.k2[p] = b;
+    while (e < s.n && e - p < kFixScan) {
+        const unsigned ve = s.val[e];
+        if (s.key[e] != T || fix_frame(s, ve) != F) break;
+        const unsigned long long k = fix_full(s, ve);
+        s.k2[e] = k;
+        mixed |= k != b;
+        ++e;
+    }
+    if (!mixed) return 0;  // exact ties (or a long group's first kFixScan: its mixed pairs further on flag)
+    if (e < s.n && s.key[e] == T && fix_frame(s, s.val[e]) == F) {  // longer than kFixScan and mixed: the fallback
+        dofs_st(s.ctr + 1, 1);
+        return 0;
+    }
+    int moved = 0;
+    for (int64_t i = p + 1; i < e; ++i) {
+        const unsigned long long k = s.k2[i];
+        const unsigned v = s.val[i];
+        int64_t j = i;
+        while (j > p && fix_less(k, v, s.k2[j - 1], s.val[j - 1])) {
+            s.k2[j] = s.k2[j - 1];
+            s.val[j] = s.val[j - 1];
+            --j;
+        }
+        if (j != i) {
+            s.k2[j] = k;
+            s.val[j] = v;
+            moved += (int)(i - j) + 1;
+        }
+    }
+    return moved;
+}
+
+// k_sortfix_local on 32-bit keys: groups are runs of equal 32-bit keys; a wave without a tie exits after
+// one ballot, and only tied positions recompute their full keys
+__global__ __launch_bounds__(kFixBlock) void k_sortfix32_local(SortFix32 s) {
+    const int lane = wave_lane();
+    const int64_t nw = (int64_t)gridDim.x * (kFixBlock / 64);
+    int moved = 0;
+    for (int64_t wv = (int64_t)blockIdx.x * (kFixBlock / 64) + threadIdx.x / 64; wv * 64 < s.n; wv += nw) {
+        const int64_t base = wv * 64, p = base + lane;
+        const bool valid = p < s.n;
+        const unsigned T = valid ? s.key[p] : 0u;
+        unsigned ta = __shfl_up(T, 1, 64), tc = __shfl_down(T, 1, 64);
+        if (lane == 0 && valid && p >= 1) ta = s.key[p - 1];
+        if (lane == 63 && p + 1 < s.n) tc = s.key[p + 1];
+        if (!__ballot((valid && p >= 1 && ta == T) || (valid && p + 1 < s.n && tc == T))) continue;  // no tie
+        // ties of the 32-bit key: a group also needs the same frame
+        const unsigned v = valid ? s.val[p] : 0u;
+        const unsigned F = fix_frame(s, v);
+        unsigned fa = __shfl_up(F, 1, 64), fc = __shfl_down(F, 1, 64);
+        if (lane == 0 && valid && p >= 1 && ta == T) fa = fix_frame(s, s.val[p - 1]);
+        if (lane == 63 && p + 1 < s.n && tc == T) fc = fix_frame(s, s.val[p + 1]);
+        const bool same_prev = valid && p >= 1 && ta == T && fa == F;
+        const bool same_next = valid && p + 1 < s.n && tc == T && fc == F;
+        if (!__ballot(same_prev || same_next)) continue;  // ties across frames only
+        const bool tied = same_prev || same_next;
+        const unsigned long long b = tied ? fix_full(s, v) : 0ull;
+        unsigned long long a = __shfl_up(b, 1, 64);
+        if (lane == 0 && same_prev) a = fix_full(s, s.val[p - 1]);
+        const unsigned long long mix = __ballot(same_prev && a != b);  // mixed pairs (lane - 1, lane)
+        const bool tail_open = __shfl(same_next ? 1 : 0, 63, 64) != 0;  // a group runs into the next wave
+        if (!mix && !tail_open) continue;
+        const unsigned long long heads = __ballot(!same_prev);
+        const unsigned long long upto = lane == 63 ? ~0ull : (2ull << lane) - 1ull;
+        const unsigned long long below = heads & upto, above = heads & ~upto;
+        const bool left_open = below == 0;
+        const int gs = left_open ? 0 : 63 - __clzll(below);
+        const int ge = above ? __ffsll((long long)above) - 1 : 64;
+        const bool right_open = above == 0 && tail_open;
+        const int g = ge - gs;
+        const unsigned long long gmask = (ge == 64 ? ~0ull : (1ull << ge) - 1ull) & ~((1ull << gs) - 1ull);
+        const bool fast = valid && !left_open && !right_open && g >= 2 && g <= kFixWin && (mix & gmask);
+        const int gmax = wave_reduce(fast ? g : 0, [](int x, int y) { return x > y ? x : y; });
+        if (gmax) {
+            int rank = 0;
+            for (int dd = 0; dd < gmax; ++dd) {
+                const int j = (gs + dd) & 63;
+                const unsigned long long kj = __shfl(b, j, 64);
+                const unsigned vj = __shfl(v, j, 64);
+                rank += (fast && dd < g && j != lane && fix_less(kj, vj, b, v)) ? 1 : 0;
+            }
+            if (fast && gs + rank != lane) {  // the group's keys are equal: only the value moves
+                s.val[base + gs + rank] = v;
+                ++moved;
+            }
+        }
+        if (!valid || fast || (!left_open && !right_open && !(mix & gmask))) continue;  // done, or exact ties
+        if (!same_prev) {
+            moved += fix32_group_scalar(s, p, T, F, b);
+        } else if (a != b) {  // a mixed pair of a scalar-path group: inside its sorter's window?
+            if (p >= kFixScan && s.key[p - kFixScan] == T && fix_frame(s, s.val[p - kFixScan]) == F)
+                dofs_st(s.ctr + 1, 1);
+        }
+    }
+    const int tot = wave_reduce(moved, [](int x, int y) { return x + y; });
+    if (tot && lane == 0) dofs_aadd(s.ctr, tot);
+}
+
+// fallback only (returns at once when the flag is clear): every position's full key into k64, for
+// k_sortfix_merge over (k64, val)
+__global__ __launch_bounds__(kFixBlock) void k_sortfix32_keys(SortFix32 s) {
+    if (!dofs_ld(s.ctr + 1)) return;
+    const int64_t step = (int64_t)gridDim.x * kFixBlock;
+    for (int64_t p = (int64_t)blockIdx.x * kFixBlock + threadIdx.x; p < s.n; p += step) s.k64[p] = fix_full(s, s.val[p]);
+}

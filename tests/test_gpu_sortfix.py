@@ -1,5 +1,8 @@
 """GPU: the batch MST sort on truncated keys + its fix-up (csrc/dofs_sortfix.h) gives the full-key order.
 
+Both key forms: the 64-bit keys cut at a bit, and the default 32-bit keys (key32_of: a window of binades
+below the frame's weight bound, m mantissa bits) whose fix-up recomputes the full weights.
+
 Kruskal's order is the stable order of the 64-bit weight keys (segment.cpp:68). The batch sort keeps the
 top 64 - cut bits and the fix-up re-sorts every run of equal truncated keys holding different weights.
 Each cut's per-merge event records (Kruskal order) must equal those of the full 64-bit sort (cut 0),
@@ -19,12 +22,16 @@ H, W, B = 180, 320, 4
 C_SORTFIX = 60  # dofs_common.h: frame 0 fix-up counters (groups sorted locally, fallback flag)
 
 
-def _run(gpu, calib, flows, cut):
+def _run(gpu, calib, flows, cut, k32=0):
+    """One batch with the 64-bit keys cut at `cut` (k32 = 0) or the 32-bit keys of k32 mantissa bits."""
     import torch
     lib = gpu.lib
     lib.dofs_debug_sort_cut.argtypes = [C.c_int]
     lib.dofs_debug_sort_cut.restype = C.c_int
+    lib.dofs_debug_sort_k32.argtypes = [C.c_int]
+    lib.dofs_debug_sort_k32.restype = C.c_int
     old = lib.dofs_debug_sort_cut(cut)
+    old_k = lib.dofs_debug_sort_k32(k32)
     try:
         sh = torch.cuda.current_stream().cuda_stream
         gpu.segment_batch_device(flows.data_ptr(), B, H, W, *calib, params=params(300, 8), stream=sh)
@@ -34,6 +41,7 @@ def _run(gpu, calib, flows, cut):
         ctr = gpu.batch_counters(B)[0, C_SORTFIX:C_SORTFIX + 2].copy()
     finally:
         lib.dofs_debug_sort_cut(old)
+        lib.dofs_debug_sort_k32(old_k)
     return ev, labels, ctr
 
 
@@ -58,6 +66,18 @@ def test_truncated_sort_matches_full(gpu, calib):
     assert seen[24][0] > 0 and seen[24][1] == 0  # mixed groups sorted by the local pass, no fallback
     assert seen[32][0] > seen[24][0]
     assert seen[48][1] == 1  # 16-bit keys: mixed groups longer than kFixScan, the fallback merge sort
+    # the default 32-bit keys (key32_of): 27 mantissa bits, then fewer, down to the fallback's
+    seen = {}
+    for m in (27, 20, 12, 6):
+        ev, lab, ctr = _run(gpu, calib, flows, 0, m)
+        seen[m] = ctr.tolist()
+        for f in range(B):
+            for name in ev0[f].dtype.names:
+                assert np.array_equal(ev[f][name], ev0[f][name]), (m, f, name)
+            assert np.array_equal(lab[f], lab0[f]), (m, f)
+    assert seen[27][1] == 0 and seen[20][1] == 0
+    assert seen[20][0] >= seen[27][0] and seen[12][0] > seen[27][0]
+    assert seen[6][1] == 1  # 6 mantissa bits: mixed groups beyond kFixScan, the fallback
 
 
 def _fixup(lib, keys, vals, cut):

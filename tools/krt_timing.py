@@ -25,13 +25,13 @@ sh = torch.cuda.current_stream(dev).cuda_stream
 runtime.synth_flow_device(flows.data_ptr(), B, H, W, 0, stream=sh)
 ctx.segment_batch_device(flows.data_ptr(), B, H, W, persp, inv, up, stream=sh)
 torch.cuda.synchronize()
-out = (C.c_double * 16)()
-L.dofs_debug_krt_timing(out, 16)
+out = (C.c_double * 20)()
+L.dofs_debug_krt_timing(out, 20)
 for _ in range(NB):
     ctx.segment_batch_device(flows.data_ptr(), B, H, W, persp, inv, up, stream=sh)
 torch.cuda.synchronize()
 ctx.records_device()
-L.dofs_debug_krt_timing(out, 16)
+L.dofs_debug_krt_timing(out, 20)
 blocks = NB * B * ((H * W - 1 + 4095) // 4096)
 names = ["sweep A finds", "sweep B root hash", "sweep C R-half unions + sizes", "sweep D stores", "sweep C L-half unions + top level", "top level",
          "deep block 1", "deep block 2", "parent epilogue", "deep depths S>=256", "deep depths S<256",
@@ -39,4 +39,9 @@ names = ["sweep A finds", "sweep B root hash", "sweep C R-half unions + sizes", 
 res = {n: {"total_ms": round(out[i] / 1e3, 2), "us_per_block": round(out[i] / blocks, 2)}
        for i, n in enumerate(names)}
 hops = {"phase A find rounds (slowest thread) per sweep block": round(out[12] * 100 / max(out[13] * 100, 1), 2)}
+# the preorder sweep (k_pre_sweep, one workgroup per frame, the same 4096-merge blocks)
+pre_names = {14: "pre: tops' pushed positions (load, LDS)", 15: "pre: positions + pushes (issue)",
+             16: "pre: store drain (block barrier)"}
+res.update({n: {"total_ms": round(out[i] / 1e3, 2), "us_per_block": round(out[i] / blocks, 2)}
+            for i, n in pre_names.items()})
 print(json.dumps({"B": B, "batches": NB, "blocks": blocks, "phases": res, "sweep": hops}, indent=1))
