@@ -184,6 +184,7 @@ struct Context {
         dofs_params prm;
         int64_t n_edges = -1;  // segment_graph: the caller's edge count (else build_graph's)
         int64_t mreal = -1;    // segment_graph: merges of the caller's graph (else H*W - 1)
+        bool lean = false;     // the batch kept only the replay records its results read (no dofs_events)
     };
     Backend be;
     Pipeline<Backend> p0, p1, p2;
@@ -213,6 +214,9 @@ struct Context {
 
     bool serial = false;
     bool skip_b = false;  // DOFS_SKIP_B=1: measurement only — graph stage alone, results invalid
+    // dofs_keep_events: batches keep every merge's replay record for dofs_events (default: only the records
+    // the results read — path tops, parked states, merges of >= min_size pixels; Ws::rv_lean)
+    bool keep_events = false;
 
     explicit Context(int device) : be(device), p0(be), p1(be), p2(be), pband(be) {
         const char* ns = getenv("DOFS_SLOTS");
@@ -366,6 +370,7 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     be.record(cx->evA[s], sa);
     if (sb != sa) be.wait(sb, cx->evA[s]);
     be.use(sb);
+    P.w.rv_lean = cx->keep_events ? 0 : 1;
     if (!cx->skip_b) P.run_b();
     be.record(cx->evDone[s], sb);
     be.wait(caller, own_in ? cx->evA[s] : cx->evRead[s]);
@@ -380,6 +385,7 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     m.prm = prm;
     m.n_edges = (d_edges || n_edges > 0) ? n_edges : graph_edges(H, W, nbr8);
     m.mreal = mreal;
+    m.lean = !cx->keep_events && Backend::kLeanReplay;
     return cx->check();
 }
 
@@ -531,6 +537,8 @@ int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity
     if (!cx->have_batch() || !ev) return cx->fail(DOFS_ERR_INVALID_ARG, "no batch");
     const int slot = cx->last_slot();
     if (frame < 0 || frame >= cx->meta[slot].B) return cx->fail(DOFS_ERR_INVALID_ARG, "no frame");
+    if (cx->meta[slot].lean)
+        return cx->fail(DOFS_ERR_INVALID_ARG, "the batch kept no event records: dofs_keep_events(ctx, 1) before it");
     cx->join(cx->nbatch - 1);
     const Ws& w = cx->pipe(slot).w;
     const Dims& d = w.d;

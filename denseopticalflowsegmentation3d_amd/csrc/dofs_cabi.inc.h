@@ -190,6 +190,12 @@ int32_t dofs_set_snapshot_capacity(dofs_ctx* ctx, int32_t per_frame) {
 
 int32_t dofs_snapshot_capacity(dofs_ctx* ctx) { return ctx ? (int32_t)ctx->snap_cap : -1; }
 
+int32_t dofs_keep_events(dofs_ctx* ctx, int32_t on) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    ctx->keep_events = on != 0;
+    return DOFS_OK;
+}
+
 int64_t dofs_batch_count(dofs_ctx* ctx) { return ctx ? ctx->nbatch : -1; }
 
 int32_t dofs_batch_frames(dofs_ctx* ctx) {

@@ -574,7 +574,7 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             RepVal* dst = w.Rv + lb + q - lane;
             if (lane == n - 1 && (finished || n < 64)) {  // the top's record (parent path) or a parked state
                 rv_publish(dst, vx, vy, rank, root, obb);
-            } else {
+            } else if (!w.rv_lean || (meta & kStepKeep)) {
                 RepVal o;
                 o.mx = vx;
                 o.my = vy;
@@ -763,14 +763,16 @@ __device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch
             }
             continue;
         }
-        RepVal o;
-        o.mx = s.mx;
-        o.my = s.my;
-        o.rank = s.rank;
-        o.root = s.root;
-        o.bb = s.bb;
-        o.pad0 = o.pad1 = 0;
-        w.Rv[lb + q] = o;
+        if (!w.rv_lean || (in.meta & kStepKeep)) {
+            RepVal o;
+            o.mx = s.mx;
+            o.my = s.my;
+            o.rank = s.rank;
+            o.root = s.root;
+            o.bb = s.bb;
+            o.pad0 = o.pad1 = 0;
+            w.Rv[lb + q] = o;
+        }
         --q;
     }
 }

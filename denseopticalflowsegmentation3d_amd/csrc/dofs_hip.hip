@@ -2806,7 +2806,7 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w, int steps, int ordw) 
                 const bool ptop = top[k] ? (x == root || (pushed[k] & kPushLight)) : nd[k].lt != 0;
                 StepIn in;
                 if (l < d.N) {
-                    in = step_in_leaf(nd[k].hl, ptop, nd[k].lB, l, lf[k], d.W);
+                    in = step_in_leaf(nd[k].hl, ptop, nd[k].lB, l, lf[k], d.W, w.min_size);
                 } else {
                     in = step_in(w, f, pos[k], ptop, l, nd[k].lB, nd[k].hl);  // (a merge light child: no load)
                 }
@@ -3228,6 +3228,9 @@ struct HipBackend {
     // slot-table race in k_dnc_compress, fixed there; tests/test_gpu_krt_dnc.py holds the two modes equal.
     static constexpr bool kDncAuto = true;
     static constexpr bool kSingleFlags = true;  // KMstEmit / KEdgeInit mark single-pixel endpoints (Ws::single)
+    // Ws::rv_lean is honoured (the dataflow replay; DOFS_REPLAY_FLOW=0's rounds still store every record,
+    // but a lean batch refuses dofs_events either way)
+    static constexpr bool kLeanReplay = true;
     // longest pointer chain the preorder's global jumping starts from: every word leaves its block
     // or goes to the block's top, so at most two words per block on any path
     static int64_t jump_chain_bound(int64_t M) { return 2 * ((M + kDeepTop - 1) / kDeepTop) + 1; }
@@ -3411,8 +3414,21 @@ struct HipBackend {
         rb.tc = reinterpret_cast<unsigned short*>(w.hlB + ((tiles * w.d.B + 1) & ~(int64_t)1));
         return rb;
     }
+    // the late rounds' grids shrink (DOFS_BORUVKA_SHRINK: the first shrinking round, 0 = never): by round
+    // 11 of a 1080p batch few tiles are active, and a full grid of early-exiting workgroups per kernel cost
+    // ~40 µs, 4 kernels a round for the ~12 rounds until ceil(log2 N) + 2 (the tile loops are grid-stride,
+    // so any grid covers every tile)
+    static int boruvka_shrink() {
+        static const int v = [] {
+            const char* e = getenv("DOFS_BORUVKA_SHRINK");
+            return e ? atoi(e) : 11;
+        }();
+        return v;
+    }
     void rec_launch(const Ws& w, int r, void (*k)(Ws, int, RecBufs), const char* name) {
-        const int64_t gx = std::min<int64_t>((tile_count(w.d) + 3) / 4, std::max<int64_t>(1, grid_cap() / w.d.B));
+        int64_t gx = std::min<int64_t>((tile_count(w.d) + 3) / 4, std::max<int64_t>(1, grid_cap() / w.d.B));
+        const int sr = boruvka_shrink();
+        if (sr > 0 && r >= sr) gx = std::max<int64_t>(std::min<int64_t>(gx, 8), gx >> std::min(r - sr + 1, 20));
         const RecBufs rb = rec_bufs(w);
         timed(name, [&] { hipLaunchKernelGGL(k, dim3((unsigned)gx, (unsigned)w.d.B), dim3(256), 0, stream, w, r, rb); });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, name);

@@ -43,6 +43,7 @@ static_assert(sizeof(StepIn) == 32, "StepIn is one 32-byte record");
 constexpr int kStepB = 1;    // light child is the end side (B) of the merge
 constexpr int kStepTop = 2;  // x is the top of its heavy path
 constexpr int kStepDyn = 4;  // light child is a merge node (value produced by the replay)
+constexpr int kStepKeep = 16;  // (8: kLongOk, dofs_hip.hip) size(x) >= min_size: scoring may read x's replay record (Ws::rv_lean)
 
 // Workspace: device pointers (frame-major; per-frame strides by size class) + constants.
 struct Ws {
@@ -132,6 +133,10 @@ struct Ws {
                     // path-top flags (the chip-wide jumping preorder of small batches), else k_pre_sweep
     int pre_steps;  // HIP: k_pre_sweep wrote every merge's StepIn (KPathInit then registers the paths only)
     int deep_wave;  // HIP: the LDS KRT's depths below 32 merges by one register pass per 16-merge window
+    // HIP dataflow replay: a short path stores a merge's replay record only where something reads it — its
+    // path top (the parent's light child), a parked state, a merge of >= min_size pixels (kStepKeep: the
+    // scoring's candidates) — not the records of the other merges (dofs_events needs them all)
+    int rv_lean;
     int single;     // HIP: EU / EV carry bit kSingleBit — the endpoint is a single pixel at this merge (the
                     // merge is its minimum incident edge, so its first in Kruskal order): the KRT sweep
                     // takes its label without a find
@@ -1179,7 +1184,7 @@ DOFS_HD inline StepIn step_in(const Ws& w, int f, int q, bool top, int lt, int l
     StepIn in;
     in.fs = (float)sh;
     in.r = 1. / (double)(sh + sl);  // size(x)
-    in.meta = (lB ? kStepB : 0) | (top ? kStepTop : 0);
+    in.meta = (lB ? kStepB : 0) | (top ? kStepTop : 0) | (sh + sl >= w.min_size ? kStepKeep : 0);
     if (lt < d.N) {
         const F2 v = w.blur[f * d.N + lt];
         in.wbx = v.x * (float)1;
@@ -1196,12 +1201,12 @@ DOFS_HD inline StepIn step_in(const Ws& w, int f, int q, bool top, int lt, int l
 }
 
 // step_in for a pixel light child whose blurred flow lf is already loaded (the preorder sweep's gather)
-DOFS_HD inline StepIn step_in_leaf(unsigned long long hl, bool top, int lB, int lt, F2 lf, int W) {
+DOFS_HD inline StepIn step_in_leaf(unsigned long long hl, bool top, int lB, int lt, F2 lf, int W, int min_size) {
     const int sh = (int)(unsigned)(hl & 0xffffffffu), sl = (int)(unsigned)(hl >> 32);
     StepIn in;
     in.fs = (float)sh;
     in.r = 1. / (double)(sh + sl);
-    in.meta = (lB ? kStepB : 0) | (top ? kStepTop : 0);
+    in.meta = (lB ? kStepB : 0) | (top ? kStepTop : 0) | (sh + sl >= min_size ? kStepKeep : 0);
     in.wbx = lf.x * (float)1;
     in.wby = lf.y * (float)1;
     in.la = (lt % W) | ((lt / W) << 16);

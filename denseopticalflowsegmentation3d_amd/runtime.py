@@ -94,6 +94,8 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_batch_counters.restype = C.c_int32
     L.dofs_set_snapshot_capacity.argtypes = [C.c_void_p, C.c_int32]
     L.dofs_set_snapshot_capacity.restype = C.c_int32
+    L.dofs_keep_events.argtypes = [C.c_void_p, C.c_int32]
+    L.dofs_keep_events.restype = C.c_int32
     L.dofs_snapshot_capacity.argtypes = [C.c_void_p]
     L.dofs_snapshot_capacity.restype = C.c_int32
     L.dofs_batch_count.argtypes = [C.c_void_p]
@@ -215,12 +217,20 @@ class FrameResult:
 class Dofs:
     """One context (one device, one stream): dofs_create / dofs_destroy."""
 
-    def __init__(self, device: int = 0, lib: C.CDLL | str | None = None):
+    def __init__(self, device: int = 0, lib: C.CDLL | str | None = None, keep_events: bool = False):
+        """keep_events: batches keep every merge's replay record for `events` (dofs_keep_events; off by
+        default, like the reference's segment(), which keeps no per-merge records)."""
         self.lib = lib if isinstance(lib, C.CDLL) else load(lib)
         self._last_merges = None
         self.ctx = self.lib.dofs_create(device)
         if not self.ctx:
             raise RuntimeError(f"dofs_create({device}) failed: no gfx950 device visible")
+        if keep_events:
+            self.keep_events(True)
+
+    def keep_events(self, on: bool = True) -> None:
+        """Per-merge event records (`events`) for the batches issued afterwards (dofs_keep_events)."""
+        self._err(self.lib.dofs_keep_events(self.ctx, 1 if on else 0), "dofs_keep_events")
 
     def close(self):
         if getattr(self, "ctx", None):

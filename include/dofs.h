@@ -275,6 +275,11 @@ int32_t dofs_batch_records_copy_id(dofs_ctx* ctx, int64_t batch, void* d_dst, in
 /* Per-frame snapshot-record capacity of the batch API (taken by each workspace at its next batch). */
 int32_t dofs_set_snapshot_capacity(dofs_ctx* ctx, int32_t per_frame);
 int32_t dofs_snapshot_capacity(dofs_ctx* ctx);
+/* Per-merge event records (dofs_events) for the batches issued afterwards: on = 1 keeps every merge's
+ * replay record; 0 (the default) keeps only those the results read — path tops, merges of at least
+ * min_size pixels — and dofs_events on such a batch fails with DOFS_ERR_INVALID_ARG. The reference's
+ * segment() keeps no per-merge records either; its boxes, scores and labels are the same in both modes. */
+int32_t dofs_keep_events(dofs_ctx* ctx, int32_t on);
 /* Number of batches issued on ctx (the last batch id + 1). */
 int64_t dofs_batch_count(dofs_ctx* ctx);
 /* Frames (B) of the last batch issued on ctx (0 if none). */

@@ -31,7 +31,7 @@ def calib():
 @pytest.fixture(scope="session")
 def gpu():
     from denseopticalflowsegmentation3d_amd.runtime import Dofs
-    ctx = Dofs(0)
+    ctx = Dofs(0, keep_events=True)
     yield ctx
     ctx.close()
 
@@ -42,6 +42,6 @@ def emu():
     from denseopticalflowsegmentation3d_amd.runtime import Dofs
     here = os.path.join(ROOT, "tests", "emu")
     locked_make(here)
-    ctx = Dofs(0, lib=os.path.join(here, "_build", "libdofs_emu.so"))
+    ctx = Dofs(0, lib=os.path.join(here, "_build", "libdofs_emu.so"), keep_events=True)
     yield ctx
     ctx.close()

@@ -240,6 +240,7 @@ struct HostBackend {
     static bool pairs_in_relabel(const Ws&) { return false; }  // KBoruvkaPairs
     static bool pre_jump(const Dims&) { return false; }  // (KDncParent writes every word itself)
     static constexpr bool kSingleFlags = false;  // its sweep model reads EU / EV as plain endpoints
+    static constexpr bool kLeanReplay = true;  // (its replay stores every record; dofs_events follows the HIP rule)
     template <class B>
     static bool pre_steps(const B&) { return false; }  // KPathInit writes the StepIn records
     void sort_mst(Ws& w, int64_t n, int nf, int value_bits, bool) {

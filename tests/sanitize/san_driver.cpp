@@ -99,6 +99,7 @@ int main() {
     dofs_ctx* ctx = dofs_create(0);  // the host emulator: always available
     CHECK(ctx != nullptr, "emulator context");
     if (!ctx) return 1;
+    CHECK(dofs_keep_events(ctx, 1) == DOFS_OK, "keep events");  // the cases compare per-merge events
     struct Case {
         int H, W;
         uint64_t seed;

@@ -80,3 +80,20 @@ def test_capacity_overflow_gpu(calib):
                lambda t: t.data_ptr(), lambda t: t.cpu().numpy())
     finally:
         ctx.close()
+
+
+def test_events_refused_without_kept_records(emu, calib):
+    """dofs_keep_events (default off): a batch issued without it has no per-merge records, and dofs_events
+    says so instead of returning unwritten ones (the emulator follows the HIP backend's rule)."""
+    from denseopticalflowsegmentation3d_amd.runtime import Dofs
+    ctx = Dofs(0, lib=emu.lib)
+    try:
+        flow = ob.synth_flow(24, 32, 5)
+        ctx.segment(flow, *calib)
+        with pytest.raises(RuntimeError, match="event records"):
+            ctx.events(0)
+        ctx.keep_events(True)
+        ctx.segment(flow, *calib)
+        assert len(ctx.events(0)) == 24 * 32 - 1
+    finally:
+        ctx.close()

@@ -6,7 +6,9 @@ sequential sweep per frame of the batch side by side. Here the same driver runs 
 configuration itself: four consecutive batches of B = 112 distinct 1080p fields (every workspace is
 reused, 112 concurrent sweeps, the MST sort's fix-up at its full cross-frame group count), and sampled
 frames of every batch — first, middle, last and one seeded random position — are compared with the
-oracle: the gathered box records (slot, size, cls, frame, move exact; score and the 3D faces within the
+oracle, in the context's default mode (no per-merge event records, dofs_keep_events off: the replay stores
+only the records the results read, as bench.py runs it): the gathered box records (slot, size, cls, frame,
+move exact; score and the 3D faces within the
 stated tolerance, parity.check_records) and, through dofs_batch_fetch_id while the batch is still
 readable, the label map and snapshots.
 

@@ -31,7 +31,7 @@ def _run(monkeypatch, mode, B, H, W, calib, seeds, prm=None, skew=0):
     from denseopticalflowsegmentation3d_amd import runtime
     monkeypatch.setenv("DOFS_KRT_DNC", mode)
     persp, inv, up = calib
-    ctx = runtime.Dofs(0)
+    ctx = runtime.Dofs(0, keep_events=True)
     ctx.lib.dofs_debug_dnc_skew.argtypes = [C.c_int]
     assert ctx.lib.dofs_debug_dnc_skew(skew) == 0
     fl = torch.empty((B, H, W, 2), dtype=torch.float32, device="cuda")
@@ -105,7 +105,7 @@ def test_tail_batch_keeps_large_workspace(calib):
     H, W = 180, 320
     prm = params(300, 8)
     persp, inv, up = calib
-    ctx = runtime.Dofs(0)
+    ctx = runtime.Dofs(0, keep_events=True)
     try:
         fl = torch.empty((16, H, W, 2), dtype=torch.float32, device="cuda")
         runtime.synth_flow_device(fl.data_ptr(), 16, H, W, 300)

@@ -1,0 +1,54 @@
+"""GPU: a batch without per-merge event records (dofs_keep_events off, the default) gives the same results.
+
+The dataflow replay then stores a merge's record only where something reads it — its path top (the parent
+path's light child), a parked state, a merge of at least min_size pixels (the scoring's candidates,
+Forest::new_merge's size test, graph.cpp:280-300) — instead of every merge's. Labels, snapshots, the
+slots' best scores and the final roots' boxes must be bit-identical to a batch that kept every record,
+and dofs_events must refuse the lean batch rather than return unwritten records.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+H, W, B = 270, 480, 6
+
+
+def _run(ctx, flows, calib):
+    import torch
+    sh = torch.cuda.current_stream().cuda_stream
+    ctx.segment_batch_device(flows.data_ptr(), B, H, W, *calib, stream=sh)
+    torch.cuda.synchronize()
+    res = [ctx.fetch(f, want_blur=False) for f in range(B)]
+    # the accessors that read replay records after the batch: the slots' best scores (their last
+    # candidates' records) and the final roots' boxes (the path tops')
+    extra = [(ctx.segment_scores(f), ctx.final_roots(f)) for f in range(B)]
+    return res, extra
+
+
+def test_lean_batch_equals_full_batch(calib):
+    import torch
+
+    from denseopticalflowsegmentation3d_amd import runtime
+    flows = torch.empty((B, H, W, 2), dtype=torch.float32, device="cuda:0")
+    runtime.synth_flow_device(flows.data_ptr(), B, H, W, seed0=321, stream=torch.cuda.current_stream().cuda_stream)
+    full = runtime.Dofs(0, keep_events=True)
+    lean = runtime.Dofs(0)
+    try:
+        rf, cf = _run(full, flows, calib)
+        ev = full.events(0)
+        assert len(ev) == H * W - 1
+        rl, cl = _run(lean, flows, calib)
+        for f in range(B):
+            assert np.array_equal(rf[f].labels, rl[f].labels), f
+            assert rf[f].snapshots.tobytes() == rl[f].snapshots.tobytes(), f
+            assert cf[f][0].tobytes() == cl[f][0].tobytes(), f
+            assert np.array_equal(cf[f][1], cl[f][1]), f
+        with pytest.raises(RuntimeError, match="event records"):
+            lean.events(0)
+        lean.keep_events(True)  # from the next batch on
+        _run(lean, flows, calib)
+        assert lean.events(0).tobytes() == ev.tobytes()
+    finally:
+        full.close()
+        lean.close()

@@ -22,7 +22,7 @@ def _run(monkeypatch, jump, B, H, W, calib, seed, prm, krt=None):
     if krt is not None:
         monkeypatch.setenv("DOFS_KRT_DNC", krt)
     persp, inv, up = calib
-    ctx = runtime.Dofs(0)
+    ctx = runtime.Dofs(0, keep_events=True)
     try:
         fl = torch.empty((B, H, W, 2), dtype=torch.float32, device="cuda")
         runtime.synth_flow_device(fl.data_ptr(), B, H, W, seed)

@@ -27,7 +27,7 @@ persp, inv, up = runtime.calib()
 fl = torch.empty((B, H, W, 2), dtype=torch.float32, device="cuda")
 runtime.synth_flow_device(fl.data_ptr(), B, H, W, 500)
 torch.cuda.synchronize()
-ctx = runtime.Dofs(0)
+ctx = runtime.Dofs(0, keep_events=True)
 ctx.segment_batch_device(fl.data_ptr(), B, H, W, persp, inv, up)
 torch.cuda.synchronize()
 c = ctx.batch_counters(B)

@@ -27,7 +27,7 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        ctx = Dofs(0, lib=EMU)
+        ctx = Dofs(0, lib=EMU, keep_events=True)
         persp, inv, up = ob.calib()
         flow = torch.from_numpy(ob.synth_flow(H, W, SEED))
         r0, r1 = band_bounds(H, world, rank)
