@@ -231,8 +231,12 @@ struct Context {
         if (lp && atoi(lp) > 0) p0.long_path = p1.long_path = p2.long_path = atoi(lp);
         const char* kd = getenv("DOFS_KRT_DNC");
         p0.krt_mode = p1.krt_mode = p2.krt_mode = kd && (kd[0] == '0' || kd[0] == '1') ? kd[0] - '0' : -1;
+        // DOFS_SPLIT: where the preorder runs — 1 (default) at the start of phase B, 0 in phase A, 2 only the
+        // path inputs (KPathInit) in B. Phase A bounds the step, phase B has slack: B = 112, same box, three
+        // runs each: 0 → 1,736-1,746 Mpix/s, 1 → 1,758-1,761, 2 → 1,733-1,745
         const char* sp = getenv("DOFS_SPLIT");
-        p0.preorder_in_b = p1.preorder_in_b = p2.preorder_in_b = sp && (sp[0] == '1' || sp[0] == '2') ? sp[0] - '0' : 0;
+        p0.preorder_in_b = p1.preorder_in_b = p2.preorder_in_b =
+            sp && (sp[0] == '0' || sp[0] == '1' || sp[0] == '2') ? sp[0] - '0' : 1;
         // stream priorities: DOFS_PRIO=1 (default) graph stage urgent, replay stage least — its workgroups
         // are dispatched first when a CU frees up, since the graph stage (Borůvka, sort, KRT, preorder)
         // bounds the step; the long-path workers keep their own top-priority stream. 2 = replay stage

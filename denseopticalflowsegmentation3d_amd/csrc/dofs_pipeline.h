@@ -54,7 +54,7 @@ struct Pipeline {
     Dims cap{};  // allocated shape
     int* pre = nullptr;
     int64_t snap_cap = 4096;
-    int preorder_in_b = 0;  // 0: the preorder in phase A; 1: in phase B; 2: the path inputs (KPathInit) in B
+    int preorder_in_b = 1;  // 0: the preorder in phase A; 1: in phase B (the API's default); 2: KPathInit in B
     // block-start labels of the KRT: the top-down global depths (DNC) or the per-frame sweep. The sweep's
     // time is one frame's sequence of blocks (≈ 40 ms at 1080p, 111 ms at 4K, whatever the batch); the
     // DNC's is proportional to the batch's merges (≈ 1.45 ms per million): DNC wins below ≈ 9 frames a
