@@ -52,8 +52,10 @@ C_LONGM = 57           # counters: merges on long heavy paths
 #     replay record (RepVal, 32 B) out = 64 B (a light merge child's 32-B record read is not counted).
 #   k_replay_flow — the whole replay in one dataflow launch; unit: a merge (every merge of the batch):
 #     StepIn 32 B in, RepVal 32 B out = 64 B.
+# k_replay_flow: the StepIn record read per merge; the 32-byte replay record is stored only where it is read
+# (path tops, parked states, merges of >= min_size pixels: DESIGN.md §2.6c) and not counted — a lower bound
 BYTES = {"k_boruvka_min4": (12, 16), "k_boruvka_pick4": 16, "k_boruvka_min": (24, 16), "k_krt_fused": 47,
-         "k_replay_long": 64, "k_replay_flow": 64}
+         "k_replay_long": 64, "k_replay_flow": 32}
 PROBES = ("k_boruvka_min4", "k_boruvka_pick4", "k_krt_fused", "k_replay_flow", "k_replay_long")
 C_FLOWERR = 58         # counters (frame 0): the dataflow replay gave up a bounded wait
 INPUT_SETS = 3         # distinct resident input batches, rotated over the steps
@@ -406,7 +408,8 @@ def main(argv=None):
                  "k_boruvka_pick4": "16 per record read",
                  "k_boruvka_min": "24 (pass 0) / 16 (pass 1) per pixel of a processed tile",
                  "k_krt_fused": f"{BYTES['k_krt_fused']} per merge",
-                 "k_replay_flow": f"{BYTES['k_replay_flow']} per merge (StepIn 32 B in, RepVal 32 B out)",
+                 "k_replay_flow": f"{BYTES['k_replay_flow']} per merge (StepIn 32 B in; the RepVal stores where "
+                                  "read are not counted)",
                  "k_replay_long": f"{BYTES['k_replay_long']} per long-path merge"}
     kern = []
     for name, (ms, launches) in probes.items():

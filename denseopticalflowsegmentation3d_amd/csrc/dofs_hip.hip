@@ -1589,33 +1589,68 @@ __global__ __launch_bounds__(256) void k_boruvka_min4(Ws w, int r, RecBufs rb) {
             // squares): sqrt is monotone and correctly rounded, so the minimum weight is sqrt of the
             // minimum sq, and an edge can tie with it only if its sq lies within 2^-48 (relative) of
             // the minimum — only those take a sqrt (the rounding interval of a weight is 2^-52 wide)
-            unsigned long long sqb[8];
-            unsigned long long msq = ~0ull;  // bits of non-negative doubles order like the values
+            // f32 prefilter: the squared lengths in f32 (relative error < 2^-22: the float differences are
+            // the f64 path's own, then two multiplies and an add) pick the candidate edges; when one edge
+            // alone lies within 2^-20 of the f32 minimum, no other edge can be within 2^-48 of it in f64
+            // (the tie window below), so it is the minimum and takes the only f64 square and sqrt. Ties,
+            // near-ties, NaN / infinite and tiny (< 2^-100: f32 underflow) minima take the f64 path over all
+            // eight edges, as before — the result is the same bit for bit either way.
+            float m32 = __builtin_huge_valf();
+            float fxm = 0.f, fym = 0.f;
+            unsigned im = kNoEdge;
+            bool odd = false;
+            float s32[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const F2 bs = j < 4 ? f0 : fq[j], be = j < 4 ? fq[j] : f0;
-                const double dx = bs.x - be.x, dy = bs.y - be.y;
-                sqb[j] = (ok[j] && cq[j] != c0) ? dbits(sq_len(dx, dy)) : ~0ull;
-                msq = sqb[j] < msq ? sqb[j] : msq;
+                const float fx = bs.x - be.x, fy = bs.y - be.y;
+                const float q = fx * fx + fy * fy;
+                const bool c = ok[j] && cq[j] != c0;
+                s32[j] = c ? q : -1.0f;  // (-1: not a candidate)
+                odd |= c && !(q < __builtin_huge_valf());
+                if (c && q < m32) {
+                    m32 = q;
+                    fxm = fx;
+                    fym = fy;
+                    im = (unsigned)(4 * (j < 4 ? p : nb[j]) + (j & 3));
+                }
             }
+            const float thr32 = m32 * (1.0f + 0x1p-20f);
+            int nsel = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) nsel += s32[j] >= 0.f && s32[j] <= thr32;
             unsigned long long best = ~0ull;
             unsigned bidx = kNoEdge;
-            if (msq != ~0ull) {
-                double mv;
-                memcpy(&mv, &msq, 8);
-                best = dbits(sqrt(mv));
-                const unsigned long long thr = dbits(mv * 1.0000000000000036);  // (1 + 2^-48) mv
+            if (!odd && nsel == 1 && m32 >= 0x1p-100f) {
+                best = dbits(sqrt(sq_len((double)fxm, (double)fym)));
+                bidx = im;
+            } else if (im != kNoEdge || odd) {
+                unsigned long long sqb[8];
+                unsigned long long msq = ~0ull;  // bits of non-negative doubles order like the values
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    if (sqb[j] > thr) continue;  // also the non-candidates (~0)
-                    bool tie = sqb[j] == msq;
-                    if (!tie) {
-                        double v;
-                        memcpy(&v, &sqb[j], 8);
-                        tie = dbits(sqrt(v)) == best;
+                    const F2 bs = j < 4 ? f0 : fq[j], be = j < 4 ? fq[j] : f0;
+                    const double dx = bs.x - be.x, dy = bs.y - be.y;
+                    sqb[j] = (ok[j] && cq[j] != c0) ? dbits(sq_len(dx, dy)) : ~0ull;
+                    msq = sqb[j] < msq ? sqb[j] : msq;
+                }
+                if (msq != ~0ull) {
+                    double mv;
+                    memcpy(&mv, &msq, 8);
+                    best = dbits(sqrt(mv));
+                    const unsigned long long thr = dbits(mv * 1.0000000000000036);  // (1 + 2^-48) mv
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        if (sqb[j] > thr) continue;  // also the non-candidates (~0)
+                        bool tie = sqb[j] == msq;
+                        if (!tie) {
+                            double v;
+                            memcpy(&v, &sqb[j], 8);
+                            tie = dbits(sqrt(v)) == best;
+                        }
+                        const unsigned idx = (unsigned)(4 * (j < 4 ? p : nb[j]) + (j & 3));
+                        if (tie && idx < bidx) bidx = idx;
                     }
-                    const unsigned idx = (unsigned)(4 * (j < 4 ? p : nb[j]) + (j & 3));
-                    if (tie && idx < bidx) bidx = idx;
                 }
             }
             has[i] = valid && bidx != kNoEdge;

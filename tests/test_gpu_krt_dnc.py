@@ -125,3 +125,23 @@ def test_tail_batch_keeps_large_workspace(calib):
         assert len(set(sizes)) == 1, sizes  # no workspace was laid out again
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_deep_depth_forms_equal(monkeypatch, calib, mode):
+    """The LDS KRT's depths below 32 merges as the register window pass (DOFS_DEEP_WAVE=1, default) and as
+    union-find depths (0) give the same tree, in both KRT modes. The union-find form leaves the first
+    half's last merge without a size in LDS (the top level writes it to SZ), which the second half's
+    prefetched labels must then take from SZ — the case this pins."""
+    B, H, W = 12, 270, 480
+    seeds = [77, 177]
+    monkeypatch.setenv("DOFS_DEEP_WAVE", "1")
+    a = _run(monkeypatch, mode, B, H, W, calib, seeds)
+    monkeypatch.setenv("DOFS_DEEP_WAVE", "0")
+    b = _run(monkeypatch, mode, B, H, W, calib, seeds)
+    for (ca, ea, la), (cb, eb, lb) in zip(a, b):
+        assert int(ca[0, 58]) == 0 and int(cb[0, 58]) == 0  # C_FLOWERR (the list positions are not ordered)
+        assert np.array_equal(la, lb)
+        for f in range(B):
+            for name in EVENT_FIELDS:
+                assert np.array_equal(ea[f][name], eb[f][name]), (f, name)

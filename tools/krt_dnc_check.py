@@ -18,7 +18,7 @@ torch.cuda.synchronize()
 res = {}
 for mode in ("1", "0"):
     os.environ["DOFS_KRT_DNC"] = mode
-    ctx = runtime.Dofs(0)
+    ctx = runtime.Dofs(0, keep_events=True)
     ctx.segment_batch_device(fl.data_ptr(), B, H, W, persp, inv, up)
     torch.cuda.synchronize()
     c = ctx.batch_counters(B)

@@ -13,7 +13,7 @@ from denseopticalflowsegmentation3d_amd import runtime  # noqa: E402
 cut = int(sys.argv[1]) if len(sys.argv) > 1 else 24
 fix = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 B, H, W = 4, 180, 320
-ctx = runtime.Dofs(0)
+ctx = runtime.Dofs(0, keep_events=True)
 L = ctx.lib
 L.dofs_debug_sort_cut.argtypes = [C.c_int]
 L.dofs_debug_sort_dump.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]

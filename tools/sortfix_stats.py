@@ -16,7 +16,7 @@ from denseopticalflowsegmentation3d_amd import runtime  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 H = int(sys.argv[2]) if len(sys.argv) > 2 else 1080
 W = int(sys.argv[3]) if len(sys.argv) > 3 else 1920
-ctx = runtime.Dofs(0)
+ctx = runtime.Dofs(0, keep_events=True)
 L = ctx.lib
 L.dofs_debug_sort_cut.argtypes = [C.c_int]
 L.dofs_debug_sort_cut.restype = C.c_int
