@@ -223,8 +223,11 @@ __global__ __launch_bounds__(kBlock) void k_generic_take(F f, int64_t n) {
 }
 // list launch: elements [0, min(n, frame counter cidx)) — the bound is read on the device, so a
 // shrinking list costs only the blocks it needs (the others exit at once)
+// (at least three waves per SIMD: KLift's lifting needed 169 VGPRs, two waves per SIMD, beside the graph
+// stage's sort passes)
 template <class F>
-__global__ __launch_bounds__(kBlock) void k_counted_take(F f, int64_t n, int cidx, int zidx) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_counted_take(F f, int64_t n, int cidx,
+                                                                                                  int zidx) {
     __shared__ int wsum[3 * kBlock / 64];
     __shared__ int base[3];
     BlockTaker t{wsum, base};
@@ -3106,12 +3109,27 @@ struct HipBackend {
         }();
         return cap;
     }
+    // The preorder-position scatters (KLeafPos, KLeafOrder, KPathInit) read and write one frame's
+    // position-indexed arrays at random. Launched uncapped, one lane per merge, the dispatcher hands out
+    // workgroups frame by frame (blockIdx.x fastest), so the chip works on about one frame's arrays
+    // at a time and their random lines stay in the memory-side cache instead of spanning the batch.
+    // DOFS_FRAME_MAJOR=0: the capped grid-stride launch of every other kernel.
+    static bool frame_major_on() {
+        static const bool on = [] {
+            const char* e = getenv("DOFS_FRAME_MAJOR");
+            return e ? e[0] == '1' : false;
+        }();
+        return on;
+    }
+    template <class F>
+    static constexpr bool frame_major_v =
+        std::is_same_v<F, KPathInit> || std::is_same_v<F, KLeafOrder> || std::is_same_v<F, KLeafPos>;
     template <class F>
     static int launch_on(hipStream_t s, int nf, int64_t n, const F& f) {
         if (n <= 0 || nf <= 0) return DOFS_OK;
         int64_t gx = (n + kBlock - 1) / kBlock;
         const int64_t cap = grid_cap() > 0 ? std::max<int64_t>(1, grid_cap() / nf) : 8192;
-        if (gx > cap) gx = cap;
+        if (gx > cap && !(frame_major_v<F> && frame_major_on() && gx <= (int64_t)1 << 30)) gx = cap;
         if constexpr (takes<F>::value)
             hipLaunchKernelGGL(k_generic_take<F>, dim3((unsigned)gx, (unsigned)nf), dim3(kBlock), 0, s, f, n);
         else
@@ -3720,6 +3738,7 @@ struct HipBackend {
     // Kruskal order of each frame's MST edges into w.val_out (values of frame f at [f n, (f + 1) n)).
     // Packed: w.EU (written later by KEdgeInit) is the scratch between the two passes.
     static int sort_k32() { return g_sort_k32; }  // KMstEmit's 32-bit keys for the packed sort (0: 64-bit)
+    static int sort_k32_bits() { return dofs::sort_k32_bits(); }
     void sort_mst(Ws& w, int64_t n, int nf, int value_bits, bool packed) {
         if (!packed) {
             sort_pairs(w.key_in, w.key_out, w.val_in, w.val_out, n, nf, value_bits);
@@ -3732,12 +3751,13 @@ struct HipBackend {
             unsigned* k32_out = reinterpret_cast<unsigned*>(w.key_out);
             unsigned* vmid = reinterpret_cast<unsigned*>(w.EU);
             size_t b1 = 0, b2 = 0;
-            note(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, k32_in, k32_out, w.val_in, vmid, tot, 0, 32, stream),
+            const int kb = sort_k32_bits();
+            note(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, k32_in, k32_out, w.val_in, vmid, tot, 0, kb, stream),
                  "sort size");
             note(hipcub::DeviceRadixSort::SortKeys(nullptr, b2, vmid, w.val_out, tot, value_bits, value_bits + fb, stream),
                  "sort size");
             void* t = temp(std::max(b1, b2));
-            note(hipcub::DeviceRadixSort::SortPairs(t, b1, k32_in, k32_out, w.val_in, vmid, tot, 0, 32, stream), "sort");
+            note(hipcub::DeviceRadixSort::SortPairs(t, b1, k32_in, k32_out, w.val_in, vmid, tot, 0, kb, stream), "sort");
             if (g_sort_fix) sort_fixup32(w, vmid, tot, value_bits);
             if (g_sort_dump[0]) {  // diagnosis: 32-bit keys (4 bytes each) and values after the fix-up
                 const size_t m = (size_t)std::min<int64_t>(tot, g_sort_dump_cap);
@@ -3843,6 +3863,13 @@ extern "C" int dofs_debug_sort_cut(int cut) {
 extern "C" int dofs_debug_sort_k32(int m) {
     const int old = dofs::g_sort_k32;
     if (m == 0 || (m >= 4 && m <= 30)) dofs::g_sort_k32 = m;
+    return old;
+}
+// Test knob: the exponent bits of those keys, 1 .. 8 (m + e < 32: a key of m + e bits, fewer sort digits),
+// or 0 for 32 - m; e < 0 only reads it. Returns the previous value.
+extern "C" int dofs_debug_sort_k32e(int e) {
+    const int old = dofs::g_sort_k32e;
+    if (e >= 0 && e <= 8) dofs::g_sort_k32e = e;
     return old;
 }
 // Diagnosis only: fix-up on / off (the truncated order is not Kruskal's: results differ), and a copy of

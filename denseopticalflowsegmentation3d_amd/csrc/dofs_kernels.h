@@ -189,10 +189,12 @@ DOFS_HD inline unsigned long long dbits(double w) {
 // (32 - m)-bit exponent offset inside the window of 2^(32 - m) binades that ends at etop, the biased
 // double exponent bound of every weight of the frame. Monotone non-decreasing in the 64-bit key read as
 // unsigned: below the window (zero included) 0; above it, or a set sign bit, the largest key.
-DOFS_HD inline unsigned key32_of(unsigned long long k, int etop, int m) {
-    if (k >> 63) return 0xFFFFFFFFu;
-    const int e = (int)((k >> 52) & 0x7FF), lo = etop - ((1 << (32 - m)) - 1);
-    if (e > etop) return 0xFFFFFFFFu;
+// tb: the key's width in bits (m mantissa bits, tb - m exponent bits; the largest key is 2^tb - 1)
+DOFS_HD inline unsigned key32_of(unsigned long long k, int etop, int m, int tb = 32) {
+    const unsigned top = tb >= 32 ? 0xFFFFFFFFu : (1u << tb) - 1u;
+    if (k >> 63) return top;
+    const int e = (int)((k >> 52) & 0x7FF), lo = etop - ((1 << (tb - m)) - 1);
+    if (e > etop) return top;
     if (e < lo) return 0u;
     return ((unsigned)(e - lo) << m) | (unsigned)((k >> (52 - m)) & ((1ull << m) - 1));
 }
@@ -608,6 +610,7 @@ struct KMstEmit {
     Ws w;
     int fshift;  // > 0: the frame id rides above the emission index (one batch-wide frame sort, HIP)
     int k32m = 0;  // > 0: 32-bit keys (key32_of, this many mantissa bits) into key_in's first half (HIP)
+    int k32b = 32;  // their width in bits (key32_of's tb)
     DOFS_HD void operator()(int f, int64_t p) const {
         const Dims& d = w.d;
         const int bits = (int)mst_bits(w.mstbits[f * d.N + p]);
@@ -634,7 +637,7 @@ struct KMstEmit {
                 const double dx = bp.x - bq[k].x, dy = bp.y - bq[k].y;  // edge_weight(b, p, q)
                 const unsigned long long key = dbits(sqrt(sq_len(dx, dy)));
                 if (k32m)
-                    reinterpret_cast<unsigned*>(w.key_in)[f * d.M + j] = key32_of(key, etop, k32m);
+                    reinterpret_cast<unsigned*>(w.key_in)[f * d.M + j] = key32_of(key, etop, k32m, k32b);
                 else
                     w.key_in[f * d.M + j] = key;
                 // p's first merge is its minimum edge (slot k); the far end receives this edge in its slot 4 + k

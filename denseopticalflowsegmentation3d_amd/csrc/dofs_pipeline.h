@@ -323,6 +323,7 @@ struct Pipeline {
         const bool packed = be.mst_packed(M, B, vb);
         KMstEmit em{w, packed ? vb : 0};
         em.k32m = packed ? Backend::sort_k32() : 0;  // 32-bit sort keys (HIP batch sort, dofs_sortfix.h)
+        em.k32b = Backend::sort_k32_bits();
         be.launch(B, N, em);
         be.sort_mst(w, M, B, vb, packed);
         keys_by_frame = !packed;

@@ -223,6 +223,14 @@ inline int g_sort_k32 = [] {
     const int m = e ? atoi(e) : 27;
     return m == 0 || (m >= 4 && m <= 30) ? m : 27;
 }();
+// host: exponent bits of the 32-bit keys (0: 32 - m, the full word). With m + e = 24 the pair sort takes
+// three 8-bit digits instead of four; DOFS_SORT_K32E sets it (A/B runs on one library)
+inline int g_sort_k32e = [] {
+    const char* e = getenv("DOFS_SORT_K32E");
+    const int x = e ? atoi(e) : 0;
+    return x >= 1 && x <= 8 ? x : 0;
+}();
+inline int sort_k32_bits() { return g_sort_k32e && g_sort_k32 + g_sort_k32e < 32 ? g_sort_k32 + g_sort_k32e : 32; }
 
 struct SortFix32 {
     const unsigned* key;      // sorted 32-bit keys (key_out's first half; never permuted)

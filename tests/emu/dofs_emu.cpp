@@ -235,6 +235,7 @@ struct HostBackend {
     }
     static bool mst_packed(int64_t, int, int) { return false; }
     static int sort_k32() { return 0; }  // (per-frame 64-bit sorts)
+    static int sort_k32_bits() { return 32; }
     bool replay_flow(const Ws&) { return false; }  // the round launches (KReplay)
     bool pre_sweep(const Ws&) { return false; }  // KJump (the emulator's KRT has no block epilogue)
     static bool pairs_in_relabel(const Ws&) { return false; }  // KBoruvkaPairs
@@ -279,5 +280,9 @@ extern "C" void emu_line_mask(int32_t H, int32_t W, float ax, float ay, float bx
 // Test-only: the HIP batch sort's 32-bit keys (dofs_kernels.h key32_of / key32_etop) of n 64-bit weight keys.
 extern "C" void emu_key32(const uint64_t* k, int64_t n, int etop, int m, uint32_t* out) {
     for (int64_t i = 0; i < n; ++i) out[i] = dofs::key32_of(k[i], etop, m);
+}
+// ... of tb bits (m mantissa bits, tb - m exponent bits)
+extern "C" void emu_key32b(const uint64_t* k, int64_t n, int etop, int m, int tb, uint32_t* out) {
+    for (int64_t i = 0; i < n; ++i) out[i] = dofs::key32_of(k[i], etop, m, tb);
 }
 extern "C" int emu_key32_etop(int mbits) { return dofs::key32_etop(mbits); }

@@ -22,8 +22,9 @@ H, W, B = 180, 320, 4
 C_SORTFIX = 60  # dofs_common.h: frame 0 fix-up counters (groups sorted locally, fallback flag)
 
 
-def _run(gpu, calib, flows, cut, k32=0):
-    """One batch with the 64-bit keys cut at `cut` (k32 = 0) or the 32-bit keys of k32 mantissa bits."""
+def _run(gpu, calib, flows, cut, k32=0, k32e=0):
+    """One batch with the 64-bit keys cut at `cut` (k32 = 0) or the 32-bit keys of k32 mantissa bits (and
+    k32e exponent bits: a narrower key, fewer sort digits)."""
     import torch
     lib = gpu.lib
     lib.dofs_debug_sort_cut.argtypes = [C.c_int]
@@ -32,6 +33,9 @@ def _run(gpu, calib, flows, cut, k32=0):
     lib.dofs_debug_sort_k32.restype = C.c_int
     old = lib.dofs_debug_sort_cut(cut)
     old_k = lib.dofs_debug_sort_k32(k32)
+    lib.dofs_debug_sort_k32e.argtypes = [C.c_int]
+    lib.dofs_debug_sort_k32e.restype = C.c_int
+    old_e = lib.dofs_debug_sort_k32e(k32e)
     try:
         sh = torch.cuda.current_stream().cuda_stream
         gpu.segment_batch_device(flows.data_ptr(), B, H, W, *calib, params=params(300, 8), stream=sh)
@@ -42,6 +46,7 @@ def _run(gpu, calib, flows, cut, k32=0):
     finally:
         lib.dofs_debug_sort_cut(old)
         lib.dofs_debug_sort_k32(old_k)
+        lib.dofs_debug_sort_k32e(old_e)
     return ev, labels, ctr
 
 
@@ -68,14 +73,14 @@ def test_truncated_sort_matches_full(gpu, calib):
     assert seen[48][1] == 1  # 16-bit keys: mixed groups longer than kFixScan, the fallback merge sort
     # the default 32-bit keys (key32_of): 27 mantissa bits, then fewer, down to the fallback's
     seen = {}
-    for m in (27, 20, 12, 6):
-        ev, lab, ctr = _run(gpu, calib, flows, 0, m)
+    for m in (27, 20, 12, 6, (19, 5)):  # (19, 5): 24-bit keys, three sort digits
+        ev, lab, ctr = _run(gpu, calib, flows, 0, *(m if isinstance(m, tuple) else (m,)))
         seen[m] = ctr.tolist()
         for f in range(B):
             for name in ev0[f].dtype.names:
                 assert np.array_equal(ev[f][name], ev0[f][name]), (m, f, name)
             assert np.array_equal(lab[f], lab0[f]), (m, f)
-    assert seen[27][1] == 0 and seen[20][1] == 0
+    assert seen[27][1] == 0 and seen[20][1] == 0 and seen[(19, 5)][1] == 0
     assert seen[20][0] >= seen[27][0] and seen[12][0] > seen[27][0]
     assert seen[6][1] == 1  # 6 mantissa bits: mixed groups beyond kFixScan, the fallback
 

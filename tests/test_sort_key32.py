@@ -20,6 +20,7 @@ def L(emu):
     lib.emu_key32.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_void_p]
     lib.emu_key32_etop.argtypes = [C.c_int]
     lib.emu_key32_etop.restype = C.c_int
+    lib.emu_key32b.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_void_p]
     return lib
 
 
@@ -83,3 +84,23 @@ def test_key32_keeps_27_mantissa_bits_in_the_window(L):
     same32 = k32[1:] == k32[:-1]
     assert not np.any(same32 & (top[1:] != top[:-1]))
     assert k32.min() > 0  # nothing of the window collapses to the bottom key
+
+
+@pytest.mark.parametrize("m,e", [(19, 5), (21, 3), (16, 8)])
+def test_narrow_keys_monotone_and_capped(L, m, e):
+    """Keys of m + e < 32 bits (DOFS_SORT_K32E: three sort digits at 24 bits) stay monotone and below 2^(m+e),
+    the sign-bit NaN and weights above the window at the largest one."""
+    rng = np.random.default_rng(31 + m)
+    M = 9.25
+    w = np.concatenate([_weights(rng, 20000, M), np.exp(rng.uniform(-40, 6, 20000)),
+                        np.array([0.0, 1e-300, 1.0, 1e30, np.inf, -np.nan])])
+    k64 = np.sort(w.view(np.uint64))
+    tb = m + e
+    out = np.empty(len(k64), np.uint32)
+    L.emu_key32b(k64.ctypes.data, len(k64), _etop(L, M), m, tb, out.ctypes.data)
+    assert np.all(np.diff(out.astype(np.int64)) >= 0)
+    assert int(out.max()) == (1 << tb) - 1 and out[-1] == (1 << tb) - 1 and out[0] == 0
+    wide = np.empty(len(k64), np.uint32)  # inside the window the mantissa bits are the 32-bit key's
+    L.emu_key32b(k64.ctypes.data, len(k64), _etop(L, M), m, 32, wide.ctypes.data)
+    inw = (out > 0) & (out < (1 << tb) - 1)
+    assert np.array_equal(out[inw] & np.uint32((1 << m) - 1), wide[inw] & np.uint32((1 << m) - 1))
