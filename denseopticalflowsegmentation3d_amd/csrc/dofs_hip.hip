@@ -3113,23 +3113,29 @@ struct HipBackend {
     // position-indexed arrays at random. Launched uncapped, one lane per merge, the dispatcher hands out
     // workgroups frame by frame (blockIdx.x fastest), so the chip works on about one frame's arrays
     // at a time and their random lines stay in the memory-side cache instead of spanning the batch.
-    // DOFS_FRAME_MAJOR=0: the capped grid-stride launch of every other kernel.
-    static bool frame_major_on() {
-        static const bool on = [] {
+    // DOFS_FRAME_MAJOR=0: the capped grid-stride launch of every other kernel; 2: also the scoring
+    // stage's gathers (KFilter, KSnapshot, KLabel, KSlotInit)
+    static int frame_major_mode() {
+        static const int m = [] {
             const char* e = getenv("DOFS_FRAME_MAJOR");
-            return e ? e[0] == '1' : false;
+            return e ? atoi(e) : 1;
         }();
-        return on;
+        return m;
     }
     template <class F>
-    static constexpr bool frame_major_v =
-        std::is_same_v<F, KPathInit> || std::is_same_v<F, KLeafOrder> || std::is_same_v<F, KLeafPos>;
+    static bool frame_major() {
+        const int m = frame_major_mode();
+        if (m >= 1 && (std::is_same_v<F, KPathInit> || std::is_same_v<F, KLeafOrder> || std::is_same_v<F, KLeafPos>))
+            return true;
+        return m >= 2 && (std::is_same_v<F, KFilter> || std::is_same_v<F, KSnapshot> || std::is_same_v<F, KLabel> ||
+                          std::is_same_v<F, KSlotInit>);
+    }
     template <class F>
     static int launch_on(hipStream_t s, int nf, int64_t n, const F& f) {
         if (n <= 0 || nf <= 0) return DOFS_OK;
         int64_t gx = (n + kBlock - 1) / kBlock;
         const int64_t cap = grid_cap() > 0 ? std::max<int64_t>(1, grid_cap() / nf) : 8192;
-        if (gx > cap && !(frame_major_v<F> && frame_major_on() && gx <= (int64_t)1 << 30)) gx = cap;
+        if (gx > cap && !(frame_major<F>() && gx <= (int64_t)1 << 30)) gx = cap;
         if constexpr (takes<F>::value)
             hipLaunchKernelGGL(k_generic_take<F>, dim3((unsigned)gx, (unsigned)nf), dim3(kBlock), 0, s, f, n);
         else
