@@ -3905,6 +3905,43 @@ extern "C" int dofs_debug_sortfix_run(void* d_keys, void* d_vals, void* d_k2, vo
     const hipError_t e = hipDeviceSynchronize();
     return e == hipSuccess ? (int)hipGetLastError() : (int)e;
 }
+// Test-only: the 32-bit keys' fix-up (k_sortfix32_local, then the fallback's full keys and merge sort) over
+// n (32-bit key, value) pairs in truncated-key stable order. d_keys: 8 n bytes, the 32-bit keys in its
+// first 4 n (the fallback overwrites it with full keys); values 4 p + k of the frames' edges, frame above
+// bit vb; d_blur: B frames of H x W blurred flow (float2), the weights' source. d_ctr: 3 ints (moved,
+// fallback flag, -).
+extern "C" int dofs_debug_sortfix32_run(void* d_keys, void* d_vals, void* d_k2, void* d_v2, int64_t n, const void* d_blur,
+                                        int B, int H, int W, int vb, int* d_ctr) {
+    using namespace dofs;
+    if (n <= 0 || B < 1 || H < 1 || W < 1 || vb < 3 || vb > 31 || !d_keys || !d_vals || !d_k2 || !d_v2 || !d_blur ||
+        !d_ctr)
+        return (int)hipErrorInvalidValue;
+    Dims d{};
+    d.H = H;
+    d.W = W;
+    d.N = (int64_t)H * W;
+    d.M = d.N - 1;
+    d.NL = d.N + d.M;
+    d.B = B;
+    d.nbr8 = 0;
+    if (4 * d.N > ((int64_t)1 << vb)) return (int)hipErrorInvalidValue;
+    SortFix32 s{(const unsigned*)d_keys, (unsigned*)d_vals, (unsigned long long*)d_keys, (unsigned long long*)d_k2,
+                (unsigned*)d_v2, (const F2*)d_blur, d, vb, ~0u, d_ctr, n};
+    int lgs = 0;
+    while (((int64_t)1 << lgs) < n) ++lgs;
+    lgs += lgs & 1;
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    const unsigned gx = (unsigned)std::min<int64_t>((n + kFixBlock - 1) / kFixBlock, 8192);
+    hipLaunchKernelGGL(k_sortfix32_local, dim3(gx), dim3(kFixBlock), 0, nullptr, s);
+    hipLaunchKernelGGL(k_sortfix32_keys, dim3(2 * cus), dim3(kFixBlock), 0, nullptr, s);
+    hipLaunchKernelGGL(k_sortfix_merge, dim3(2 * cus), dim3(kFixBlock), 0, nullptr,
+                       SortFix{(unsigned long long*)d_keys, (unsigned*)d_vals, (unsigned long long*)d_k2, (unsigned*)d_v2,
+                               d_ctr, n, 1},
+                       lgs);
+    const hipError_t e = hipDeviceSynchronize();
+    return e == hipSuccess ? (int)hipGetLastError() : (int)e;
+}
 extern "C" void dofs_debug_sort_dump(void* d_keys, void* d_vals, int64_t cap) {
     dofs::g_sort_dump[0] = d_keys;
     dofs::g_sort_dump[1] = d_vals;

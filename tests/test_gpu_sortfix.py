@@ -143,3 +143,66 @@ def test_sortfix_random_groups(gpu):
     want = np.lexsort((vals, keys))
     gk, gv, ctr = _fixup(gpu.lib, keys, vals, cut)
     assert np.array_equal(gk, keys[want]) and np.array_equal(gv, vals[want]), ctr
+
+
+def _fixup32(lib, keys32, vals, blur):
+    """dofs_debug_sortfix32_run over 32-bit (keys, vals) in stable order; the weights come from `blur` (one frame,
+    1 x W); returns the values and the counters (moved, fallback flag)."""
+    import torch
+    lib.dofs_debug_sortfix32_run.argtypes = [C.c_void_p] * 4 + [C.c_int64, C.c_void_p] + [C.c_int] * 4 + [C.c_void_p]
+    lib.dofs_debug_sortfix32_run.restype = C.c_int
+    n = len(keys32)
+    k = np.zeros(2 * n, np.uint32)
+    k[:n] = keys32
+    dk = torch.from_numpy(k.view(np.int32)).cuda()
+    dv = torch.from_numpy(vals.view(np.int32).copy()).cuda()
+    k2 = torch.empty(2 * n, dtype=torch.int32, device="cuda")
+    v2 = torch.empty_like(dv)
+    db = torch.from_numpy(np.ascontiguousarray(blur, np.float32)).cuda()
+    ctr = torch.zeros(3, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    rc = lib.dofs_debug_sortfix32_run(dk.data_ptr(), dv.data_ptr(), k2.data_ptr(), v2.data_ptr(), n, db.data_ptr(),
+                                      1, 1, blur.shape[0], 30, ctr.data_ptr())
+    assert rc == 0, rc
+    return dv.cpu().numpy().view(np.uint32), ctr.cpu().numpy()[:2].tolist()
+
+
+def _edges(weights):
+    """A 1 x W blurred field whose odd pixels' left edges (values 4 p, slot 0) have the given weights
+    (|float difference|: the even pixels hold 0)."""
+    n = len(weights)
+    blur = np.zeros((2 * n + 2, 2), np.float32)
+    p = 2 * np.arange(n) + 1
+    blur[p, 0] = np.asarray(weights, np.float32)
+    return blur, (4 * p).astype(np.uint32)
+
+
+@pytest.mark.parametrize("lead", [0, 1, 37, 64, 200])
+@pytest.mark.parametrize("ties", [255, 256, 257])
+def test_sortfix32_long_exact_tie_run_then_smaller_weight(gpu, lead, ties):
+    """The 32-bit keys' fix-up at its window edge: `ties` equal weights, then one smaller weight with the same
+    32-bit key (groups of one frame). With ties >= 256 the only mixed pair lies past the scalar sorter's window:
+    the fallback must catch it; either way the order ends as (weight, value)."""
+    w = np.concatenate([0.25 + np.arange(lead) / 1024.0, np.full(ties, 1.0), [1.0 - 2.0 ** -20]])
+    keys = np.concatenate([np.arange(lead), np.full(ties + 1, lead)]).astype(np.uint32)
+    blur, vals = _edges(w)
+    got, ctr = _fixup32(gpu.lib, keys, vals, blur)
+    want = vals[np.lexsort((vals, w.astype(np.float32).astype(np.float64)))]
+    assert np.array_equal(got, want), (lead, ties, ctr)
+    assert ctr[1] == (1 if ties >= 256 else 0), ctr
+
+
+def test_sortfix32_random_groups(gpu):
+    """Random groups of 1 .. 300 pairs with few distinct weights each (ties and mixes; the longer mixed ones
+    take the fallback): the fixed order is the (weight, value) order."""
+    rng = np.random.default_rng(12)
+    ws, ks = [], []
+    for g in range(1500):
+        n = int(rng.choice([1, 2, 3, 7, 16, 17, 40, 64, 65, 255, 256, 257, 300]))
+        ws.append(1.0 + g + rng.integers(0, 4, n) / 16.0)  # exact in float; the key is the group
+        ks.append(np.full(n, g, np.uint32))
+    w, keys = np.concatenate(ws), np.concatenate(ks)
+    blur, vals = _edges(w)
+    got, ctr = _fixup32(gpu.lib, keys, vals, blur)
+    want = vals[np.lexsort((vals, w))]
+    assert np.array_equal(got, want), ctr
