@@ -3582,7 +3582,7 @@ struct HipBackend {
     static int flow_long_workers() {  // waves that run long paths (the rest of the grid runs short ones)
         static const int g = [] {
             const char* e = getenv("DOFS_FLOW_LONG");
-            return e && atoi(e) > 0 ? atoi(e) : 256;
+            return e && atoi(e) > 0 ? atoi(e) : 128;
         }();
         return g;
     }
