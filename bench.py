@@ -323,6 +323,7 @@ def main(argv=None):
     for _ in range(a.warmup):
         step()
     flush()
+    checked0 = fp.checked
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -343,6 +344,11 @@ def main(argv=None):
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    # every timed batch's records were copied through FrameParallel.collect, which fails on a batch whose
+    # replay gave up (dofs_batch_records_copy: DOFS_ERR_DEVICE); this counts the batches it checked
+    checked = fp.checked - checked0
+    if checked != a.steps * len(chunks):
+        raise RuntimeError(f"{checked} of {a.steps * len(chunks)} timed batches were checked")
     ms_ev = ev_step[0].elapsed_time(e1)
     per_step = sorted(ev_step[k].elapsed_time(ev_step[k + 1]) for k in range(a.steps))
     probes = dict(zip(a.probe.split(","), ctx.probe_read_n(8))) if a.probe else {}
@@ -504,6 +510,8 @@ def main(argv=None):
                "workspace_mb_per_frame": round(ctx.workspace_bytes() / B / 1e6, 1),
                "input_sets": 1 if a.frames else INPUT_SETS,
                "dofs_env": {k: v for k, v in sorted(os.environ.items()) if k.startswith("DOFS_")},
+               "replay_workers": ctx.flow_workers(),
+               "timed_batches_checked": checked,
                "snapshots_frame0": int(len(res.snapshots)),
                "candidates_frame0": int(res.stats["n_candidates"])}
         out = {

@@ -171,6 +171,9 @@ struct KSynth {
 
 // ---- context -----------------------------------------------------------------------------------
 
+// the error of every result accessor on a batch whose dataflow replay gave up a bounded wait (C_FLOWERR)
+constexpr const char* kFlowErrMsg = "the replay of this batch gave up a bounded wait: its results are invalid";
+
 template <class Backend>
 struct Context {
     // Workspaces used in turn by consecutive batches (kSlots, DOFS_SLOTS=2 for two). A batch runs
@@ -374,7 +377,11 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     be.record(cx->evA[s], sa);
     if (sb != sa) be.wait(sb, cx->evA[s]);
     be.use(sb);
-    P.w.rv_lean = cx->keep_events ? 0 : 1;
+    // lean replay stores only the records the scoring reads; a forest (a caller's edge list that leaves
+    // several components, mreal < M) runs full: dofs_final_roots reads the record of every component the
+    // completion merges join, and a heavy child below min_size would not have one
+    const bool lean = !cx->keep_events && mreal >= d.M;
+    P.w.rv_lean = lean ? 1 : 0;
     if (!cx->skip_b) P.run_b();
     be.record(cx->evDone[s], sb);
     be.wait(caller, own_in ? cx->evA[s] : cx->evRead[s]);
@@ -389,7 +396,7 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     m.prm = prm;
     m.n_edges = (d_edges || n_edges > 0) ? n_edges : graph_edges(H, W, nbr8);
     m.mreal = mreal;
-    m.lean = !cx->keep_events && Backend::kLeanReplay;
+    m.lean = lean && Backend::kLeanReplay;
     return cx->check();
 }
 
@@ -442,7 +449,7 @@ int api_fetch(Context<Backend>* cx, int frame, dofs_result* out, int64_t batch =
     be.sync();
     // the dataflow replay gave up a bounded wait: the batch's results are invalid (never seen with the
     // default KRT; dofs_dataflow.h), reported rather than returned
-    if (ctr0[C_FLOWERR]) return cx->fail(DOFS_ERR_DEVICE, "the replay of this batch gave up a bounded wait");
+    if (ctr0[C_FLOWERR]) return cx->fail(DOFS_ERR_DEVICE, kFlowErrMsg);
     const int ns = ctr[C_SNAP];
     out->n_snapshots = ns;
     out->stats.n_edges = m.n_edges;
@@ -739,6 +746,7 @@ template <class Backend>
 int check_overflow(Context<Backend>* cx, int64_t batch) {
     const int slot = cx->slot_of(batch);
     cx->be.event_sync(cx->evDone[slot]);
+    if (cx->be.read_int(cx->pipe(slot).w.ctr + C_FLOWERR)) return cx->fail(DOFS_ERR_DEVICE, kFlowErrMsg);
     const int ovf = cx->be.read_int(cx->pipe(slot).w.ctr + C_OVF_ANY);
     if (ovf) return cx->fail(DOFS_ERR_CAPACITY, "snapshot records overflowed the per-frame capacity");
     return cx->check();
@@ -746,9 +754,14 @@ int check_overflow(Context<Backend>* cx, int64_t batch) {
 
 // The first per_frame records of every frame are the first per_frame of its snapshots (slot order):
 // KSnapshot writes the first snap_cap of them whatever the count, so with per_frame <= snap_cap every
-// copied record exists and the copy needs no host wait — the counts say when a frame had more. A
-// per_frame above the workspace's capacity is refused whatever the data (DOFS_ERR_CAPACITY), so ranks
-// of one configuration all copy or all fail: a frame-parallel gather never sees one rank drop out.
+// copied record exists — the counts say when a frame had more. A per_frame above the workspace's capacity
+// is refused whatever the data (DOFS_ERR_CAPACITY), so ranks of one configuration all copy or all fail: a
+// frame-parallel gather never sees one rank drop out.
+// The copy waits for the batch (one host wait per collect; the pipelined caller collects batch k after
+// submitting k + slots - 1, whose graph stage it then overlaps anyway) and reads the batch's replay flag:
+// a replay that gave up a bounded wait (C_FLOWERR, dofs_dataflow.h) returns DOFS_ERR_DEVICE — after
+// writing the block with every count DOFS_RECORDS_INVALID, so a collective gather that follows still
+// moves equal blocks and every receiver sees which rank's frames are invalid.
 template <class Backend>
 int api_records_copy(Context<Backend>* cx, int64_t batch, void* dst, int per_frame, void* stream) {
     if (!cx->live(batch) || !dst || per_frame < 0) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
@@ -757,12 +770,20 @@ int api_records_copy(Context<Backend>* cx, int64_t batch, void* dst, int per_fra
     const int B = cx->meta[slot].B;
     if (per_frame > w.snap_cap)
         return cx->fail(DOFS_ERR_CAPACITY, "per_frame exceeds the snapshot capacity (dofs_set_snapshot_capacity)");
+    cx->be.event_sync(cx->evDone[slot]);
+    const bool gave_up = cx->be.read_int(w.ctr + C_FLOWERR) != 0;
     cx->be.set_stream(stream);
     cx->join(batch);
     cx->be.copy2d(dst, sizeof(int), w.ctr + C_SNAP, sizeof(int) * kCounters, sizeof(int), B);
     if (per_frame > 0)
         cx->be.copy2d((char*)dst + sizeof(int) * B, sizeof(dofs_box_record) * per_frame, w.recs,
                       sizeof(dofs_box_record) * w.snap_cap, sizeof(dofs_box_record) * per_frame, B);
+    if (gave_up) {
+        static_assert(DOFS_RECORDS_INVALID == -1, "counts are filled with 0xFF bytes");
+        cx->be.memset(dst, 0xFF, sizeof(int) * (size_t)B);
+        if (int rc = cx->check()) return rc;
+        return cx->fail(DOFS_ERR_DEVICE, kFlowErrMsg);
+    }
     return cx->check();
 }
 

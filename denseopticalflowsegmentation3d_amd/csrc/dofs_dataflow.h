@@ -57,7 +57,7 @@ enum FlowCtlIdx {
     FC_FS = 8 * kFlowLine,          // the launch anatomy: FS_N u64 counters, one 256-byte line each (FlowStat)
     FC_HDR = FC_FS + 24 * 64,       // then pl[B + 1], pt[B + 1], ps[B + 1]
 };
-constexpr int kFlowSpin = 1 << 22;  // polls of a queue slot before giving up (s_sleep between)
+inline int g_flow_order = 0;  // host: the two launches' order (dofs_debug_flow_order; 0 = side by side)
 
 // launch anatomy (a few atomics per task, not per step): per launch, in the context's control block
 // (FC_FS; so two contexts on one device never mix their counts), read by dofs_debug_flow_stats
@@ -657,14 +657,16 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
     }
 }
 
-constexpr int kFlowChunk = 256;  // initial short tasks a wave claims per atomic (its lanes take them in turn)
+constexpr int kFlowChunk = 256;  // initial short tasks a short worker claims per atomic (its lanes take them in turn)
+constexpr int kFlowHelp = 64;    // initial short tasks an idle long worker claims (one claim, then back to its queue)
 
-// Short paths, one per lane, until no lane has one: idle lanes take initial tasks while `grab` holds (from
-// the wave's claimed chunk [*cbp, *cep), refilled by one atomic per kFlowChunk tasks); a lane whose path
-// completes continues the short path parked on its top, and queues a long one (a long worker takes it).
-// inject: a short task handed over by a long path's completion (lane 0 starts with it).
-__device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch, int inject, bool grab, int* cbp,
-                                           int* cep) {
+// Short paths, one per lane, until no lane has one: idle lanes take initial tasks from the wave's claimed
+// chunk [*cbp, *cep), refilled by one atomic of `chunk` tasks at most `claims` times (-1: until the pool is
+// empty; 0: never); a lane whose path completes continues the short path parked on its top, and queues a
+// long one (a long worker takes it). inject: a short task handed over by a long path's completion (lane 0
+// starts with it). Nothing here waits for another wave: every task a wave holds runs to completion or parks.
+__device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch, int inject, int claims, int chunk,
+                                           int* cbp, int* cep) {
     const Dims& d = w.d;
     const int lane = threadIdx.x & 63;
     const int ntot = ctl[FC_NT] + ctl[FC_NS];
@@ -678,19 +680,21 @@ __device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch
     s.rank = s.root = 0;
     s.bb.x0 = s.bb.y0 = s.bb.x1 = s.bb.y1 = 0;
     for (int it = 0;; ++it) {
-        if (grab) {
+        if (claims != 0 || *cbp < *cep) {
             unsigned long long idle = __ballot(t < 0);
             while (idle) {
                 if (*cbp >= *cep) {  // claim the next chunk of the pool
+                    if (claims == 0) break;
                     int base = 0;
-                    if (lane == 0) base = atomicAdd(ctl + FC_SHORT_NEXT, kFlowChunk);
+                    if (lane == 0) base = atomicAdd(ctl + FC_SHORT_NEXT, chunk);
                     base = __shfl(base, 0, 64);
                     if (base >= ntot) {
-                        grab = false;
+                        claims = 0;
                         break;
                     }
+                    if (claims > 0) --claims;
                     *cbp = base;
-                    *cep = base + kFlowChunk < ntot ? base + kFlowChunk : ntot;
+                    *cep = base + chunk < ntot ? base + chunk : ntot;
                 }
                 const int avail = *cep - *cbp;
                 const int r = __popcll(idle & ((1ull << lane) - 1));
@@ -778,18 +782,23 @@ __device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch
 }
 
 // A long worker's next task: the initial long pool first, then a ticket of the long-path queue, whose
-// slot its pusher fills (tickets are taken only by long workers, and only while pushes are pending, so
-// there is no CAS herd on the head and at most the racing workers' tickets run ahead of the pushes).
-// -1: every long path completed (a ticket's slot that will never be filled), or a wait gave up. A slot
-// is accepted only with this launch's tag and a long task word of the batch: slots never written in
-// this launch hold Borůvka minima or older tags, which neither passes (kFlowEpochs < the high word of
-// any weight the MST stores there).
+// slot its pusher fills. A ticket is claimed only below the queue's tail (a CAS on the head), so its slot
+// already belongs to a push in progress: the wait for the slot is for a lane that is running, never for
+// work that has yet to be produced. With neither, an idle worker helps with the initial short pool
+// (kFlowHelpTask) while it is not empty. So a long worker never waits for a wave that is not running: the
+// replay completes whether the short workers' launch runs beside this one, before it or after it.
+// -1: every long path completed, or a bounded wait gave up (C_FLOWERR). A slot is accepted only with this
+// launch's tag and a long task word of the batch: slots never written in this launch hold Borůvka minima
+// or older tags, which neither passes (kFlowEpochs < the high word of any weight the MST stores there,
+// DESIGN.md §6a).
 constexpr unsigned kFlowEpochs = 0xFFFFF;
+constexpr int kFlowHelpTask = -2;  // flow_next_long: no long task now, the short pool has tasks
 __device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int nl) {
     const int lane = threadIdx.x & 63;
     int t = -1;
     if (lane == 0) {
         const int np = ctl[FC_NLPOOL];
+        const int ntot = ctl[FC_NT] + ctl[FC_NS];
         while (t < 0 && f_poll(ctl + FC_LONG_NEXT) < np) {
             const int i = atomicAdd(ctl + FC_LONG_NEXT, 1);
             if (i < np) t = flow_long_task(w, ctl, i);
@@ -800,11 +809,12 @@ __device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int 
                 f_st(ctl + FC_ERR, 1);
                 break;
             }
-            if (f_poll(ctl + FC_QHEAD) < f_poll(ctl + FC_QTAIL)) {
-                const int h = atomicAdd(ctl + FC_QHEAD, 1);
-                if (h >= ctl[FC_QCAP]) break;  // (never filled)
+            const int h = f_poll(ctl + FC_QHEAD);
+            if (h < f_poll(ctl + FC_QTAIL)) {
+                if (atomicCAS(ctl + FC_QHEAD, h, h + 1) != h) continue;  // another worker took ticket h
+                if (h >= ctl[FC_QCAP]) break;  // (never: pushes stay below the capacity)
                 const long long nframe = w.d.N;
-                for (int s2 = 0;; ++s2) {
+                for (int s2 = 0;; ++s2) {  // slot h's pusher has its ticket: its store is on the way
                     const unsigned long long v = f_poll64(w.bw + h);
                     const int c = (int)(unsigned)v;
                     if ((unsigned)(v >> 32) == epoch && c >= 0 && (c & kFlowLong) &&
@@ -812,14 +822,15 @@ __device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int 
                         t = c;
                         break;
                     }
-                    if ((s2 & 15) == 15 && f_poll(ctl + FC_LDONE) >= nl) break;
                     if (s2 >= (1 << 26)) {
                         f_st(ctl + FC_ERR, 1);
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(16);
+                    __builtin_amdgcn_s_sleep(2);
                 }
-                if (t < 0) break;  // the ticket's wait ended without a task: all long paths are done
+                if (t < 0) break;
+            } else if (f_poll(ctl + FC_SHORT_NEXT) < ntot) {
+                t = kFlowHelpTask;
             } else {
                 __builtin_amdgcn_s_sleep(32);
             }
@@ -855,6 +866,12 @@ __global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigne
         __builtin_amdgcn_s_setprio(3);  // the chains go first in their SIMD's arbitration
         for (int it = 0; it < (1 << 26); ++it) {
             int t = flow_next_long(w, ctl, epoch, nl);
+            if (t == kFlowHelpTask) {  // idle: one claim of the initial short pool, at the short workers' priority
+                __builtin_amdgcn_s_setprio(0);
+                flow_short(w, ctl, epoch, -1, 1, kFlowHelp, &cb, &ce);
+                __builtin_amdgcn_s_setprio(3);
+                continue;
+            }
             if (t < 0) break;
             const unsigned long long t1 = fs_now();
             while (t >= 0) {
@@ -863,7 +880,7 @@ __global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigne
                                     : flow_long<false>(w, ctl, t, buf[wv], ob[wv], keyfast);
                 if (nx >= 0 && !(nx & kFlowLong)) {  // a short waiter: a one-lane short round (and its waiters)
                     if (lane == 0) fs_add(ctl, FS_INJECT, 1);
-                    flow_short(w, ctl, epoch, nx, false, &cb, &ce);
+                    flow_short(w, ctl, epoch, nx, 0, 0, &cb, &ce);
                     break;
                 }
                 t = nx;
@@ -872,7 +889,7 @@ __global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigne
         }
     } else {
         const unsigned long long t1 = fs_now();
-        flow_short(w, ctl, epoch, -1, true, &cb, &ce);
+        flow_short(w, ctl, epoch, -1, -1, kFlowChunk, &cb, &ce);
         if (lane == 0) {
             fs_add(ctl, FS_SROUNDS, 1);
             fs_add(ctl, FS_STICKS, fs_now() - t1);

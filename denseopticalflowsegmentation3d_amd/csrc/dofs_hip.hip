@@ -3617,10 +3617,18 @@ struct HipBackend {
             note(hipEventRecord(flow_ev[0], stream), "hipEventRecord");
             note(hipStreamWaitEvent(flow_stream, flow_ev[0], 0), "hipStreamWaitEvent");
             const int kf = keyfast(w.d);
-            hipLaunchKernelGGL((k_replay_flow<true, kFlowLongW>), dim3((unsigned)gl), dim3(64 * kFlowLongW), 0, flow_stream,
-                               w, flow_ctl, flow_epoch, kf, flow_pipe());
+            // g_flow_order (test entry dofs_debug_flow_order): 1 / 2 run the two launches one after the other on
+            // one stream (long workers first / short workers first) — the replay must complete either way
+            const int order = g_flow_order;
+            hipStream_t ls = order ? stream : flow_stream;
+            if (order != 2)
+                hipLaunchKernelGGL((k_replay_flow<true, kFlowLongW>), dim3((unsigned)gl), dim3(64 * kFlowLongW), 0, ls,
+                                   w, flow_ctl, flow_epoch, kf, flow_pipe());
             hipLaunchKernelGGL((k_replay_flow<false, kFlowShortW>), dim3((unsigned)gs), dim3(64 * kFlowShortW), 0, stream,
                                w, flow_ctl, flow_epoch, kf, 0);
+            if (order == 2)
+                hipLaunchKernelGGL((k_replay_flow<true, kFlowLongW>), dim3((unsigned)gl), dim3(64 * kFlowLongW), 0, ls,
+                                   w, flow_ctl, flow_epoch, kf, flow_pipe());
             note(hipEventRecord(flow_ev[1], flow_stream), "hipEventRecord");
             note(hipStreamWaitEvent(stream, flow_ev[1], 0), "hipStreamWaitEvent");
         });
@@ -3816,14 +3824,14 @@ struct HipBackend {
             // the fallback (both return at once unless the flag is up): full keys, then the merge sort
             hipLaunchKernelGGL(k_sortfix32_keys, dim3(2 * cus), dim3(kFixBlock), 0, stream, s);
             hipLaunchKernelGGL(k_sortfix_merge, dim3(2 * cus), dim3(kFixBlock), 0, stream,
-                               SortFix{w.key_out, vmid, w.key_in, w.val_in, w.ctr + C_SORTFIX, tot, 1}, lgs);
+                               SortFix{w.key_out, vmid, w.key_in, w.val_in, w.ctr + C_SORTFIX, tot, 1, s.vm}, lgs);
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "sort fix-up launch");
     }
     // dofs_sortfix.h: the groups of equal truncated keys sorted by the full key (val_out, written by the
     // frame pass next, holds the lists; key_in / val_in, dead after the pair sort, the scratch)
     void sort_fixup(Ws& w, unsigned* vmid, int64_t tot, int cut) {
-        SortFix s{w.key_out, vmid, w.key_in, w.val_in, w.ctr + C_SORTFIX, tot, cut};
+        SortFix s{w.key_out, vmid, w.key_in, w.val_in, w.ctr + C_SORTFIX, tot, cut, w.single ? 0x3FFFFFFFu : ~0u};
         const int64_t cap = grid_cap() > 0 ? grid_cap() : 8192;
         const unsigned gx = (unsigned)std::min<int64_t>((tot + kFixBlock - 1) / kFixBlock, cap);
         int lgs = 0;
@@ -3893,7 +3901,7 @@ extern "C" int dofs_debug_sortfix_run(void* d_keys, void* d_vals, void* d_k2, vo
                                       int* d_ctr) {
     using namespace dofs;
     if (n <= 0 || cut < 1 || cut > 48 || !d_keys || !d_vals || !d_k2 || !d_v2 || !d_ctr) return (int)hipErrorInvalidValue;
-    SortFix s{(unsigned long long*)d_keys, (unsigned*)d_vals, (unsigned long long*)d_k2, (unsigned*)d_v2, d_ctr, n, cut};
+    SortFix s{(unsigned long long*)d_keys, (unsigned*)d_vals, (unsigned long long*)d_k2, (unsigned*)d_v2, d_ctr, n, cut, ~0u};
     int lgs = 0;
     while (((int64_t)1 << lgs) < n) ++lgs;
     lgs += lgs & 1;
@@ -3937,10 +3945,25 @@ extern "C" int dofs_debug_sortfix32_run(void* d_keys, void* d_vals, void* d_k2, 
     hipLaunchKernelGGL(k_sortfix32_keys, dim3(2 * cus), dim3(kFixBlock), 0, nullptr, s);
     hipLaunchKernelGGL(k_sortfix_merge, dim3(2 * cus), dim3(kFixBlock), 0, nullptr,
                        SortFix{(unsigned long long*)d_keys, (unsigned*)d_vals, (unsigned long long*)d_k2, (unsigned*)d_v2,
-                               d_ctr, n, 1},
+                               d_ctr, n, 1, s.vm},
                        lgs);
     const hipError_t e = hipDeviceSynchronize();
     return e == hipSuccess ? (int)hipGetLastError() : (int)e;
+}
+// Test knob: the dataflow replay's two worker launches (dofs_dataflow.h) side by side on two streams (0, the
+// default), or one after the other on the stage's stream: 1 = long workers first, 2 = short workers first.
+// Neither role waits for work the other launch has yet to produce, so every order completes. Returns the
+// previous value; order < 0 only reads it.
+extern "C" int dofs_debug_flow_order(int order) {
+    const int old = dofs::g_flow_order;
+    if (order >= 0 && order <= 2) dofs::g_flow_order = order;
+    return old;
+}
+// Inspection: the dataflow replay's worker counts (waves) — long-path workers (DOFS_FLOW_LONG) and short ones.
+extern "C" int dofs_flow_workers(int* long_waves, int* short_waves) {
+    if (long_waves) *long_waves = dofs::HipBackend::flow_long_workers();
+    if (short_waves) *short_waves = dofs::HipBackend::flow_grid();
+    return 0;
 }
 extern "C" void dofs_debug_sort_dump(void* d_keys, void* d_vals, int64_t cap) {
     dofs::g_sort_dump[0] = d_keys;

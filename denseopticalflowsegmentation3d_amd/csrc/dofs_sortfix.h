@@ -42,12 +42,14 @@ struct SortFix {
                // [2] the fallback's grid barrier
     int64_t n;
     int cut;
+    unsigned vm;  // the frame and index bits of a value: below the singleton flags when Ws::single, else all
+                  // 32 (a batch with vb + fb > 30 has frame bits in 30-31, and they keep the pairs distinct)
 };
 
-// values compare below their two top bits (the KRT sweep's singleton flags, dofs_kernels.h kValSingle*: the
-// frame and emission index, distinct for all pairs, sit below them)
-__device__ inline bool fix_less(unsigned long long ka, unsigned va, unsigned long long kb, unsigned vb) {
-    return ka < kb || (ka == kb && (va & 0x3FFFFFFFu) < (vb & 0x3FFFFFFFu));
+// values compare on their frame and emission index bits only (vm): with Ws::single the two top bits are the
+// KRT sweep's singleton flags (dofs_kernels.h kValSingle*), not part of the pair's identity
+__device__ inline bool fix_less(unsigned long long ka, unsigned va, unsigned long long kb, unsigned vb, unsigned vm) {
+    return ka < kb || (ka == kb && (va & vm) < (vb & vm));
 }
 
 // the scalar path of one group [p, ...) from its first position: at most kFixScan positions, in place
@@ -73,7 +75,7 @@ __device__ inline int fix_group_scalar(const SortFix& s, int64_t p, unsigned lon
         const unsigned long long k = s.key[i];
         const unsigned v = s.val[i];
         int64_t j = i;
-        while (j > p && fix_less(k, v, s.key[j - 1], s.val[j - 1])) {
+        while (j > p && fix_less(k, v, s.key[j - 1], s.val[j - 1], s.vm)) {
             s.key[j] = s.key[j - 1];
             s.val[j] = s.val[j - 1];
             --j;
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(kFixBlock) void k_sortfix_local(SortFix s) {
                 const int j = (gs + d) & 63;
                 const unsigned long long kj = __shfl(b, j, 64);
                 const unsigned vj = __shfl(v, j, 64);
-                rank += (fast && d < g && j != lane && fix_less(kj, vj, b, v)) ? 1 : 0;
+                rank += (fast && d < g && j != lane && fix_less(kj, vj, b, v, s.vm)) ? 1 : 0;
             }
             if (fast && gs + rank != lane) {
                 s.key[base + gs + rank] = b;
@@ -185,7 +187,7 @@ __global__ __launch_bounds__(kFixBlock) void k_sortfix_merge(SortFix s, int lgs)
             const int64_t l0 = lo;
             while (lo < hi) {  // partner pairs below (k, v)
                 const int64_t m = lo + (hi - lo) / 2;
-                if (fix_less(ka[m], va[m], k, v))
+                if (fix_less(ka[m], va[m], k, v, s.vm))
                     lo = m + 1;
                 else
                     hi = m;
@@ -285,7 +287,7 @@ __device__ inline int fix32_group_scalar(const SortFix32& s, int64_t p, unsigned
         const unsigned long long k = s.k2[i];
         const unsigned v = s.val[i];
         int64_t j = i;
-        while (j > p && fix_less(k, v, s.k2[j - 1], s.val[j - 1])) {
+        while (j > p && fix_less(k, v, s.k2[j - 1], s.val[j - 1], s.vm)) {
             s.k2[j] = s.k2[j - 1];
             s.val[j] = s.val[j - 1];
             --j;
@@ -346,7 +348,7 @@ __global__ __launch_bounds__(kFixBlock) void k_sortfix32_local(SortFix32 s) {
                 const int j = (gs + dd) & 63;
                 const unsigned long long kj = __shfl(b, j, 64);
                 const unsigned vj = __shfl(v, j, 64);
-                rank += (fast && dd < g && j != lane && fix_less(kj, vj, b, v)) ? 1 : 0;
+                rank += (fast && dd < g && j != lane && fix_less(kj, vj, b, v, s.vm)) ? 1 : 0;
             }
             if (fast && gs + rank != lane) {  // the group's keys are equal: only the value moves
                 s.val[base + gs + rank] = v;

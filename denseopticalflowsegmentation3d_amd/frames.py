@@ -14,6 +14,8 @@ import torch.distributed as dist
 from .abi import DofsBoxRecord
 
 RECORD_DTYPE = DofsBoxRecord.np_dtype()
+RECORDS_INVALID = -1  # include/dofs.h DOFS_RECORDS_INVALID: the frame's batch failed (its replay gave up)
+DOFS_ERR_DEVICE = 3
 
 
 def frame_shard(total: int, rank: int, world: int) -> range:
@@ -55,9 +57,12 @@ def records_nbytes(frames: int, per_frame: int) -> int:
 
 
 def decode_records(buf: np.ndarray, frames: int, per_frame: int) -> list[np.ndarray]:
-    """Per-frame arrays of valid box records from one rank's block."""
+    """Per-frame arrays of valid box records from one rank's block. A block whose counts are
+    RECORDS_INVALID (its rank's batch failed) raises instead of decoding."""
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
     counts = buf[:4 * frames].view(np.int32)
+    if (counts == RECORDS_INVALID).any():
+        raise RuntimeError("gathered box records of a batch whose replay gave up (DOFS_RECORDS_INVALID)")
     recs = buf[4 * frames:records_nbytes(frames, per_frame)].view(RECORD_DTYPE).reshape(frames, per_frame)
     return [recs[f, :min(int(counts[f]), per_frame)].copy() for f in range(frames)]
 
@@ -96,6 +101,7 @@ class FrameParallel:
         self.ctx, self.world, self.per_frame = ctx, world, per_frame
         self.block = None
         self.frames = {}
+        self.checked = 0  # batches collected whose replay completed (records_copy checks each)
 
     def submit(self, flows: torch.Tensor, persp, inv, inv_upper, params=None, stream: int | None = None) -> int:
         B, H, W = flows.shape[:3]
@@ -111,8 +117,16 @@ class FrameParallel:
         nb = records_nbytes(B, self.per_frame)
         if self.block is None or self.block.numel() != nb:
             self.block = torch.empty(nb, dtype=torch.uint8, device=device)
-        self.ctx.records_copy(self.block.data_ptr(), self.per_frame, stream=stream, batch=bid)
-        return gather_records(self.block, self.world)
+        # every batch collected is checked: a replay that gave up fails here (after the gather, which the
+        # other ranks are in; its block carries RECORDS_INVALID counts so the receivers see it too)
+        rc = self.ctx.records_copy(self.block.data_ptr(), self.per_frame, stream=stream, batch=bid, check=False)
+        if rc not in (0, DOFS_ERR_DEVICE):
+            raise RuntimeError(f"dofs_batch_records_copy failed ({rc}): {self.ctx.last_error()}")
+        out = gather_records(self.block, self.world)
+        self.checked += 1
+        if rc:
+            raise RuntimeError(f"batch {bid}: dofs_batch_records_copy failed ({rc}): {self.ctx.last_error()}")
+        return out
 
     def step(self, flows: torch.Tensor, persp, inv, inv_upper, params=None, stream: int | None = None):
         return self.collect(self.submit(flows, persp, inv, inv_upper, params, stream), stream)

@@ -398,15 +398,32 @@ class Dofs:
                   "dofs_batch_records_device")
         return rec.value, cnt.value, cap.value
 
-    def records_copy(self, d_dst: int, per_frame: int, stream: int | None = None, batch: int | None = None) -> None:
+    def records_copy(self, d_dst: int, per_frame: int, stream: int | None = None, batch: int | None = None,
+                     check: bool = True) -> int:
         """int32 counts[B] then B × per_frame DofsBoxRecord into a device buffer (stream-ordered), of the
-        last batch or of batch id `batch` (one of the last batch_slots())."""
+        last batch or of batch id `batch` (one of the last batch_slots()). A batch whose replay gave up is
+        copied with every count DOFS_RECORDS_INVALID (-1) and fails (RuntimeError; with check=False the
+        status is returned instead, for a caller that must reach a collective first)."""
         if batch is None:
             rc = self.lib.dofs_batch_records_copy(self.ctx, C.c_void_p(d_dst), per_frame, C.c_void_p(stream or 0))
         else:
             rc = self.lib.dofs_batch_records_copy_id(self.ctx, batch, C.c_void_p(d_dst), per_frame,
                                                      C.c_void_p(stream or 0))
-        self._err(rc, "dofs_batch_records_copy")
+        if check:
+            self._err(rc, "dofs_batch_records_copy")
+        return int(rc)
+
+    def last_error(self) -> str:
+        return self.lib.dofs_last_error(self.ctx).decode()
+
+    def flow_workers(self) -> dict | None:
+        """The dataflow replay's worker waves {"long": .., "short": ..} (HIP library only)."""
+        f = getattr(self.lib, "dofs_flow_workers", None)
+        if f is None:
+            return None
+        nl, ns = C.c_int(0), C.c_int(0)
+        f(C.byref(nl), C.byref(ns))
+        return {"long": nl.value, "short": ns.value}
 
     def batch_counters(self, B: int) -> np.ndarray:
         """The last batch's per-frame counter blocks (B x 64 int32; Borůvka round flags at 16 + r)."""

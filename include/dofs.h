@@ -267,7 +267,12 @@ int32_t dofs_batch_records_device(dofs_ctx* ctx, void** d_records, void** d_coun
  * was truncated by the caller's per_frame, which the counts show. Each frame keeps its first
  * dofs_snapshot_capacity() records (default 4096), so per_frame must not exceed that capacity:
  * DOFS_ERR_CAPACITY (nothing copied) otherwise, whatever the data — ranks of one configuration
- * therefore all copy or all fail. Never waits on the host. The labels are exact in every case. */
+ * therefore all copy or all fail. The labels are exact in every case.
+ * Waits on the host for the batch (one wait per copy) and checks its replay: a batch whose replay gave up
+ * a bounded wait (never seen) is copied with every count = DOFS_RECORDS_INVALID and the
+ * call returns DOFS_ERR_DEVICE, so a gather that follows still moves equal blocks and every receiver can
+ * tell which frames are invalid. */
+#define DOFS_RECORDS_INVALID (-1)
 int32_t dofs_batch_records_copy(dofs_ctx* ctx, void* d_dst, int32_t per_frame, void* stream);
 /* Same for batch id `batch` (one of the last three issued); ordered after that batch on `stream`. */
 int32_t dofs_batch_records_copy_id(dofs_ctx* ctx, int64_t batch, void* d_dst, int32_t per_frame,

@@ -95,6 +95,14 @@ int main(int argc, char** argv) {
                 CHECK(dofs_segment_scores(ctx, -1, 0, sc, 12) == DOFS_OK);
                 CHECK(dofs_segment_scores(ctx, -1, 0, sc, 11) == DOFS_ERR_CAPACITY);
             }
+            { /* per-merge events: refused on a batch issued without dofs_keep_events (the default), returned
+               * for the batches issued after it */
+                dofs_event ev[11];
+                CHECK(dofs_events(ctx, 0, ev, 11) == DOFS_ERR_INVALID_ARG);
+                CHECK(dofs_keep_events(ctx, 1) == DOFS_OK);
+                CHECK(dofs_segment_graph(ctx, flow, 3, 4, 0, edges, n, persp, inv, up, &p, &res) == DOFS_OK);
+                CHECK(dofs_events(ctx, 0, ev, 11) == DOFS_OK);
+            }
             dofs_destroy(ctx);
         }
     }

@@ -52,3 +52,36 @@ def test_lean_batch_equals_full_batch(calib):
     finally:
         full.close()
         lean.close()
+
+
+def test_lean_context_forest_of_small_components(calib):
+    """segment_graph on a caller edge list that leaves only components smaller than
+    min_size (edges inside 3 x 3 tiles, min_size 20). dofs_final_roots reads the replay record of every
+    component the completion merges join, including heavy children below min_size, which a lean replay
+    would not store: a default (lean) context must still return the oracle's final roots and boxes
+    (Forest::get_bounding_box after the loop, graph.cpp:446-452)."""
+    from denseopticalflowsegmentation3d_amd import runtime
+    from oracle import binding as ob
+    from parity import params
+    from test_forest_accessors import _final_from_oracle
+    from test_graph_api import _edges
+
+    persp, inv, up = calib
+    h, w = 60, 81
+    blurred = ob.blur(ob.synth_flow(h, w, 9))
+    s, e, wt = ob.build_graph(blurred, neighbor=8)
+    tile = lambda p: (p // w) // 3 * 1000 + (p % w) // 3  # noqa: E731
+    keep = tile(s) == tile(e)
+    edges = _edges(s[keep], e[keep], wt[keep])
+    prm = params(20, 8)
+    o = ob.segment_graph(blurred, edges["start"], edges["end"], edges["weight"], persp, inv, up, params=prm,
+                         mode=1, forest=True)
+    want = _final_from_oracle(o)
+    assert len(want) == (h // 3) * (w // 3)  # one root per tile
+    lean = runtime.Dofs(0)
+    try:
+        for _ in range(4):  # later runs reuse workspaces whose records hold an earlier run's
+            lean.segment_graph(blurred, edges, persp, inv, up, params=prm)
+            assert np.array_equal(lean.final_roots(0), want)
+    finally:
+        lean.close()

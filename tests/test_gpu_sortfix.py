@@ -145,9 +145,9 @@ def test_sortfix_random_groups(gpu):
     assert np.array_equal(gk, keys[want]) and np.array_equal(gv, vals[want]), ctr
 
 
-def _fixup32(lib, keys32, vals, blur):
-    """dofs_debug_sortfix32_run over 32-bit (keys, vals) in stable order; the weights come from `blur` (one frame,
-    1 x W); returns the values and the counters (moved, fallback flag)."""
+def _fixup32(lib, keys32, vals, blur, nframes=1, vb=30):
+    """dofs_debug_sortfix32_run over 32-bit (keys, vals) in stable order; the weights come from `blur` (nframes
+    frames of 1 x W, the frame id above value bit vb); returns the values and the counters (moved, fallback flag)."""
     import torch
     lib.dofs_debug_sortfix32_run.argtypes = [C.c_void_p] * 4 + [C.c_int64, C.c_void_p] + [C.c_int] * 4 + [C.c_void_p]
     lib.dofs_debug_sortfix32_run.restype = C.c_int
@@ -162,7 +162,7 @@ def _fixup32(lib, keys32, vals, blur):
     ctr = torch.zeros(3, dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
     rc = lib.dofs_debug_sortfix32_run(dk.data_ptr(), dv.data_ptr(), k2.data_ptr(), v2.data_ptr(), n, db.data_ptr(),
-                                      1, 1, blur.shape[0], 30, ctr.data_ptr())
+                                      nframes, 1, blur.shape[0] // nframes, vb, ctr.data_ptr())
     assert rc == 0, rc
     return dv.cpu().numpy().view(np.uint32), ctr.cpu().numpy()[:2].tolist()
 
@@ -205,4 +205,46 @@ def test_sortfix32_random_groups(gpu):
     blur, vals = _edges(w)
     got, ctr = _fixup32(gpu.lib, keys, vals, blur)
     want = vals[np.lexsort((vals, w))]
+    assert np.array_equal(got, want), ctr
+
+
+def test_sortfix_frame_bits_above_bit_29(gpu):
+    """a packed batch with value bits + frame bits > 30 carries frame ids in value bits 30-31
+    (no singleton flags then). Pairs of frames that differ only there, with equal keys and emission index, must
+    stay distinct in the fix-up's (key, value) compare — the local pass and the merge-sort fallback (a mixed
+    group longer than the window forces it) — or one value is lost and another duplicated."""
+    cut = 24
+    K = np.uint64(0x3FF0_0000_1234_5678)
+    idx = np.arange(300, dtype=np.uint32) * 4
+    parts_k, parts_v = [], []
+    for fr in (0, 1, 2, 3):  # frame bits 30-31 (vb = 30)
+        parts_k.append(np.where(np.arange(300) % 3 == 0, K - np.uint64(1), K).astype(np.uint64))
+        parts_v.append(idx | np.uint32(fr << 30))
+    keys, vals = np.concatenate(parts_k), np.concatenate(parts_v)
+    keys, vals = _truncated_stable(keys, vals, cut)
+    want = np.lexsort((vals, keys))
+    gk, gv, ctr = _fixup(gpu.lib, keys, vals, cut)
+    assert ctr[1] == 1, ctr  # the group is longer than the window: the fallback ran
+    assert len(np.unique(gv)) == len(gv)
+    assert np.array_equal(gk, keys[want]) and np.array_equal(gv, vals[want]), ctr
+
+
+def test_sortfix32_frame_bits_above_bit_29(gpu):
+    """The 32-bit keys' fix-up with frame ids reaching value bits 30-31 (vb = 26, 64 frames): frames f and
+    f + 16 / f + 32 have identical fields, so their pairs share full keys and emission indices and differ only in
+    the frame bits. A long mixed group forces the fallback's global (full key, value) merge sort."""
+    nf, vb = 64, 26
+    w1 = np.concatenate([np.full(200, 1.0), np.full(100, 1.0 - 2.0 ** -20)])
+    blur1, idx = _edges(w1)
+    blur = np.concatenate([blur1] * nf)
+    keys, vals = [], []
+    for f in (0, 16, 32, 48):  # frame bits 30 and 31
+        keys.append(np.full(len(idx), 7, np.uint32))
+        vals.append(idx | np.uint32(f << vb))
+    keys, vals = np.concatenate(keys), np.concatenate(vals)
+    got, ctr = _fixup32(gpu.lib, keys, vals, blur, nframes=nf, vb=vb)
+    wf = np.tile(w1.astype(np.float32).astype(np.float64), 4)
+    want = vals[np.lexsort((vals, wf))]
+    assert ctr[1] == 1, ctr
+    assert len(np.unique(got)) == len(got)
     assert np.array_equal(got, want), ctr
