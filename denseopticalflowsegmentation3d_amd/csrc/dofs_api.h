@@ -11,6 +11,7 @@
 #include <string>
 #include <vector>
 
+#include "dofs_knobs.h"
 #include "dofs_overlay.h"
 #include "dofs_pipeline.h"
 
@@ -176,7 +177,7 @@ constexpr const char* kFlowErrMsg = "the replay of this batch gave up a bounded 
 
 template <class Backend>
 struct Context {
-    // Workspaces used in turn by consecutive batches (kSlots, DOFS_SLOTS=2 for two). A batch runs
+    // Workspaces used in turn by consecutive batches (kSlots). A batch runs
     // phase A (graph) on stream sA and phase B (replay + scoring) on stream sB, so batch k's phase B
     // overlaps the next batches' phase A. A workspace is reused only after its previous batch's
     // phase B (evDone) ended: with three, the latency-bound phase B of batch k may run as long as
@@ -207,55 +208,32 @@ struct Context {
     bool used[kSlots] = {false, false, false};
     Meta meta[kSlots];
     void* sA = nullptr;
-    void* sA1 = nullptr;  // the graph stage of odd batches (DOFS_DUAL_A=0: all on sA)
     void* sB = nullptr;
     void* evIn = nullptr;
     void* evA[kSlots] = {nullptr, nullptr, nullptr};
     void* evRead[kSlots] = {nullptr, nullptr, nullptr};  // the batch's input consumed (after the blur)
     void* evDone[kSlots] = {nullptr, nullptr, nullptr};
-    bool dual_a = false;
 
     bool serial = false;
-    bool skip_b = false;  // DOFS_SKIP_B=1: measurement only — graph stage alone, results invalid
+    bool skip_b = false;  // DOFS_SKIP_B=1 (measurement builds only): graph stage alone, results invalid
     // dofs_keep_events: batches keep every merge's replay record for dofs_events (default: only the records
     // the results read — path tops, parked states, merges of >= min_size pixels; Ws::rv_lean)
     bool keep_events = false;
 
     explicit Context(int device) : be(device), p0(be), p1(be), p2(be), pband(be) {
-        const char* ns = getenv("DOFS_SLOTS");
-        if (ns && (ns[0] == '2' || ns[0] == '3')) nslots = ns[0] - '0';
-        const char* e = getenv("DOFS_SERIAL");
-        serial = e && e[0] == '1';
-        const char* sk = getenv("DOFS_SKIP_B");
-        skip_b = sk && sk[0] == '1';
-        const char* sm = getenv("DOFS_SKIPMASK");
-        p0.skip_mask = p1.skip_mask = p2.skip_mask = sm ? atoi(sm) : 0;
-        const char* lp = getenv("DOFS_LONG_PATH");
-        if (lp && atoi(lp) > 0) p0.long_path = p1.long_path = p2.long_path = atoi(lp);
-        const char* kd = getenv("DOFS_KRT_DNC");
-        p0.krt_mode = p1.krt_mode = p2.krt_mode = kd && (kd[0] == '0' || kd[0] == '1') ? kd[0] - '0' : -1;
-        // DOFS_SPLIT: where the preorder runs — 1 (default) at the start of phase B, 0 in phase A, 2 only the
-        // path inputs (KPathInit) in B. Phase A bounds the step, phase B has slack: B = 112, same box, three
-        // runs each: 0 → 1,736-1,746 Mpix/s, 1 → 1,758-1,761, 2 → 1,733-1,745
-        const char* sp = getenv("DOFS_SPLIT");
-        p0.preorder_in_b = p1.preorder_in_b = p2.preorder_in_b =
-            sp && (sp[0] == '0' || sp[0] == '1' || sp[0] == '2') ? sp[0] - '0' : 1;
-        // stream priorities: DOFS_PRIO=1 (default) graph stage urgent, replay stage least — its workgroups
-        // are dispatched first when a CU frees up, since the graph stage (Borůvka, sort, KRT, preorder)
-        // bounds the step; the long-path workers keep their own top-priority stream. 2 = replay stage
-        // urgent (the default while the replay ran in rounds and was the critical chain), 0 = equal.
-        // Round 3, B = 112, same box (Mpix/s): 1 → 1,559 / 1,561, 2 → 1,499 / 1,499, 0 → 1,253 / 1,255
-        const char* pr = getenv("DOFS_PRIO");
-        const int prio = pr ? atoi(pr) : 1;
-        // DOFS_DUAL_A=1: two graph-stage streams, batches alternating — batch k + 1's graph stage starts
-        // once batch k has read its input, so one batch's latency-bound sweeps (KRT, preorder) may overlap
-        // the next one's bandwidth-bound kernels. Measured equal to one stream (B = 112, same box: 1,485 /
-        // 1,480 vs 1,479 / 1,479 Mpix/s; the chip's total work bounds the step), so it is off by default
-        const char* da = getenv("DOFS_DUAL_A");
-        dual_a = da && da[0] == '1';
-        sA = be.new_stream(prio == 1 ? 1 : 0);
-        sA1 = be.new_stream(prio == 1 ? 1 : 0);
-        sB = be.new_stream(prio == 1 ? -1 : (prio == 2 ? 1 : 0));
+        const Knobs& kn = be.kn;  // the knobs dofs_create validated (dofs_knobs.h), kept by the backend
+        serial = kn.serial != 0;
+        skip_b = kn.skip_b != 0;
+        p0.skip_mask = p1.skip_mask = p2.skip_mask = kn.skip_mask;
+        if (kn.long_path > 0) p0.long_path = p1.long_path = p2.long_path = kn.long_path;
+        p0.krt_mode = p1.krt_mode = p2.krt_mode = kn.krt_dnc;
+        // stream priorities: the graph stage (Borůvka, sort, KRT) bounds the step, so its stream is the most
+        // urgent and the replay + scoring stage's the least — a freed CU takes the graph stage's next
+        // workgroup first (round 3, B = 112, same box: 1,559 / 1,561 Mpix/s against 1,499 / 1,499 with the
+        // replay stage urgent and 1,253 / 1,255 with equal priorities); the long-path replay workers keep
+        // a top-priority stream of their own
+        sA = be.new_stream(1);
+        sB = be.new_stream(-1);
         evIn = be.new_event();
         for (int s = 0; s < kSlots; ++s) {
             evA[s] = be.new_event();
@@ -323,6 +301,9 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     if (B <= 0 || H <= 0 || W <= 0 || !persp || !inv || !inv_upper) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
     if (H > 32767 || W > 32767) return cx->fail(DOFS_ERR_INVALID_ARG, "H and W must be < 32768");
     if ((int64_t)H * W >= (1 << 26)) return cx->fail(DOFS_ERR_INVALID_ARG, "H*W must be < 2^26");
+    // the dataflow replay's task words hold frame * H*W + path in 30 bits (dofs_dataflow.h); such a batch
+    // (B >= 518 at 1080p) would not fit a workspace in HBM either
+    if ((int64_t)B * H * W >= ((int64_t)1 << 30)) return cx->fail(DOFS_ERR_INVALID_ARG, "B*H*W must be < 2^30");
     dofs_params prm;
     if (params)
         prm = *params;
@@ -357,7 +338,7 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     // the caller's own inputs beyond the flow (an edge list, an edge mask) are read past the blur: those
     // batches release the caller after the whole graph stage, on sA
     const bool own_in = allow || d_edges || n_edges > 0;
-    void* sa = (cx->dual_a && !serial && !own_in && (id & 1)) ? cx->sA1 : cx->sA;
+    void* sa = cx->sA;
     void* sb = serial ? cx->sA : cx->sB;
     be.record(cx->evIn, caller);
     be.wait(sa, cx->evIn);

@@ -61,19 +61,28 @@ int32_t dofs_obj_size(int32_t cls, double out[2]) {
     return DOFS_OK;
 }
 
+// why the last dofs_create returned NULL (dofs_last_error(NULL))
+static std::string g_create_err = "null context";
+
 dofs_ctx* dofs_create(int32_t device) {
-    if (!DofsBackend::device_ok(device)) return nullptr;
+    if (!dofs::knobs_load(&g_create_err)) return nullptr;  // an unknown DOFS_* knob or an invalid value
+    if (!DofsBackend::device_ok(device)) {
+        g_create_err = "no gfx950 device " + std::to_string(device);
+        return nullptr;
+    }
     dofs_ctx* c = new dofs_ctx(device);
     if (!c->be.ok()) {
+        g_create_err = c->be.error();
         delete c;
         return nullptr;
     }
+    g_create_err = "null context";
     return c;
 }
 
 void dofs_destroy(dofs_ctx* ctx) { delete ctx; }
 
-const char* dofs_last_error(dofs_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+const char* dofs_last_error(dofs_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
 
 int32_t dofs_segment(dofs_ctx* ctx, const float* flow_uv, int32_t H, int32_t W, size_t row_stride_bytes,
                      const float persp[9], const float inv[9], const float inv_upper[27], const dofs_params* params,

@@ -58,6 +58,10 @@ enum FlowCtlIdx {
     FC_HDR = FC_FS + 24 * 64,       // then pl[B + 1], pt[B + 1], ps[B + 1]
 };
 inline int g_flow_order = 0;  // host: the two launches' order (dofs_debug_flow_order; 0 = side by side)
+// host: constant-key chunks in the long-path loop (flow_long; 1 = on, the default: 96 % of the chunks, one 4K
+// frame's replay 93 → 72 ms). dofs_debug_replay_keyfast(0) runs every chunk with the key update, the test of
+// tests/test_gpu_replay_modes.py that the two give identical merge events.
+inline int g_keyfast = 1;
 
 // launch anatomy (a few atomics per task, not per step): per launch, in the context's control block
 // (FC_FS; so two contexts on one device never mix their counts), read by dofs_debug_flow_stats
@@ -277,7 +281,7 @@ __device__ inline int flow_resolve(const Ws& w, int64_t lb, int p, int top, OneR
     return meta;
 }
 
-// The pipelined resolve of a long path's chunks (flow_long<true>). Resolving a chunk is three dependent
+// The pipelined resolve of a long path's chunks (flow_long). Resolving a chunk is three dependent
 // global round trips — its StepIn records, then the state words of its dynamic light children, then the
 // records of those that are done (rv_fetch only after the state word was seen done: the publisher wrote
 // the record before the state word) — and the synchronous form paid all three at the top of every
@@ -348,7 +352,6 @@ __device__ inline void pipe_restart(const Ws& w, int64_t lb, int q, int top, int
 
 // A long path (task word t) on this wave, from its cursor: returns the task word of the parent path
 // that was parked on its top (to run next), or -1 (parked itself, or completed with nobody waiting).
-template <bool kPipe>
 __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut* ob, int keyfast) {
     const Dims& d = w.d;
     const int g = t & kFlowIdMask;
@@ -378,7 +381,7 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
     unsigned curlk = rec.lk;  // this lane's step key in the current chunk (valid for lanes < n)
     unsigned chunks = 0, steps = 0, kfast = 0, restarts = 1;  // anatomy, added once per call
     FlowPipe P;
-    if constexpr (kPipe) pipe_restart(w, lb, q, top, lane, P);
+    pipe_restart(w, lb, q, top, lane, P);
 #ifdef DOFS_FLOW_PROF
     unsigned long long p_steps = 0, p_tail = 0, p_next = 0, p_t = wall_clock64();
 #define FLOW_PROF_MARK(acc)                                 \
@@ -416,14 +419,10 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
         RepVal rv2;
         int rdy3 = kFlowDone;
         StepIn in4;
-        if constexpr (kPipe) {
-            nmeta = pipe_build(P.in1, P.rdy1, P.rv1, q - 64 - lane, top, &nrec, &nlbb);
-            rv2 = pipe_rv(w, lb, P.in2, P.rdy2, q - 128 - lane, top);  // issued now, used a chunk later
-            rdy3 = pipe_rdy(w, lb, P.in3, q - 192 - lane, top);
-            in4 = pipe_in(w, lb, q - 256 - lane, top);
-        } else {
-            nmeta = flow_resolve(w, lb, q - 64 - lane, top, &nrec, &nlbb);
-        }
+        nmeta = pipe_build(P.in1, P.rdy1, P.rv1, q - 64 - lane, top, &nrec, &nlbb);
+        rv2 = pipe_rv(w, lb, P.in2, P.rdy2, q - 128 - lane, top);  // issued now, used a chunk later
+        rdy3 = pipe_rdy(w, lb, P.in3, q - 192 - lane, top);
+        in4 = pipe_in(w, lb, q - 256 - lane, top);
         const unsigned long long blocked = __ballot(!(meta & kLongOk));
         const unsigned long long tops = __ballot((meta & kLongOk) && (meta & kStepTop));
         const int fb = blocked ? __ffsll((long long)blocked) - 1 : 64;
@@ -633,24 +632,20 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             meta = flow_resolve(w, lb, q - lane, top, &rec, &lbb, pb);
             buf[cb][lane] = rec;
             curlk = rec.lk;
-            if constexpr (kPipe) {  // the stages were for the old cursor
-                pipe_restart(w, lb, q, top, lane, P);
-                ++restarts;
-            }
+            pipe_restart(w, lb, q, top, lane, P);  // the stages were for the old cursor
+            ++restarts;
             continue;
         }
         q -= 64;
         cb ^= 1;
         meta = nmeta;
         lbb = nlbb;
-        if constexpr (kPipe) {
-            P.in1 = P.in2;
-            P.rdy1 = P.rdy2;
-            P.rv1 = rv2;
-            P.in2 = P.in3;
-            P.rdy2 = rdy3;
-            P.in3 = in4;
-        }
+        P.in1 = P.in2;
+        P.rdy1 = P.rdy2;
+        P.rv1 = rv2;
+        P.in2 = P.in3;
+        P.rdy2 = rdy3;
+        P.in3 = in4;
         FLOW_PROF_MARK(p_tail);
         buf[cb][lane] = nrec;
         curlk = nrec.lk;
@@ -831,6 +826,7 @@ __device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int 
                 if (t < 0) break;
             } else if (f_poll(ctl + FC_SHORT_NEXT) < ntot) {
                 t = kFlowHelpTask;
+                break;
             } else {
                 __builtin_amdgcn_s_sleep(32);
             }
@@ -854,7 +850,7 @@ __device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int 
 // Measured (112 frames, 1080p, tools/flow_stats.py, serial): short paths done at 26.7 ms, the last
 // chain at 42.4 ms; same-box bench 1,518-1,540 Mpixels/s with 128 long and 2,048 short workers.
 template <bool kLong, int kW>
-__global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigned epoch, int keyfast, int pipe) {
+__global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigned epoch, int keyfast) {
     __shared__ OneRec buf[kLong ? kW : 1][2][64];
     __shared__ __attribute__((aligned(16))) OneOut ob[kLong ? kW : 1][128];
     const int lane = threadIdx.x & 63;
@@ -876,8 +872,7 @@ __global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigne
             const unsigned long long t1 = fs_now();
             while (t >= 0) {
                 if (lane == 0) fs_add(ctl, FS_LRUNS, 1);
-                const int nx = pipe ? flow_long<true>(w, ctl, t, buf[wv], ob[wv], keyfast)
-                                    : flow_long<false>(w, ctl, t, buf[wv], ob[wv], keyfast);
+                const int nx = flow_long(w, ctl, t, buf[wv], ob[wv], keyfast);
                 if (nx >= 0 && !(nx & kFlowLong)) {  // a short waiter: a one-lane short round (and its waiters)
                     if (lane == 0) fs_add(ctl, FS_INJECT, 1);
                     flow_short(w, ctl, epoch, nx, 0, 0, &cb, &ce);

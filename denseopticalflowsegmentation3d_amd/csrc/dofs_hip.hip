@@ -50,6 +50,7 @@ __device__ inline int dofs_aadd(int* p, int v) { return atomicAdd(p, v); }
 __device__ inline void dofs_aor(int* p, int v) { atomicOr(p, v); }
 
 #include "dofs_common.h"
+#include "dofs_knobs.h"
 
 // Keyed atomic updates aggregated across the wave: when all 64 lanes are present, the lanes whose
 // key equals the first active lane's key are reduced with cross-lane shuffles and updated by one
@@ -248,85 +249,16 @@ struct takes<F, std::void_t<decltype(F::kBlockTake)>> : std::true_type {};
 
 
 // ---------------------------------------------------------------------------------------------
-// K5 (long heavy paths): three wave64s per path. The float running mean of Forest::merge
-// (graph.cpp:184-190) is a strictly sequential recurrence — f32 mul, f32 add, cvt, f64 mul, cvt per
-// merge — whose roundings must be replayed in Kruskal order. Waves 0 and 1 carry only that chain
-// (mean x, mean y; one per SIMD: tools/replay_micro.hip measured 41 ns/step against 54 for one wave
-// doing both); wave 2 carries the union-by-rank rank/root recurrence and the bbox. Per 64-step
-// chunk every lane resolves one position's inputs (StepIn, plus the light child's replay output
-// when it is a merge node) into its wave's LDS records while the previous chunk is consumed; the
-// chains read step k with uniform LDS loads and write step k's output to LDS; one coalesced store
-// per chunk writes the outputs back by preorder position.
+// K5 support: the replay's step records, staged in LDS by the long-path workers (dofs_dataflow.h).
+// Rank and root of a running set travel as one key K = rank << 27 | root (H*W < 2^26, rank <= 26): the
+// union-by-rank step (step_merge, graph.cpp:177-182, 210-213) becomes K' = max(K, LK) for unequal ranks
+// and, for equal ranks, (B ? LK : K) + (1 << 27) — five VALU ops instead of eleven, which matters because
+// one wave issues at most one instruction per four cycles and the chain loop is issue-bound.
 // ---------------------------------------------------------------------------------------------
-struct ChainRec {  // wave 0/1 step record (16 B)
-    float fs;
-    float wb;
-    double r;
-};
-struct SideRec {  // wave 2 step record (16 B)
-    int meta;     // StepIn meta | kLongOk
-    int lrank;
-    int lroot;
-    int pad;
-};
-constexpr int kLongOk = 8;
-
-struct LongShared {
-    ChainRec chain[2][2][64];  // [wave][buffer][step]
-    SideRec side[2][64];       // [buffer][step]
-    float om[2][2][64];        // [buffer][wave][step]: the chains' outputs, stored by wave 2
-    int go;                    // blocked step: 1 = its light child completed (continue), 0 = park
-};
-constexpr unsigned long long kSpinTicks = 5000000ull;  // 50 ms of s_memrealtime (100 MHz)
+constexpr int kLongOk = 8;  // meta flag: the step's inputs are resolved
 #ifndef DOFS_SPIN_SLEEP
 #define DOFS_SPIN_SLEEP 8  // s_sleep units (64 cycles) between polls of a flag another workgroup sets
 #endif
-
-// Resolve position p for wave `wv`. Returns the meta flags (kLongOk when the inputs are ready).
-__device__ inline int long_resolve(const Ws& w, int64_t lb, int p, int top, int round, int wv, ChainRec* cr,
-                                   SideRec* sr, B4* lbb, int accept = -1) {
-    lbb->x0 = lbb->y0 = 0x7fff;  // neutral for the bbox scan (positions past the stop)
-    lbb->x1 = lbb->y1 = -1;
-    if (p < top) return 0;
-    const StepIn in = w.In[lb + p];
-    int meta = in.meta;
-    float wb;
-    int lrank = 0, lroot = in.lb;
-    if (in.meta & kStepDyn) {
-        const int lq = in.lb;
-        // light child not complete in an earlier phase (or, at `accept`, in this one — the long-path
-        // pass 2*round+1 — whose producer's release this workgroup acquired)
-        const int phase = 2 * round + 1;
-        if (w.ready[lb + lq] >= (p == accept ? phase + 1 : phase)) return meta;
-        if (wv < 2) {
-            wb = (wv ? w.Rv[lb + lq].my : w.Rv[lb + lq].mx) * (float)in.la;
-        } else {
-            wb = 0.f;
-            const RepVal lv = w.Rv[lb + lq];
-            lrank = lv.rank;
-            lroot = lv.root;
-            *lbb = lv.bb;
-        }
-    } else {
-        wb = wv ? in.wby : in.wbx;
-        if (wv == 2) {
-            lbb->x0 = lbb->x1 = (int16_t)(in.la & 0xffff);
-            lbb->y0 = lbb->y1 = (int16_t)(in.la >> 16);
-        }
-    }
-    meta |= kLongOk;
-    if (wv < 2) {
-        cr->fs = in.fs;
-        cr->wb = wb;
-        cr->r = in.r;
-    } else {
-        sr->meta = meta;
-        sr->lrank = lrank;
-        sr->lroot = lroot;
-        sr->pad = 0;
-    }
-    return meta;
-}
 
 __device__ inline B4 bb_join(B4 a, B4 b) {
     B4 r;
@@ -347,176 +279,6 @@ __device__ inline B4 bb_shfl_up(B4 b, int delta) {
     return r;
 }
 
-__device__ void replay_long_path(const Ws& w, int f, int jj, int round, bool can_wait, LongShared& sh) {
-    const Dims& d = w.d;
-    const int j = w.list_long[f * d.N + jj];
-    int* curp = w.cur + f * d.N + j;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform role
-    const int lane = threadIdx.x & 63;
-    int q = *curp;
-    const int top = w.ptop[f * d.N + j];
-    __syncthreads();  // every wave has read the cursor before it may be rewritten
-    if (q < 0) return;
-    const int64_t lb = f * d.NL;
-    float m = 0.f;
-    int rank = 0, root = 0;
-    B4 bb;
-    bb.x0 = bb.y0 = bb.x1 = bb.y1 = 0;
-    {
-        float mx, my;
-        path_start(w, f, q + 1, &mx, &my, &rank, &root, &bb);
-        m = wv == 0 ? mx : my;
-    }
-    int cb = 0;
-    ChainRec cr;
-    SideRec sr;
-    B4 lbb;
-    int meta = long_resolve(w, lb, q - lane, top, round, wv, &cr, &sr, &lbb);
-    if (wv < 2)
-        sh.chain[wv][cb][lane] = cr;
-    else
-        sh.side[cb][lane] = sr;
-    for (;;) {
-        ChainRec ncr;
-        SideRec nsr;
-        B4 nlbb;
-        const int nmeta = long_resolve(w, lb, q - 64 - lane, top, round, wv, &ncr, &nsr, &nlbb);
-        // steps to run in this chunk: up to the first blocked position or through the path top
-        const unsigned long long blocked = __ballot(!(meta & kLongOk));
-        const unsigned long long tops = __ballot((meta & kLongOk) && (meta & kStepTop));
-        const int fb = blocked ? __ffsll((long long)blocked) - 1 : 64;
-        const int ft = tops ? __ffsll((long long)tops) - 1 : 64;
-        const int finished = ft < fb;
-        const int n = finished ? ft + 1 : fb;
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS records have landed
-        __builtin_amdgcn_wave_barrier();
-        // the loops read their step records from LDS and keep step k's output in lane k (no LDS
-        // stores inside the loop, so the compiler can issue the record loads ahead of the chain)
-        float om = 0.f;
-        int orank = 0, oroot = 0;
-        B4 obb;
-        if (wv < 2) {
-            const ChainRec* c = sh.chain[wv][cb];
-#pragma unroll 8
-            for (int k = 0; k < n; ++k) {
-                const ChainRec st = c[k];
-                m = (float)((double)(m * st.fs + st.wb) * st.r);
-                om = lane == k ? m : om;
-            }
-        } else {
-            const SideRec* c = sh.side[cb];
-#pragma unroll 8
-            for (int k = 0; k < n; ++k) {
-                const SideRec st = c[k];
-                const int nroot = (st.meta & kStepB) ? (rank > st.lrank ? root : st.lroot)
-                                                     : (st.lrank > rank ? st.lroot : root);
-                rank = (rank == st.lrank) ? rank + 1 : (rank > st.lrank ? rank : st.lrank);
-                root = nroot;
-                orank = lane == k ? rank : orank;
-                oroot = lane == k ? root : oroot;
-            }
-            // bbox: inclusive prefix join over the chunk (lane = step), then the carried box
-            B4 x = lbb;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const B4 y = bb_shfl_up(x, o);
-                if (lane >= o) x = bb_join(x, y);
-            }
-            x = bb_join(x, bb);
-            obb = x;
-            {
-                const int src = n > 0 ? n - 1 : 0;
-                const int lo = __shfl((int)((unsigned short)x.x0 | ((unsigned)(unsigned short)x.y0 << 16)), src, 64);
-                const int hi = __shfl((int)((unsigned short)x.x1 | ((unsigned)(unsigned short)x.y1 << 16)), src, 64);
-                if (n > 0) {
-                    bb.x0 = (int16_t)(lo & 0xffff);
-                    bb.y0 = (int16_t)(lo >> 16);
-                    bb.x1 = (int16_t)(hi & 0xffff);
-                    bb.y1 = (int16_t)(hi >> 16);
-                }
-            }
-        }
-        // the chunk's records: the chains hand their outputs to wave 2 through LDS (double-buffered
-        // by chunk parity), which stores each step's 32-byte record, 64 steps contiguous
-        if (wv < 2) sh.om[cb][wv][lane] = om;
-        __syncthreads();
-        if (wv == 2 && lane < n) {
-            RepVal o;
-            o.mx = sh.om[cb][0][lane];
-            o.my = sh.om[cb][1][lane];
-            o.rank = orank;
-            o.root = oroot;
-            o.bb = obb;
-            o.pad0 = o.pad1 = 0;
-            w.Rv[lb + q - lane] = o;
-        }
-        if (finished) {
-            // publish the path top: every wave's output stores, then one agent-scope release, then
-            // the flag (a consumer spinning in this round acquires before reading the outputs)
-            __syncthreads();
-            if (threadIdx.x == 128) {
-                *curp = -1;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                __hip_atomic_store(w.ready + lb + top, 2 * round + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            return;
-        }
-        if (n < 64) {
-            // blocked at position pb: its light child is a heavy-path top not complete in an earlier
-            // round. A long path (kPendLong) may complete in this round: wait for it (bounded), then
-            // continue; a short path or a path that parked this round: park until the next round.
-            const int pb = q - n;
-            __syncthreads();
-            if (threadIdx.x == 128) {
-                const int lq = w.In[lb + pb].lb;
-                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                int rd;
-                for (;;) {
-                    rd = __hip_atomic_load(w.ready + lb + lq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (!can_wait || rd <= 2 * round + 1 || rd == kIntMax || rd == kParkBase - round) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) break;
-                    __builtin_amdgcn_s_sleep(DOFS_SPIN_SLEEP);
-                }
-                const int go = rd <= 2 * round + 1;
-                sh.go = go;
-                if (go) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                } else {
-                    *curp = pb;
-                    __hip_atomic_store(w.ready + lb + top, kParkBase - round, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            __syncthreads();
-            if (!sh.go) return;
-            q = pb;  // re-resolve the chunk from the blocked step into the buffer just consumed
-            meta = long_resolve(w, lb, q - lane, top, round, wv, &cr, &sr, &lbb, pb);
-            if (wv < 2)
-                sh.chain[wv][cb][lane] = cr;
-            else
-                sh.side[cb][lane] = sr;
-            continue;
-        }
-        q -= 64;
-        cb ^= 1;
-        meta = nmeta;
-        lbb = nlbb;
-        if (wv < 2)
-            sh.chain[wv][cb][lane] = ncr;
-        else
-            sh.side[cb][lane] = nsr;
-    }
-}
-
-// One-wave form (default; DOFS_LONG_WAVES=3 selects the three-wave kernel below): a single wave64 per
-// long path carries both mean chains (independent, so they interleave), the rank/root recurrence
-// and the bbox. Each step's chain latency grows (~54 vs 41 ns, tools/replay_micro.hip) but the
-// path holds a third of the wave slots, which the graph stage of the next batches running beside it
-// uses: +1.5 % end to end at B = 96 once the graph stage got shorter than the replay stage's slack.
-// Rank and root of a running set travel as one key K = rank << 27 | root (H*W < 2^26, rank <= 26): the
-// union-by-rank step (step_merge) becomes K' = max(K, LK) for unequal ranks and, for equal ranks,
-// (B ? LK : K) + (1 << 27) — five VALU ops instead of eleven, which matters because one wave issues at
-// most one instruction per four cycles and this loop is issue-bound, not latency-bound.
 constexpr int kRankShift = 27;
 __device__ inline unsigned rk_pack(int rank, int root) { return ((unsigned)rank << kRankShift) | (unsigned)root; }
 struct alignas(16) OneHalf {  // the part of a step record one chain reads: x (even lanes) or y (odd lanes)
@@ -535,215 +297,6 @@ struct OneOut {  // per-step chain outputs, staged in LDS (one ds_write_b64 per 
     float v;     // mx (h = 0) or my (h = 1)
     unsigned k;  // key
 };
-__device__ inline int one_resolve(const Ws& w, int64_t lb, int p, int top, int round, OneRec* o, B4* lbb,
-                                  int accept = -1) {
-    lbb->x0 = lbb->y0 = 0x7fff;
-    lbb->x1 = lbb->y1 = -1;
-    if (p < top) return 0;
-    const StepIn in = w.In[lb + p];
-    int meta = in.meta;
-    int lrank = 0, lroot = in.lb;
-    if (in.meta & kStepDyn) {
-        const int lq = in.lb;
-        const int phase = 2 * round + 1;
-        if (w.ready[lb + lq] >= (p == accept ? phase + 1 : phase)) return meta;
-        const RepVal lv = w.Rv[lb + lq];
-        o->h[0].wb = lv.mx * (float)in.la;
-        o->h[1].wb = lv.my * (float)in.la;
-        lrank = lv.rank;
-        lroot = lv.root;
-        *lbb = lv.bb;
-    } else {
-        o->h[0].wb = in.wbx;
-        o->h[1].wb = in.wby;
-        lbb->x0 = lbb->x1 = (int16_t)(in.la & 0xffff);
-        lbb->y0 = lbb->y1 = (int16_t)(in.la >> 16);
-    }
-    meta |= kLongOk;
-    o->h[0].fs = o->h[1].fs = in.fs;
-    o->h[0].r = o->h[1].r = in.r;
-    o->pad = 0;
-    o->lk = rk_pack(lrank, lroot);
-    o->lkp = o->lk + (1u << kRankShift);
-    o->bm = (meta & kStepB) ? ~0u : 0u;
-    return meta;
-}
-
-__device__ void replay_long_path1(const Ws& w, int f, int jj, int round, bool can_wait, OneRec (*buf)[64],
-                                  OneOut* ob) {
-    const Dims& d = w.d;
-    const int j = w.list_long[f * d.N + jj];
-    int* curp = w.cur + f * d.N + j;
-    const int lane = threadIdx.x & 63;
-    int q = *curp;
-    const int top = w.ptop[f * d.N + j];
-    __builtin_amdgcn_wave_barrier();
-    if (q < 0) return;
-    const int64_t lb = f * d.NL;
-    const int h = lane & 1;  // even lanes carry the x mean, odd lanes the y mean: one instruction
-                             // stream advances both chains (the wave issues one VALU op per 4 cycles)
-    float v;
-    unsigned K;
-    B4 bb;
-    {
-        float mx, my;
-        int rank, root;
-        path_start(w, f, q + 1, &mx, &my, &rank, &root, &bb);
-        v = h ? my : mx;
-        K = rk_pack(rank, root);
-    }
-    int cb = 0;
-    OneRec rec;
-    B4 lbb;
-    int meta = one_resolve(w, lb, q - lane, top, round, &rec, &lbb);
-    buf[cb][lane] = rec;
-    for (;;) {
-        OneRec nrec;
-        B4 nlbb;
-        const int nmeta = one_resolve(w, lb, q - 64 - lane, top, round, &nrec, &nlbb);
-        const unsigned long long blocked = __ballot(!(meta & kLongOk));
-        const unsigned long long tops = __ballot((meta & kLongOk) && (meta & kStepTop));
-        const int fb = blocked ? __ffsll((long long)blocked) - 1 : 64;
-        const int ft = tops ? __ffsll((long long)tops) - 1 : 64;
-        const int finished = ft < fb;
-        const int n = finished ? ft + 1 : fb;
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this chunk's LDS records have landed
-        __builtin_amdgcn_wave_barrier();
-        const OneRec* c = buf[cb];
-        auto step = [&](int k, uint4 a, OneHalf b) {  // a = {lk, bm, lkp}, b = {r, wb, fs}
-            v = (float)((double)(v * b.fs + b.wb) * b.r);
-            const unsigned lk = a.x, bm = a.y, lkp = a.z;
-            unsigned eq = (bm & lkp) | (~bm & (K + (1u << kRankShift)));
-            unsigned ne = K > lk ? K : lk;
-            asm volatile("" : "+v"(eq), "+v"(ne));  // both arms in registers: a select, not a branch
-            K = (K ^ lk) < (1u << kRankShift) ? eq : ne;
-            OneOut o;
-            o.v = v;
-            o.k = K;
-            ob[2 * k + h] = o;
-        };
-        auto lda = [&](int k) { return *reinterpret_cast<const uint4*>(&c[k]); };
-        int k = 0;
-        // unrolled by hand (the asm barrier is convergent: no auto-unroll) and software-pipelined: the
-        // next group's records (indices wrapped into the 64-entry buffer) are read while this one runs
-        uint4 a0 = lda(0), a1 = lda(1), a2 = lda(2), a3 = lda(3);
-        OneHalf b0 = c[0].h[h], b1 = c[1].h[h], b2 = c[2].h[h], b3 = c[3].h[h];
-        for (; k + 4 <= n; k += 4) {
-            const int m = (k + 4) & 63;
-            const uint4 na0 = lda(m), na1 = lda(m + 1), na2 = lda(m + 2), na3 = lda(m + 3);
-            const OneHalf nb0 = c[m].h[h], nb1 = c[m + 1].h[h], nb2 = c[m + 2].h[h], nb3 = c[m + 3].h[h];
-            step(k, a0, b0);
-            step(k + 1, a1, b1);
-            step(k + 2, a2, b2);
-            step(k + 3, a3, b3);
-            a0 = na0, a1 = na1, a2 = na2, a3 = na3;
-            b0 = nb0, b1 = nb1, b2 = nb2, b3 = nb3;
-        }
-        for (; k < n; ++k) step(k, lda(k), c[k].h[h]);
-        B4 obb;
-        {  // bbox: inclusive prefix join over the chunk (lane = step), then the carried box
-            B4 x = lbb;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const B4 y = bb_shfl_up(x, o);
-                if (lane >= o) x = bb_join(x, y);
-            }
-            x = bb_join(x, bb);
-            obb = x;
-            const int src = n > 0 ? n - 1 : 0;
-            const int lo = __shfl((int)((unsigned short)x.x0 | ((unsigned)(unsigned short)x.y0 << 16)), src, 64);
-            const int hi = __shfl((int)((unsigned short)x.x1 | ((unsigned)(unsigned short)x.y1 << 16)), src, 64);
-            if (n > 0) {
-                bb.x0 = (int16_t)(lo & 0xffff);
-                bb.y0 = (int16_t)(lo >> 16);
-                bb.x1 = (int16_t)(hi & 0xffff);
-                bb.y1 = (int16_t)(hi >> 16);
-            }
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // the chunk's output records are in LDS
-        __builtin_amdgcn_wave_barrier();
-        if (lane < n) {
-            const OneOut sx = ob[2 * lane], sy = ob[2 * lane + 1];
-            RepVal o;
-            o.mx = sx.v;
-            o.my = sy.v;
-            o.rank = (int)(sx.k >> kRankShift);
-            o.root = (int)(sx.k & ((1u << kRankShift) - 1));
-            o.bb = obb;
-            o.pad0 = o.pad1 = 0;
-            w.Rv[lb + q - lane] = o;
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // ob reads done before the next chunk overwrites it
-        __builtin_amdgcn_wave_barrier();
-        if (finished) {  // publish the top: output stores, agent-scope release, then the flag
-            __builtin_amdgcn_s_waitcnt(0);
-            __builtin_amdgcn_wave_barrier();
-            if (lane == 0) {
-                *curp = -1;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                __hip_atomic_store(w.ready + lb + top, 2 * round + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            return;
-        }
-        if (n < 64) {  // blocked at pb: wait (bounded) for a long light child of this round, or park
-            const int pb = q - n;
-            int go = 0;
-            if (lane == 0) {
-                const int lq = w.In[lb + pb].lb;
-                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                int rd;
-                for (;;) {
-                    rd = __hip_atomic_load(w.ready + lb + lq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (!can_wait || rd <= 2 * round + 1 || rd == kIntMax || rd == kParkBase - round) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) break;
-                    __builtin_amdgcn_s_sleep(DOFS_SPIN_SLEEP);
-                }
-                go = rd <= 2 * round + 1;
-                if (go) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                } else {
-                    *curp = pb;
-                    __hip_atomic_store(w.ready + lb + top, kParkBase - round, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            go = __shfl(go, 0, 64);
-            if (!go) return;
-            q = pb;
-            __builtin_amdgcn_wave_barrier();
-            meta = one_resolve(w, lb, q - lane, top, round, &rec, &lbb, pb);
-            buf[cb][lane] = rec;
-            continue;
-        }
-        q -= 64;
-        cb ^= 1;
-        meta = nmeta;
-        lbb = nlbb;
-        buf[cb][lane] = nrec;
-    }
-}
-
-__global__ __launch_bounds__(64) void k_replay_long1(Ws w, int round, int wait) {
-    // the chain loop issues one instruction per slot it gets: it goes first in its SIMD's arbitration
-    // over the graph-stage waves sharing it (which are memory-bound and lose little)
-    __builtin_amdgcn_s_setprio(3);
-    __shared__ OneRec buf[2][64];
-    __shared__ OneOut ob[128];
-    const int f = blockIdx.y;
-    const int n = w.C(f)[C_LONG];
-    const bool can_wait = wait && n <= (int)gridDim.x;
-    for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path1(w, f, jj, round, can_wait, buf, ob);
-}
-
-__global__ __launch_bounds__(192) void k_replay_long(Ws w, int round, int wait) {
-    __shared__ LongShared sh;
-    const int f = blockIdx.y;
-    const int n = w.C(f)[C_LONG];
-    // waiting on another long path is safe only when every long path has its own workgroup
-    const bool can_wait = wait && n <= (int)gridDim.x;
-    for (int jj = blockIdx.x; jj < n; jj += gridDim.x) replay_long_path(w, f, jj, round, can_wait, sh);
-}
-
 }  // namespace dofs
 #include "dofs_dataflow.h"
 namespace dofs {
@@ -762,6 +315,9 @@ namespace dofs {
 #ifndef DOFS_DEEP_S
 #define DOFS_DEEP_S 2048
 #endif
+// host: the depths below 32 merges of an LDS KRT block as one register window pass (1, the default: deep
+// block 51.7 → 43.5 µs) or as union-find depths (0); dofs_debug_krt_deep_wave (tests/test_gpu_krt_dnc.py)
+inline int g_deep_wave = 1;
 constexpr int kDeepS = DOFS_DEEP_S;
 constexpr int kDeepK = 2 * kDeepS;              // distinct labels of a block (two per merge)
 constexpr int kDeepL = kDeepK + kDeepS;         // local label space
@@ -2273,11 +1829,6 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
     }
 }
 
-__global__ __launch_bounds__(kSeqT) void k_krt_seq(Ws w) {
-    __shared__ SweepShared sh;
-    krt_sweep(w, blockIdx.x, sh, nullptr);
-}
-
 // ---------------------------------------------------------------------------------------------
 // Borůvka per-pixel passes, four pixels per lane (one 16-byte label load): KBoruvkaHook and
 // KBoruvkaRelabelFind of dofs_kernels.h. A frame's unaligned head and tail (H*W % 4 != 0) run
@@ -2681,7 +2232,7 @@ __global__ __launch_bounds__(kFbT) void k_blur_fused(Ws w) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// K3 fused (default; DOFS_FUSED=0: k_krt_seq then k_dnc_deep): one persistent launch in which the
+// K3 fused: one persistent launch in which the
 // latency-bound sweeps and the LDS KRT blocks share the chip. Every workgroup first claims a frame's
 // sweep while any is unclaimed (a claimed sweep runs to its end without waiting on anything), then
 // takes LDS-KRT blocks in block-major order; a block waits (agent-scope poll of its frame's
@@ -2745,27 +2296,25 @@ __global__ __launch_bounds__(kDeepT) void k_krt_fused(Ws w, int* progress) {
 constexpr int kPreT = 1024, kPreK = kDeepTop / kPreT;
 static_assert(kPreK * kPreT == kDeepTop, "preorder sweep shape");
 constexpr int kPushLight = (int)0x80000000u;
-// steps: also the StepIn records (DOFS_PRE_STEPS); ordw: also the merges' ord[] entries (else KLeafPos
-// writes them, chip-wide after the sweep: random 4-byte stores from one CU are bound by its waves'
-// outstanding-store slots, not by bandwidth)
-__global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w, int steps, int ordw) {
+// The merges' ord[] entries and StepIn records are not written here (KLeafPos and KPathInit write them,
+// chip-wide after the sweep): random stores from the one CU of a frame's sweep are bound by its waves'
+// outstanding-store slots and sit inside its latency chain (round 4: −1.5 % and −0.3 % end to end).
+__global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w) {
     __shared__ int lpos[kDeepTop];
     const Dims& d = w.d;
     const int f = blockIdx.x;
     const int64_t lb = f * d.NL, eb = f * d.M;
     unsigned long long* J = w.J + lb;
     int* pre = w.pre + lb;
-    int* ord = w.ord + lb;
     const int tid = threadIdx.x;
     const int64_t nblk = (d.M + kDeepTop - 1) / kDeepTop;
     const int64_t root = d.N + d.M - 1;
     struct Node {  // a merge's static inputs (final until swept)
         unsigned long long v, hl;
         int a, b;
-        unsigned char lB, lt;  // light side, path-top flag (the epilogue's, for a merge under an in-block parent)
+        unsigned char lB;  // light side
     };
     Node nd[kPreK];
-    F2 lf[kPreK];  // the light child's blurred flow when it is a pixel (its StepIn, KPathInit's step_in)
     auto load = [&](int64_t blk, Node (&o)[kPreK]) {
         const int64_t s0 = blk * kDeepTop;
         const int cnt = (int)((d.M - s0) < kDeepTop ? (d.M - s0) : kDeepTop);
@@ -2778,25 +2327,10 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w, int steps, int ordw) 
                 o[k].a = w.lu[eb + s0 + t];
                 o[k].b = w.lv[eb + s0 + t];
                 o[k].lB = w.hlB[eb + s0 + t];
-                o[k].lt = w.lite[lb + d.N + s0 + t];
             }
         }
     };
-    const F2* bl = w.blur + f * d.N;
-    auto gather = [&](int64_t blk) {  // issued a block ahead of its use (after the block's inputs arrived)
-        const int64_t s0 = blk * kDeepTop;
-        const int cnt = (int)((d.M - s0) < kDeepTop ? (d.M - s0) : kDeepTop);
-#pragma unroll
-        for (int k = 0; k < kPreK; ++k) {
-            const int t = tid + k * kPreT;
-            const int l = nd[k].lB ? nd[k].b : nd[k].a;
-            if (t < cnt && l < d.N) lf[k] = bl[l];
-        }
-    };
-    if (nblk > 0) {
-        load(nblk - 1, nd);
-        if (steps) gather(nblk - 1);
-    }
+    if (nblk > 0) load(nblk - 1, nd);
     KT_DECL
     for (int64_t blk = nblk - 1; blk >= 0; --blk) {
         const int64_t s0 = blk * kDeepTop, x0 = d.N + s0;
@@ -2830,33 +2364,18 @@ __global__ __launch_bounds__(kPreT) void k_pre_sweep(Ws w, int steps, int ordw) 
             const int64_t x = x0 + t;
             if (!top[k]) pos[k] = jump_sum(nd[k].v) + lpos[jump_anc(nd[k].v) - x0];
             pre[x] = pos[k];  // (the converged word is not needed: nothing reads J after this pass)
-            if (ordw) ord[pos[k]] = (int)x;
             // push the merge children outside the block (tops of earlier blocks) their positions;
             // the leaves get theirs from KLeafPos, in parallel after the sweep
             const int sh = (int)(unsigned)(nd[k].hl & 0xffffffffu);
             const int h = nd[k].lB ? nd[k].a : nd[k].b, l = nd[k].lB ? nd[k].b : nd[k].a;
             if (h < x0 && h >= d.N) pre[h] = pos[k] + 1;
             if (l < x0 && l >= d.N) pre[l] = (pos[k] + 2 * sh) | kPushLight;
-            // the merge's replay inputs at its position (KPathInit's step_in, the same record; random
-            // 32-B stores, fire and forget): a top's path-top flag is its push's, a merge under an
-            // in-block parent has its flag from the KRT epilogue
-            if (steps) {
-                const bool ptop = top[k] ? (x == root || (pushed[k] & kPushLight)) : nd[k].lt != 0;
-                StepIn in;
-                if (l < d.N) {
-                    in = step_in_leaf(nd[k].hl, ptop, nd[k].lB, l, lf[k], d.W, w.min_size);
-                } else {
-                    in = step_in(w, f, pos[k], ptop, l, nd[k].lB, nd[k].hl);  // (a merge light child: no load)
-                }
-                w.In[lb + pos[k]] = in;
-            }
         }
         KT(15);
         __syncthreads();  // the pushes are read by the blocks below
         if (blk > 0) {
 #pragma unroll
             for (int k = 0; k < kPreK; ++k) nd[k] = nx[k];
-            if (steps) gather(blk - 1);
         }
         KT(16);
     }
@@ -2957,7 +2476,8 @@ struct HipBackend {
         return std::string(prop.gcnArchName).rfind("gfx950", 0) == 0;
     }
 
-    explicit HipBackend(int dev) : device(dev) {
+    Knobs kn;  // the context's runtime knobs (dofs_knobs.h), read when it was created
+    explicit HipBackend(int dev) : device(dev), kn(knobs()) {
         note(hipSetDevice(dev), "hipSetDevice");
         note(hipStreamCreateWithFlags(&own, hipStreamNonBlocking), "hipStreamCreate");
         stream = own;
@@ -3102,39 +2622,23 @@ struct HipBackend {
 
     // total workgroups of one grid-stride launch (all frames): enough to fill 256 CUs several
     // times over, few enough that near-empty passes (converged rounds) cost little to dispatch
-    static int64_t grid_cap() {
-        static const int64_t cap = [] {
-            const char* e = getenv("DOFS_GRID_CAP");
-            return e ? (int64_t)atoll(e) : (int64_t)16384;
-        }();
-        return cap;
-    }
+    // (round 4, same box: a cap of 32,768 1,752-1,759 Mpix/s, 8,192 1,719-1,725, uncapped 1,622-1,628 against
+    // 1,781-1,785 at 16,384 — converged Borůvka rounds pay for their grids)
+    static constexpr int64_t grid_cap() { return 16384; }
     // The preorder-position scatters (KLeafPos, KLeafOrder, KPathInit) read and write one frame's
     // position-indexed arrays at random. Launched uncapped, one lane per merge, the dispatcher hands out
-    // workgroups frame by frame (blockIdx.x fastest), so the chip works on about one frame's arrays
-    // at a time and their random lines stay in the memory-side cache instead of spanning the batch.
-    // DOFS_FRAME_MAJOR=0: the capped grid-stride launch of every other kernel; 2: also the scoring
-    // stage's gathers (KFilter, KSnapshot, KLabel, KSlotInit)
-    static int frame_major_mode() {
-        static const int m = [] {
-            const char* e = getenv("DOFS_FRAME_MAJOR");
-            return e ? atoi(e) : 1;
-        }();
-        return m;
-    }
+    // workgroups frame by frame (blockIdx.x fastest), and short workgroups hand their CU slots back within
+    // microseconds to the graph stage's urgent kernels (round 4, same box: 1,749-1,751 → 1,778-1,779
+    // Mpix/s; the scoring gathers launched the same way were 0.3 % slower)
     template <class F>
-    static bool frame_major() {
-        const int m = frame_major_mode();
-        if (m >= 1 && (std::is_same_v<F, KPathInit> || std::is_same_v<F, KLeafOrder> || std::is_same_v<F, KLeafPos>))
-            return true;
-        return m >= 2 && (std::is_same_v<F, KFilter> || std::is_same_v<F, KSnapshot> || std::is_same_v<F, KLabel> ||
-                          std::is_same_v<F, KSlotInit>);
+    static constexpr bool frame_major() {
+        return std::is_same_v<F, KPathInit> || std::is_same_v<F, KLeafOrder> || std::is_same_v<F, KLeafPos>;
     }
     template <class F>
     static int launch_on(hipStream_t s, int nf, int64_t n, const F& f) {
         if (n <= 0 || nf <= 0) return DOFS_OK;
         int64_t gx = (n + kBlock - 1) / kBlock;
-        const int64_t cap = grid_cap() > 0 ? std::max<int64_t>(1, grid_cap() / nf) : 8192;
+        const int64_t cap = std::max<int64_t>(1, grid_cap() / nf);
         if (gx > cap && !(frame_major<F>() && gx <= (int64_t)1 << 30)) gx = cap;
         if constexpr (takes<F>::value)
             hipLaunchKernelGGL(k_generic_take<F>, dim3((unsigned)gx, (unsigned)nf), dim3(kBlock), 0, s, f, n);
@@ -3244,7 +2748,7 @@ struct HipBackend {
     void launch_counted(int nf, int64_t n, const F& f, int cidx, int zidx = -1) {
         if (n <= 0 || nf <= 0) return;
         int64_t gx = (n + kBlock - 1) / kBlock;
-        const int64_t cap = grid_cap() > 0 ? std::max<int64_t>(1, grid_cap() / nf) : 8192;
+        const int64_t cap = std::max<int64_t>(1, grid_cap() / nf);
         if (gx > cap) gx = cap;
         timed(functor_name<F>(), [&] {
             hipLaunchKernelGGL(k_counted_take<F>, dim3((unsigned)gx, (unsigned)nf), dim3(kBlock), 0, stream, f, n, cidx,
@@ -3256,11 +2760,7 @@ struct HipBackend {
     void dnc_parent(const Ws&) {}  // done by k_dnc_deep's epilogue
     void blur(const Ws& w) {  // KBlurRow + KBlurCol, LDS-tiled
         const int64_t cap = std::max<int64_t>(1, grid_cap() / w.d.B);
-        static const bool fused_on = [] {
-            const char* e = getenv("DOFS_BLUR_FUSED");
-            return !(e && e[0] == '0');
-        }();
-        if (fused_on && w.bn == 2 * kFbR + 1 && w.d.W >= 128 && w.d.H >= 64) {  // sigma = 3: one pass
+        if (w.bn == 2 * kFbR + 1 && w.d.W >= 128 && w.d.H >= 64) {  // sigma = 3: one pass
             const int64_t ft = (int64_t)((w.d.W + kFbW - 1) / kFbW) * ((w.d.H + kFbH - 1) / kFbH);
             timed("k_blur_fused", [&] {
                 hipLaunchKernelGGL(k_blur_fused, dim3((unsigned)std::min(ft, cap), (unsigned)w.d.B), dim3(kFbT), 0,
@@ -3293,68 +2793,35 @@ struct HipBackend {
     // longest pointer chain the preorder's global jumping starts from: every word leaves its block
     // or goes to the block's top, so at most two words per block on any path
     static int64_t jump_chain_bound(int64_t M) { return 2 * ((M + kDeepTop - 1) / kDeepTop) + 1; }
-    static bool fused() {
-        static const bool on = [] {
-            const char* e = getenv("DOFS_FUSED");
-            return !(e && e[0] == '0');
-        }();
-        return on;
-    }
+    // the frames' sweeps + the LDS KRT in one persistent launch (k_krt_fused), one 1,024-thread workgroup per
+    // CU: a workgroup holds a whole CU (151 KB of LDS, all VGPRs). With the graph stage urgent and the
+    // constant-key replay (round 3, B = 112, same box) every CU: 256 workgroups 1,593 / 1,586 / 1,584 / 1,587
+    // Mpix/s against 240 (1/16 of the CUs left to the replay) 1,551 / 1,543 / 1,549 / 1,544
     void krt_seq(const Ws& w) {
-        if (fused()) {  // sweep + LDS KRT in one persistent launch (k_krt_fused); dnc_deep is a no-op
-            launch(w.d.B, w.d.N, KSeqInitRec{reinterpret_cast<SeqRec*>(w.In), 2 * w.d.NL});
-            // persistent workgroups: the frames' sweeps plus `extra` LDS-KRT workers (DOFS_FUSED_EXTRA),
-            // at most one per CU. A workgroup holds a whole CU (151 KB of LDS, all VGPRs), so the
-            // other stream's replay cannot run beside it. With the graph stage urgent and the
-            // constant-key replay (round 3, B = 112, same box) every CU: 256 workgroups 1,593 / 1,586 /
-            // 1,584 / 1,587 Mpix/s against 240 (1/16 of the CUs left to the replay, the earlier default)
-            // 1,551 / 1,543 / 1,549 / 1,544; round 2's round-based replay needed 1/8 free: 224 982, 256 957
-            static const int extra = [] {
-                const char* e = getenv("DOFS_FUSED_EXTRA");
-                return e ? atoi(e) : -1;
-            }();
-            int dev_cus = 256;
-            (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, device);
-            const int cap = dev_cus;
-            const int nwg = std::max(1, std::min(cap, extra < 0 ? cap : w.d.B + extra));
-            Ws wk = w;
-            wk.deep_wave = deep_wave_on() ? 1 : 0;
-            timed("k_krt_fused", [&] {
-                hipLaunchKernelGGL(k_krt_fused, dim3((unsigned)nwg), dim3(kDeepT), 0, stream, wk, w.ctr + C_PROG);
-            });
-            if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_krt_fused launch");
-            fused_done = true;
-            return;
-        }
-        swept_top = true;
         launch(w.d.B, w.d.N, KSeqInitRec{reinterpret_cast<SeqRec*>(w.In), 2 * w.d.NL});
-        timed("k_krt_seq", [&] {
-            hipLaunchKernelGGL(k_krt_seq, dim3((unsigned)w.d.B), dim3(kSeqT), 0, stream, w);
+        int nwg = 256;
+        (void)hipDeviceGetAttribute(&nwg, hipDeviceAttributeMultiprocessorCount, device);
+        Ws wk = w;
+        wk.deep_wave = g_deep_wave;
+        timed("k_krt_fused", [&] {
+            hipLaunchKernelGGL(k_krt_fused, dim3((unsigned)std::max(1, nwg)), dim3(kDeepT), 0, stream, wk, w.ctr + C_PROG);
         });
-        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_krt_seq launch");
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_krt_fused launch");
+        fused_done = true;
     }
-    bool fused_done = false;  // the last krt_seq already ran the LDS KRT
-    bool swept_top = false;   // the last krt_seq (unfused) did the blocks' top level
+    bool fused_done = false;  // the last krt_seq already ran the LDS KRT (k_krt_fused)
     void dnc_deep(const Ws& w) {
         if (fused_done) {
             fused_done = false;
             return;
         }
         const unsigned nb = (unsigned)((w.d.M + kDeepTop - 1) / kDeepTop);
-        const int top = swept_top ? 0 : 1;  // DOFS_KRT_DNC: the global depths stop above the block
-        swept_top = false;
         Ws wk = w;
-        wk.deep_wave = deep_wave_on() ? 1 : 0;
-        timed("k_dnc_deep", [&] {
-            hipLaunchKernelGGL(k_dnc_deep, dim3(nb, (unsigned)w.d.B), dim3(kDeepT), 0, stream, wk, top);
+        wk.deep_wave = g_deep_wave;
+        timed("k_dnc_deep", [&] {  // after the top-down global depths (DNC KRT): the block's top level too
+            hipLaunchKernelGGL(k_dnc_deep, dim3(nb, (unsigned)w.d.B), dim3(kDeepT), 0, stream, wk, 1);
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_dnc_deep launch");
-    }
-    // DOFS_DEEP_WAVE=0: the LDS KRT's depths below 32 merges by the union-find depths instead of the
-    // one-pass window form (read per batch, for A/B runs on one library)
-    static bool deep_wave_on() {
-        const char* e = getenv("DOFS_DEEP_WAVE");
-        return !(e && e[0] == '0');
     }
     void boruvka_hook(const Ws& w, int r) {
         if (rec_path(w)) {
@@ -3374,48 +2841,28 @@ struct HipBackend {
             launch(w.d.B, w.d.M, KOrdMerge{w});
         } else {
             timed("k_pre_sweep", [&] {
-                hipLaunchKernelGGL(k_pre_sweep, dim3((unsigned)w.d.B), dim3(kPreT), 0, stream, w, pre_steps_on() ? 1 : 0,
-                                   pre_ord_on() ? 1 : 0);
+                hipLaunchKernelGGL(k_pre_sweep, dim3((unsigned)w.d.B), dim3(kPreT), 0, stream, w);
             });
             if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_pre_sweep launch");
         }
-        pre_steps_done = !w.jscatter && pre_steps_on();  // the sweep wrote every StepIn (KPathInit: paths only)
-        if (!w.jscatter && !pre_ord_on())  // the merges' ord entries: the merge mark, one fill (KLeafPos)
+        if (!w.jscatter)  // the merges' ord entries: the merge mark, one fill (KLeafPos places the leaves)
             note(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.ord), kOrdMerge, (size_t)w.d.B * w.d.NL, stream),
                  "hipMemsetD32Async");
         launch(w.d.B, w.d.M, KLeafPos{w});
         return true;
     }
-    // K4 by jumping (Ws::jscatter) for batches of at most `pre_jump_frames` frames (DOFS_PRE_JUMP = the
-    // frame bound; 0 = always the sweep): the sweep is one workgroup per frame, so a lone 4K frame walks its
-    // ~2,000 KRT blocks on one CU while the rest of the chip idles
-    static int pre_jump_frames() {  // read per batch (tests switch it within one process)
-        const char* e = getenv("DOFS_PRE_JUMP");
-        return e ? atoi(e) : 8;
-    }
-    static bool pre_jump(const Dims& d) { return d.B <= pre_jump_frames(); }
-    bool pre_steps_done = false;  // the last pre_sweep wrote the StepIn records (k_pre_sweep)
-    // DOFS_PRE_STEPS=1: the preorder sweep writes the StepIn records instead of KPathInit (read per batch).
-    // Off by default: B = 112, one library, same box, three runs each: sweep-written 1,584 / 1,591 /
-    // 1,588 Mpix/s (preorder stage 25.3 ms), KPathInit-written 1,591 / 1,592 / 1,591 (24.7 ms)
-    static bool pre_steps_on() {
-        const char* e = getenv("DOFS_PRE_STEPS");
-        return e && e[0] == '1';
-    }
-    static bool pre_steps(const HipBackend& b) { return b.pre_steps_done; }
-    // DOFS_PRE_ORD=1: the preorder sweep writes the merges' ord[] entries (else KLeafPos; read per batch)
-    static bool pre_ord_on() {
-        const char* e = getenv("DOFS_PRE_ORD");
-        return e && e[0] == '1';
-    }
+    // K4 by jumping (Ws::jscatter) for batches of at most DOFS_PRE_JUMP frames (default 8; 0 = always the
+    // sweep): the sweep is one workgroup per frame, so a lone 4K frame walks its ~2,000 KRT blocks on one CU
+    // while the rest of the chip idles
+    bool pre_jump(const Dims& d) const { return d.B <= kn.pre_jump; }
     void boruvka_relabel(const Ws& w, int r) {
-        if (r >= 1 && rec_path(w) && relabel_tiles()) {  // round 0 runs before the tile flags exist
+        if (r >= 1 && rec_path(w)) {  // round 0 runs before the tile flags exist
             rec_launch(w, r, k_boruvka_relabel_t, "k_boruvka_relabelt");
             return;
         }
-        if (r == 0 && tile0_on() && w.d.W >= 3) {  // KBoruvkaPairs + the relabel's in-tile part, then tile hops
+        if (r == 0 && w.d.W >= 3) {  // KBoruvkaPairs + the relabel's in-tile part, then tile hops
             const int64_t tiles = (int64_t)((w.d.W + kT0X - 1) / kT0X) * ((w.d.H + kT0Y - 1) / kT0Y);
-            const int64_t cap = std::max<int64_t>(1, (grid_cap() > 0 ? grid_cap() : 8192) / w.d.B);
+            const int64_t cap = std::max<int64_t>(1, grid_cap() / w.d.B);
             timed("k_boruvka_tile0", [&] {
                 hipLaunchKernelGGL(k_boruvka_tile0, dim3((unsigned)std::min(tiles, cap), (unsigned)w.d.B), dim3(kT0T), 0,
                                    stream, w);
@@ -3426,22 +2873,9 @@ struct HipBackend {
         }
         pixel4(w, r, k_boruvka_relabel4<false>, "KBoruvkaRelabelFind");
     }
-    // DOFS_TILE0=0: round 0 by KBoruvkaPairs + k_boruvka_relabel4 over uf (else k_boruvka_tile0 + hops)
-    static bool tile0_on() {
-        static const bool on = [] {
-            const char* e = getenv("DOFS_TILE0");
-            return !(e && e[0] == '0');
-        }();
-        return on;
-    }
-    static bool pairs_in_relabel(const Ws& w) { return tile0_on() && w.d.W >= 3; }
-    static bool relabel_tiles() {  // DOFS_RELABEL_TILES=0: every pixel every round (k_boruvka_relabel4)
-        static const bool on = [] {
-            const char* e = getenv("DOFS_RELABEL_TILES");
-            return !(e && atoi(e) == 0);
-        }();
-        return on;
-    }
+    // round 0's pairs and relabel per LDS tile (k_boruvka_tile0) on frames at least 3 wide; narrower ones
+    // take KBoruvkaPairs + k_boruvka_relabel4 over uf
+    static bool pairs_in_relabel(const Ws& w) { return w.d.W >= 3; }
     void pixel4(const Ws& w, int r, void (*k)(Ws, int), const char* name) {
         const int64_t n4 = (w.d.N + 3) / 4;
         int64_t gx = (n4 + 255) / 256;
@@ -3457,11 +2891,7 @@ struct HipBackend {
     // the record-based rounds (k_boruvka_min4, ...): 16-byte label loads need W % 4 == 0; the tile
     // counts (u16) sit after the tile flags in the heavy/light bytes, which hold 3 bytes per tile
     static bool rec_path(const Ws& w) {
-        static const bool off = [] {
-            const char* e = getenv("DOFS_BORUVKA_REC");
-            return e && atoi(e) == 0;
-        }();
-        return !off && !w.allow && w.d.W % 4 == 0 && w.d.N >= 1024 && 3 * tile_count(w.d) + 2 <= w.d.M;
+        return !w.allow && w.d.W % 4 == 0 && w.d.N >= 1024 && 3 * tile_count(w.d) + 2 <= w.d.M;
     }
     RecBufs rec_bufs(const Ws& w) {
         const int64_t tiles = tile_count(w.d);
@@ -3473,17 +2903,10 @@ struct HipBackend {
         rb.tc = reinterpret_cast<unsigned short*>(w.hlB + ((tiles * w.d.B + 1) & ~(int64_t)1));
         return rb;
     }
-    // the late rounds' grids shrink (DOFS_BORUVKA_SHRINK: the first shrinking round, 0 = never): by round
-    // 11 of a 1080p batch few tiles are active, and a full grid of early-exiting workgroups per kernel cost
-    // ~40 µs, 4 kernels a round for the ~12 rounds until ceil(log2 N) + 2 (the tile loops are grid-stride,
-    // so any grid covers every tile)
-    static int boruvka_shrink() {
-        static const int v = [] {
-            const char* e = getenv("DOFS_BORUVKA_SHRINK");
-            return e ? atoi(e) : 11;
-        }();
-        return v;
-    }
+    // the late rounds' grids shrink from round 11: by then few tiles of a 1080p batch are active, and a full
+    // grid of early-exiting workgroups per kernel cost ~40 µs, 4 kernels a round for the ~12 rounds until
+    // ceil(log2 N) + 2 (the tile loops are grid-stride, so any grid covers every tile)
+    static constexpr int boruvka_shrink() { return 11; }
     void rec_launch(const Ws& w, int r, void (*k)(Ws, int, RecBufs), const char* name) {
         int64_t gx = std::min<int64_t>((tile_count(w.d) + 3) / 4, std::max<int64_t>(1, grid_cap() / w.d.B));
         const int sr = boruvka_shrink();
@@ -3531,67 +2954,21 @@ struct HipBackend {
         });
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_dnc_compress launch");
     }
-    static bool long_wait() {  // DOFS_LONG_WAIT=0: park instead of waiting on a running long path
-        static const bool on = [] {
-            const char* e = getenv("DOFS_LONG_WAIT");
-            return !(e && e[0] == '0');
-        }();
-        return on;
-    }
-    static int long_grid() {  // workgroups per frame of the long-path replay (DOFS_LONG_GRID)
-        static const int n = [] {
-            const char* e = getenv("DOFS_LONG_GRID");
-            const int v = e ? atoi(e) : 256;
-            return v > 0 ? v : 256;
-        }();
-        return n;
-    }
-    // K5 as one dataflow launch (dofs_dataflow.h); false: run the round launches (DOFS_REPLAY_FLOW=0, or a
-    // batch whose task ids would not fit 30 bits)
+    // K5 as one dataflow launch (dofs_dataflow.h): the round launches the emulator runs are not built here
+    static constexpr bool kReplayFlow = true;
     int* flow_ctl = nullptr;
     size_t flow_ctl_n = 0;
     hipStream_t flow_stream = nullptr;
     hipEvent_t flow_ev[2] = {nullptr, nullptr};
     unsigned flow_epoch = 0;
-    static int flow_grid() {  // short-path workers (waves) of the persistent replay
-        static const int g = [] {
-            const char* e = getenv("DOFS_FLOW_GRID");
-            return e && atoi(e) > 0 ? atoi(e) : 2048;
-        }();
-        return g;
-    }
-    // constant-key chunks in the long-path loop (dofs_dataflow.h): the chain carries only the mean where
-    // no step of a 64-step chunk reaches the carried rank. DOFS_KEYFAST=0 / 1; default on (96 % of the
-    // chunks; one 4K frame's replay 93 → 72 ms; B = 112 with the graph stage urgent, same box: 1,559 /
-    // 1,561 vs 1,546 / 1,535 Mpix/s)
-    static int keyfast(const Dims&) {
-        static const int m = [] {
-            const char* e = getenv("DOFS_KEYFAST");
-            return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
-        }();
-        return m >= 0 ? m : 1;
-    }
-    // pipelined resolve of the long paths' chunks (dofs_dataflow.h FlowPipe): DOFS_FLOW_PIPE=0 / 1, default 1
-    static int flow_pipe() {
-        static const int m = [] {
-            const char* e = getenv("DOFS_FLOW_PIPE");
-            return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : 1;
-        }();
-        return m;
-    }
-    static int flow_long_workers() {  // waves that run long paths (the rest of the grid runs short ones)
-        static const int g = [] {
-            const char* e = getenv("DOFS_FLOW_LONG");
-            return e && atoi(e) > 0 ? atoi(e) : 128;
-        }();
-        return g;
-    }
+    static constexpr int flow_grid() { return 2048; }  // short-path workers (waves; 1,024 and 4,096 measured equal)
+    // long-path workers (waves): DOFS_FLOW_LONG, default 128
+    int flow_long_workers() const { return kn.flow_long > 0 ? kn.flow_long : 128; }
     bool replay_flow(const Ws& w) {
-        static const bool on = [] {
-            const char* e = getenv("DOFS_REPLAY_FLOW");
-            return !(e && e[0] == '0');
-        }();
-        if (!on || (int64_t)w.d.B * w.d.N >= (int64_t)kFlowLong) return false;
+        if ((int64_t)w.d.B * w.d.N >= (int64_t)kFlowLong) {  // (api_run refuses such batches)
+            note(hipErrorInvalidValue, "batch too large for the replay's 30-bit task words");
+            return false;
+        }
         const size_t n = FC_HDR + 3 * (size_t)(w.d.B + 1);
         if (n > flow_ctl_n) {
             if (flow_ctl) {
@@ -3616,40 +2993,25 @@ struct HipBackend {
             const int gl = (flow_long_workers() + kFlowLongW - 1) / kFlowLongW;
             note(hipEventRecord(flow_ev[0], stream), "hipEventRecord");
             note(hipStreamWaitEvent(flow_stream, flow_ev[0], 0), "hipStreamWaitEvent");
-            const int kf = keyfast(w.d);
+            const int kf = g_keyfast;
             // g_flow_order (test entry dofs_debug_flow_order): 1 / 2 run the two launches one after the other on
             // one stream (long workers first / short workers first) — the replay must complete either way
             const int order = g_flow_order;
             hipStream_t ls = order ? stream : flow_stream;
             if (order != 2)
                 hipLaunchKernelGGL((k_replay_flow<true, kFlowLongW>), dim3((unsigned)gl), dim3(64 * kFlowLongW), 0, ls,
-                                   w, flow_ctl, flow_epoch, kf, flow_pipe());
+                                   w, flow_ctl, flow_epoch, kf);
             hipLaunchKernelGGL((k_replay_flow<false, kFlowShortW>), dim3((unsigned)gs), dim3(64 * kFlowShortW), 0, stream,
-                               w, flow_ctl, flow_epoch, kf, 0);
+                               w, flow_ctl, flow_epoch, kf);
             if (order == 2)
                 hipLaunchKernelGGL((k_replay_flow<true, kFlowLongW>), dim3((unsigned)gl), dim3(64 * kFlowLongW), 0, ls,
-                                   w, flow_ctl, flow_epoch, kf, flow_pipe());
+                                   w, flow_ctl, flow_epoch, kf);
             note(hipEventRecord(flow_ev[1], flow_stream), "hipEventRecord");
             note(hipStreamWaitEvent(stream, flow_ev[1], 0), "hipStreamWaitEvent");
         });
         hipLaunchKernelGGL(k_flow_report, dim3(1), dim3(64), 0, stream, w, flow_ctl);
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_replay_flow launch");
         return true;
-    }
-    void replay_long(const Ws& w, int round) {
-        static const bool one = [] {  // DOFS_LONG_WAVES=3: the three-wave form (measured ~1.5 % slower)
-            const char* e = getenv("DOFS_LONG_WAVES");
-            return !(e && e[0] == '3');
-        }();
-        timed("k_replay_long", [&] {
-            if (one)
-                hipLaunchKernelGGL(k_replay_long1, dim3((unsigned)long_grid(), (unsigned)w.d.B), dim3(64), 0, stream,
-                                   w, round, long_wait() ? 1 : 0);
-            else
-                hipLaunchKernelGGL(k_replay_long, dim3((unsigned)long_grid(), (unsigned)w.d.B), dim3(192), 0, stream,
-                                   w, round, long_wait() ? 1 : 0);
-        });
-        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_replay_long launch");
     }
 
     void* temp(size_t bytes) {
@@ -3889,6 +3251,20 @@ extern "C" int dofs_debug_sort_k32e(int e) {
 // Diagnosis only: fix-up on / off (the truncated order is not Kruskal's: results differ), and a copy of
 // the next packed batch's sorted (key, value) pairs — at most cap — into device buffers.
 extern "C" void dofs_debug_sort_fix(int on) { dofs::g_sort_fix = on != 0; }
+// Test knob: constant-key chunks of the long-path replay (dofs_dataflow.h g_keyfast; 1 = on, the default).
+// Returns the previous value; on < 0 only reads it.
+extern "C" int dofs_debug_replay_keyfast(int on) {
+    const int old = dofs::g_keyfast;
+    if (on >= 0) dofs::g_keyfast = on ? 1 : 0;
+    return old;
+}
+// Test knob: the LDS KRT's depths below 32 merges as one register window pass (1, the default) or as
+// union-find depths (0), g_deep_wave. Returns the previous value; on < 0 only reads it.
+extern "C" int dofs_debug_krt_deep_wave(int on) {
+    const int old = dofs::g_deep_wave;
+    if (on >= 0) dofs::g_deep_wave = on ? 1 : 0;
+    return old;
+}
 // Test knob: k_dnc_compress's wave skew (0 = off), see g_dnc_skew. Returns 0 or a HIP error code.
 extern "C" int dofs_debug_dnc_skew(int skew) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(dofs::g_dnc_skew), &skew, sizeof(int));
@@ -3959,12 +3335,6 @@ extern "C" int dofs_debug_flow_order(int order) {
     if (order >= 0 && order <= 2) dofs::g_flow_order = order;
     return old;
 }
-// Inspection: the dataflow replay's worker counts (waves) — long-path workers (DOFS_FLOW_LONG) and short ones.
-extern "C" int dofs_flow_workers(int* long_waves, int* short_waves) {
-    if (long_waves) *long_waves = dofs::HipBackend::flow_long_workers();
-    if (short_waves) *short_waves = dofs::HipBackend::flow_grid();
-    return 0;
-}
 extern "C" void dofs_debug_sort_dump(void* d_keys, void* d_vals, int64_t cap) {
     dofs::g_sort_dump[0] = d_keys;
     dofs::g_sort_dump[1] = d_vals;
@@ -3973,6 +3343,14 @@ extern "C" void dofs_debug_sort_dump(void* d_keys, void* d_vals, int64_t cap) {
 
 using DofsBackend = dofs::HipBackend;
 #include "dofs_cabi.inc.h"
+
+// Inspection: the dataflow replay's worker counts (waves) — long-path workers (DOFS_FLOW_LONG) and short ones.
+extern "C" int dofs_flow_workers(dofs_ctx* ctx, int* long_waves, int* short_waves) {
+    if (!ctx) return DOFS_ERR_INVALID_ARG;
+    if (long_waves) *long_waves = ctx->be.flow_long_workers();
+    if (short_waves) *short_waves = dofs::HipBackend::flow_grid();
+    return 0;
+}
 
 // Diagnosis only (tools/flow_dump.py): device pointers of the last batch's workspace arrays, after a sync:
 // out = {cur, ptop, list_long, In, ready, ord, lite, ctr, Rv, pre, flow control block, bw, lu, lv, SZ, hls,

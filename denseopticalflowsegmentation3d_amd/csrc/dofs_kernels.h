@@ -131,7 +131,6 @@ struct Ws {
     int long_path;  // heavy paths at least this long run on the wave-cooperative replay
     int jscatter;   // HIP: the LDS KRT's epilogue writes its block's outside children's jump words and
                     // path-top flags (the chip-wide jumping preorder of small batches), else k_pre_sweep
-    int pre_steps;  // HIP: k_pre_sweep wrote every merge's StepIn (KPathInit then registers the paths only)
     int deep_wave;  // HIP: the LDS KRT's depths below 32 merges by one register pass per 16-merge window
     // HIP dataflow replay: a short path stores a merge's replay record only where something reads it — its
     // path top (the parent's light child), a parked state, a merge of >= min_size pixels (kStepKeep: the
@@ -1203,20 +1202,6 @@ DOFS_HD inline StepIn step_in(const Ws& w, int f, int q, bool top, int lt, int l
     return in;
 }
 
-// step_in for a pixel light child whose blurred flow lf is already loaded (the preorder sweep's gather)
-DOFS_HD inline StepIn step_in_leaf(unsigned long long hl, bool top, int lB, int lt, F2 lf, int W, int min_size) {
-    const int sh = (int)(unsigned)(hl & 0xffffffffu), sl = (int)(unsigned)(hl >> 32);
-    StepIn in;
-    in.fs = (float)sh;
-    in.r = 1. / (double)(sh + sl);
-    in.meta = (lB ? kStepB : 0) | (top ? kStepTop : 0) | (sh + sl >= min_size ? kStepKeep : 0);
-    in.wbx = lf.x * (float)1;
-    in.wby = lf.y * (float)1;
-    in.la = (lt % W) | ((lt / W) << 16);
-    in.lb = lt;
-    return in;
-}
-
 struct KPathInit {  // one lane per merge node x = N + k; path ids and lists through the list taker
     Ws w;
     const int* pre;
@@ -1231,7 +1216,7 @@ struct KPathInit {  // one lane per merge node x = N + k; path ids and lists thr
         if (valid) {
             q = pre[lb + x];
             top = w.lite[lb + x] != 0;
-            if (!w.pre_steps) {  // (else the preorder sweep wrote it, k_pre_sweep: the same record)
+            {
                 int lt, lB;
                 heavy_child(w, f, (int)x, &lt, &lB);
                 const unsigned long long hl = w.hls[f * d.M + k];  // children's sizes (the KRT's parent pass)

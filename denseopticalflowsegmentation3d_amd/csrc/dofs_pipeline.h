@@ -54,7 +54,6 @@ struct Pipeline {
     Dims cap{};  // allocated shape
     int* pre = nullptr;
     int64_t snap_cap = 4096;
-    int preorder_in_b = 1;  // 0: the preorder in phase A; 1: in phase B (the API's default); 2: KPathInit in B
     // block-start labels of the KRT: the top-down global depths (DNC) or the per-frame sweep. The sweep's
     // time is one frame's sequence of blocks (≈ 40 ms at 1080p, 111 ms at 4K, whatever the batch); the
     // DNC's is proportional to the batch's merges (≈ 1.45 ms per million): DNC wins below ≈ 9 frames a
@@ -390,7 +389,7 @@ struct Pipeline {
         const int B = d.B;
         const int64_t N = d.N, M = d.M, NL = d.NL;
         be.mark(3);
-        w.jscatter = Backend::pre_jump(d) ? 1 : 0;
+        w.jscatter = be.pre_jump(d) ? 1 : 0;
         const bool dnc = use_dnc(d);
         KEdgeInit ei{w, dnc};
         ei.given = given;
@@ -411,12 +410,11 @@ struct Pipeline {
         }
         be.dnc_deep(w);
         be.dnc_parent(w);  // KDncParent (HIP: k_dnc_deep's epilogue)
-
-        if (preorder_in_b == 0) preorder();
-        if (preorder_in_b == 2) preorder_pos();
     }
 
-    // K4 heavy-first preorder (pointer jumping) and the replay's per-position inputs
+    // K4 heavy-first preorder (pointer jumping) and the replay's per-position inputs. It runs at the start of
+    // phase B: phase A bounds the step and phase B has slack (round 4, B = 112, same box: in phase A
+    // 1,736-1,746 Mpix/s, in phase B 1,758-1,761)
     void preorder() {
         preorder_pos();
         path_init();
@@ -443,27 +441,29 @@ struct Pipeline {
         be.scan_excl_leaf(w.ord, w.lscan, NL, B, N);
         be.launch(B, NL, KLeafOrder{w, pre});
     }
-    void path_init() {
-        w.pre_steps = Backend::pre_steps(be) ? 1 : 0;
-        be.launch(w.d.B, w.d.M, KPathInit{w, w.pre});
-    }
+    void path_init() { be.launch(w.d.B, w.d.M, KPathInit{w, w.pre}); }
 
     // Phase B (replay + scoring): the order-dependent replay is latency-bound (a few waves per
     // frame), so the HIP backend overlaps it with the next batch's phase A on a second stream.
     void run_b() {
-        const Dims& d = w.d;
-        const int B = d.B;
-        const int64_t N = d.N, M = d.M;
-        if (M <= 0) return;
-        if (preorder_in_b == 1) preorder();
-        if (preorder_in_b == 2) {
-            pre = w.pre;
-            path_init();
-        }
+        if (w.d.M <= 0) return;
+        preorder();
         be.mark(5);
         // K5 bottom-up replay of Forest::merge along heavy paths: one dataflow launch (HIP), else rounds
-        const bool flow = !(skip_mask & 3) && be.replay_flow(w);
-        const int RR = flow ? 0 : ceil_log2(N) + 2;
+        if constexpr (Backend::kReplayFlow) {
+            if (!(skip_mask & 3)) be.replay_flow(w);
+        } else {
+            replay_rounds();
+        }
+        score();
+    }
+
+    // K5 in rounds (the emulator): round r advances the short paths parked in round r - 1 and the long paths
+    void replay_rounds() {
+        const Dims& d = w.d;
+        const int B = d.B;
+        const int64_t N = d.N;
+        const int RR = ceil_log2(N) + 2;
         // short paths: round r advances the paths parked in round r - 1 (lists ping-pong between two
         // pixel-sized buffers whose owners, the MST passes, are done)
         int* park[2] = {w.off, w.comp};
@@ -480,9 +480,14 @@ struct Pipeline {
                 in = park[r & 1];
                 inc = oc;
             }
-            if (!(skip_mask & 2)) be.replay_long(w, r);  // HIP: three-wave kernel; emulator: KReplay
+            if (!(skip_mask & 2)) be.replay_long(w, r);
         }
+    }
 
+    void score() {
+        const Dims& d = w.d;
+        const int B = d.B;
+        const int64_t N = d.N, M = d.M;
         be.mark(6);
         // K6 new_merge filters, lifting, per-slot arg-max, snapshots
         be.launch(B, M, KFilter{w, pre});

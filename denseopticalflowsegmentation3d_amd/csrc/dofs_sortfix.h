@@ -218,20 +218,12 @@ __global__ __launch_bounds__(kFixBlock) void k_sortfix_merge(SortFix s, int lgs)
 // A group's 32-bit keys are equal, so only values move. Weights below the window (zero included) share
 // key 0 and weights above it (none for finite flows) the largest key: a long mixed group there takes
 // the fallback — slower, never wrong.
-// host: mantissa bits of the 32-bit keys (0: the 64-bit keys and g_sort_cut); DOFS_SORT_K32 sets the
-// start value (A/B runs on one library)
-inline int g_sort_k32 = [] {
-    const char* e = getenv("DOFS_SORT_K32");
-    const int m = e ? atoi(e) : 27;
-    return m == 0 || (m >= 4 && m <= 30) ? m : 27;
-}();
+// host: mantissa bits of the 32-bit keys (0: the 64-bit keys and g_sort_cut); dofs_debug_sort_k32 sets it
+// (tests/test_gpu_sortfix.py)
+inline int g_sort_k32 = 27;
 // host: exponent bits of the 32-bit keys (0: 32 - m, the full word). With m + e = 24 the pair sort takes
-// three 8-bit digits instead of four; DOFS_SORT_K32E sets it (A/B runs on one library)
-inline int g_sort_k32e = [] {
-    const char* e = getenv("DOFS_SORT_K32E");
-    const int x = e ? atoi(e) : 0;
-    return x >= 1 && x <= 8 ? x : 0;
-}();
+// three 8-bit digits instead of four; dofs_debug_sort_k32e sets it (measured slower: DESIGN.md §8)
+inline int g_sort_k32e = 0;
 inline int sort_k32_bits() { return g_sort_k32e && g_sort_k32 + g_sort_k32e < 32 ? g_sort_k32 + g_sort_k32e : 32; }
 
 struct SortFix32 {

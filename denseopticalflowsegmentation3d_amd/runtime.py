@@ -224,7 +224,7 @@ class Dofs:
         self._last_merges = None
         self.ctx = self.lib.dofs_create(device)
         if not self.ctx:
-            raise RuntimeError(f"dofs_create({device}) failed: no gfx950 device visible")
+            raise RuntimeError(f"dofs_create({device}) failed: {self.lib.dofs_last_error(None).decode()}")
         if keep_events:
             self.keep_events(True)
 
@@ -421,8 +421,9 @@ class Dofs:
         f = getattr(self.lib, "dofs_flow_workers", None)
         if f is None:
             return None
+        f.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         nl, ns = C.c_int(0), C.c_int(0)
-        f(C.byref(nl), C.byref(ns))
+        self._err(f(self.ctx, C.byref(nl), C.byref(ns)), "dofs_flow_workers")
         return {"long": nl.value, "short": ns.value}
 
     def batch_counters(self, B: int) -> np.ndarray:

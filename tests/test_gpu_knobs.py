@@ -1,0 +1,56 @@
+"""GPU: each runtime knob of the product library (csrc/dofs_knobs.h) changes nothing but speed.
+
+A context created under the knob runs the same seeded 1080p batch as a default context: every merge event
+(root, rank, size, mean bits, bbox), the labels and the snapshots must be identical, and the replay must
+complete (C_FLOWERR clear). DOFS_KRT_DNC and DOFS_PRE_JUMP have their own tests (test_gpu_krt_dnc.py,
+test_gpu_preorder_modes.py)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+B, H, W = 12, 1080, 1920
+
+
+def _run(fl, calib):
+    import torch
+
+    from denseopticalflowsegmentation3d_amd import runtime
+    ctx = runtime.Dofs(0, keep_events=True)
+    try:
+        bid = ctx.segment_batch_device(fl.data_ptr(), B, H, W, *calib)
+        torch.cuda.synchronize()
+        err = int(ctx.batch_counters(B)[0, 58])
+        blk = torch.empty(4 * B + 96 * 4 * B, dtype=torch.uint8, device="cuda")
+        ctx.records_copy(blk.data_ptr(), 4, batch=bid)
+        ev = [ctx.events(f).view(np.uint8).copy() for f in range(B)]
+        res = [ctx.fetch(f, want_blur=False) for f in range(B)]
+        return err, ev, res
+    finally:
+        ctx.close()
+
+
+@pytest.fixture(scope="module")
+def batch_and_default(calib):
+    import torch
+
+    from denseopticalflowsegmentation3d_amd import runtime
+    fl = torch.empty((B, H, W, 2), dtype=torch.float32, device="cuda")
+    runtime.synth_flow_device(fl.data_ptr(), B, H, W, 4242)
+    torch.cuda.synchronize()
+    return fl, _run(fl, calib)
+
+
+@pytest.mark.parametrize("env", [{"DOFS_SERIAL": "1"}, {"DOFS_FLOW_LONG": "256"}, {"DOFS_FLOW_LONG": "4"},
+                                 {"DOFS_LONG_PATH": "64"}, {"DOFS_LONG_PATH": "4096"}])
+def test_knob_changes_nothing_but_speed(monkeypatch, calib, batch_and_default, env):
+    fl, (e0, ev0, r0) = batch_and_default
+    assert e0 == 0
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    err, ev, res = _run(fl, calib)
+    assert err == 0
+    for f in range(B):
+        assert ev[f].tobytes() == ev0[f].tobytes(), (env, f)
+        assert np.array_equal(res[f].labels, r0[f].labels), (env, f)
+        assert res[f].snapshots.tobytes() == r0[f].snapshots.tobytes(), (env, f)

@@ -129,16 +129,25 @@ def test_tail_batch_keeps_large_workspace(calib):
 
 @pytest.mark.parametrize("mode", ["0", "1"])
 def test_deep_depth_forms_equal(monkeypatch, calib, mode):
-    """The LDS KRT's depths below 32 merges as the register window pass (DOFS_DEEP_WAVE=1, default) and as
-    union-find depths (0) give the same tree, in both KRT modes. The union-find form leaves the first
+    """The LDS KRT's depths below 32 merges as the register window pass (dofs_debug_krt_deep_wave(1), the
+    default) and as union-find depths (0) give the same tree, in both KRT modes. The union-find form leaves the first
     half's last merge without a size in LDS (the top level writes it to SZ), which the second half's
     prefetched labels must then take from SZ — the case this pins."""
+    import ctypes as C
+
+    from denseopticalflowsegmentation3d_amd import runtime
     B, H, W = 12, 270, 480
     seeds = [77, 177]
-    monkeypatch.setenv("DOFS_DEEP_WAVE", "1")
-    a = _run(monkeypatch, mode, B, H, W, calib, seeds)
-    monkeypatch.setenv("DOFS_DEEP_WAVE", "0")
-    b = _run(monkeypatch, mode, B, H, W, calib, seeds)
+    lib = runtime.load()
+    lib.dofs_debug_krt_deep_wave.argtypes = [C.c_int]
+    lib.dofs_debug_krt_deep_wave.restype = C.c_int
+    old = lib.dofs_debug_krt_deep_wave(1)
+    try:
+        a = _run(monkeypatch, mode, B, H, W, calib, seeds)
+        lib.dofs_debug_krt_deep_wave(0)
+        b = _run(monkeypatch, mode, B, H, W, calib, seeds)
+    finally:
+        lib.dofs_debug_krt_deep_wave(old)
     for (ca, ea, la), (cb, eb, lb) in zip(a, b):
         assert int(ca[0, 58]) == 0 and int(cb[0, 58]) == 0  # C_FLOWERR (the list positions are not ordered)
         assert np.array_equal(la, lb)
