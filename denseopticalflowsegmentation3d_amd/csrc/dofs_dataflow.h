@@ -776,62 +776,75 @@ __device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch
     }
 }
 
-// A long worker's next task: the initial long pool first, then a ticket of the long-path queue, whose
-// slot its pusher fills. A ticket is claimed only below the queue's tail (a CAS on the head), so its slot
-// already belongs to a push in progress: the wait for the slot is for a lane that is running, never for
-// work that has yet to be produced. With neither, an idle worker helps with the initial short pool
-// (kFlowHelpTask) while it is not empty. So a long worker never waits for a wave that is not running: the
-// replay completes whether the short workers' launch runs beside this one, before it or after it.
+// A long worker's next task: the initial long pool first, then a ticket of the long-path queue, whose slot
+// its pusher fills (tickets are taken only while pushes are pending, so there is no atomic herd on the head,
+// and at most the racing workers' tickets run ahead of the pushes). A worker whose ticket's slot is not filled
+// yet, or that has no ticket, helps with the initial short pool while it is not empty (kFlowHelpTask; it keeps
+// its ticket, *ticket, across the help). So a long worker never waits for work that no running wave holds:
+// while the short pool has tasks it runs them itself, and once it is empty every unfinished task is held by a
+// running wave or parked on one — the replay completes whether the short workers' launch runs beside this
+// one, before it or after it (tests/test_gpu_flow_order.py).
 // -1: every long path completed, or a bounded wait gave up (C_FLOWERR). A slot is accepted only with this
 // launch's tag and a long task word of the batch: slots never written in this launch hold Borůvka minima
 // or older tags, which neither passes (kFlowEpochs < the high word of any weight the MST stores there,
 // DESIGN.md §6a).
 constexpr unsigned kFlowEpochs = 0xFFFFF;
 constexpr int kFlowHelpTask = -2;  // flow_next_long: no long task now, the short pool has tasks
-__device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int nl) {
+__device__ inline int flow_next_long(const Ws& w, int* ctl, unsigned epoch, int nl, int* ticket) {
     const int lane = threadIdx.x & 63;
-    int t = -1;
+    int t = -1, tk = *ticket;
     if (lane == 0) {
         const int np = ctl[FC_NLPOOL];
         const int ntot = ctl[FC_NT] + ctl[FC_NS];
-        while (t < 0 && f_poll(ctl + FC_LONG_NEXT) < np) {
+        while (tk < 0 && t < 0 && f_poll(ctl + FC_LONG_NEXT) < np) {
             const int i = atomicAdd(ctl + FC_LONG_NEXT, 1);
             if (i < np) t = flow_long_task(w, ctl, i);
         }
+        const long long nframe = w.d.N;
         for (int spin = 0; t < 0; ++spin) {
-            if (f_poll(ctl + FC_LDONE) >= nl) break;  // every long path completed: nothing more will come
             if (spin >= (1 << 26)) {
                 f_st(ctl + FC_ERR, 1);
                 break;
             }
-            const int h = f_poll(ctl + FC_QHEAD);
-            if (h < f_poll(ctl + FC_QTAIL)) {
-                if (atomicCAS(ctl + FC_QHEAD, h, h + 1) != h) continue;  // another worker took ticket h
-                if (h >= ctl[FC_QCAP]) break;  // (never: pushes stay below the capacity)
-                const long long nframe = w.d.N;
-                for (int s2 = 0;; ++s2) {  // slot h's pusher has its ticket: its store is on the way
-                    const unsigned long long v = f_poll64(w.bw + h);
-                    const int c = (int)(unsigned)v;
-                    if ((unsigned)(v >> 32) == epoch && c >= 0 && (c & kFlowLong) &&
-                        (long long)(c & kFlowIdMask) < nframe * w.d.B) {
-                        t = c;
-                        break;
-                    }
-                    if (s2 >= (1 << 26)) {
+            if (tk < 0) {
+                if (f_poll(ctl + FC_LDONE) >= nl) break;  // every long path completed: nothing more will come
+                if (f_poll(ctl + FC_QHEAD) < f_poll(ctl + FC_QTAIL)) {
+                    tk = atomicAdd(ctl + FC_QHEAD, 1);
+                    if (tk >= ctl[FC_QCAP]) {  // (never: pushes stay below the capacity)
                         f_st(ctl + FC_ERR, 1);
+                        tk = -1;
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(2);
+                    continue;
                 }
-                if (t < 0) break;
-            } else if (f_poll(ctl + FC_SHORT_NEXT) < ntot) {
-                t = kFlowHelpTask;
-                break;
-            } else {
+                if (f_poll(ctl + FC_SHORT_NEXT) < ntot) {
+                    t = kFlowHelpTask;
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(32);
+                continue;
             }
+            const unsigned long long v = f_poll64(w.bw + tk);
+            const int c = (int)(unsigned)v;
+            if ((unsigned)(v >> 32) == epoch && c >= 0 && (c & kFlowLong) && (long long)(c & kFlowIdMask) < nframe * w.d.B) {
+                t = c;
+                tk = -1;
+                break;
+            }
+            if ((spin & 15) == 15) {
+                if (f_poll(ctl + FC_LDONE) >= nl) {  // a ticket ahead of the last push: never filled
+                    tk = -1;
+                    break;
+                }
+                if (f_poll(ctl + FC_SHORT_NEXT) < ntot) {  // the push may need short work: help, keep the ticket
+                    t = kFlowHelpTask;
+                    break;
+                }
+            }
+            __builtin_amdgcn_s_sleep(16);
         }
     }
+    *ticket = __shfl(tk, 0, 64);
     return __shfl(t, 0, 64);
 }
 
@@ -860,8 +873,9 @@ __global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigne
     if (lane == 0) fs_min(ctl, FS_T0, fs_now());
     if constexpr (kLong) {
         __builtin_amdgcn_s_setprio(3);  // the chains go first in their SIMD's arbitration
+        int ticket = -1;  // a long-path queue ticket whose slot is not filled yet (kept across help rounds)
         for (int it = 0; it < (1 << 26); ++it) {
-            int t = flow_next_long(w, ctl, epoch, nl);
+            int t = flow_next_long(w, ctl, epoch, nl, &ticket);
             if (t == kFlowHelpTask) {  // idle: one claim of the initial short pool, at the short workers' priority
                 __builtin_amdgcn_s_setprio(0);
                 flow_short(w, ctl, epoch, -1, 1, kFlowHelp, &cb, &ce);

@@ -2962,8 +2962,9 @@ struct HipBackend {
     hipEvent_t flow_ev[2] = {nullptr, nullptr};
     unsigned flow_epoch = 0;
     static constexpr int flow_grid() { return 2048; }  // short-path workers (waves; 1,024 and 4,096 measured equal)
-    // long-path workers (waves): DOFS_FLOW_LONG, default 128
-    int flow_long_workers() const { return kn.flow_long > 0 ? kn.flow_long : 128; }
+    // long-path workers (waves): DOFS_FLOW_LONG, default 256 (round 5, B = 112, same box, two runs each:
+    // 128 → 1,816 / 1,823 Mpix/s, replay stage 36.7 ms; 256 → 1,869 / 1,869, 22.4 ms; 512 → 1,830 / 1,828)
+    int flow_long_workers() const { return kn.flow_long > 0 ? kn.flow_long : 256; }
     bool replay_flow(const Ws& w) {
         if ((int64_t)w.d.B * w.d.N >= (int64_t)kFlowLong) {  // (api_run refuses such batches)
             note(hipErrorInvalidValue, "batch too large for the replay's 30-bit task words");

@@ -15,7 +15,7 @@ namespace dofs {
 
 struct Knobs {
     int serial = 0;      // DOFS_SERIAL=1: a batch's two stages back to back on one stream (clean per-kernel profiles)
-    int flow_long = 0;   // DOFS_FLOW_LONG: long-path replay workers (waves, 4 .. 1024; 0 = the backend's default)
+    int flow_long = 0;   // DOFS_FLOW_LONG: long-path replay workers (waves, 4 .. 1024; 0 = the backend's default, 256)
     int long_path = 0;   // DOFS_LONG_PATH: merges from which a heavy path is replayed by a whole wave (16 .. 65536)
     int krt_dnc = -1;    // DOFS_KRT_DNC: 0 the per-frame sweep KRT, 1 the top-down global depths (-1 auto)
     int pre_jump = 8;    // DOFS_PRE_JUMP: batches of at most this many frames take the chip-wide preorder
