@@ -55,7 +55,7 @@ enum FlowCtlIdx {
     FC_QCAP = FC_NL + 3,            // queue slots: B * N (w.bw); tickets and pushes stay below it
     FC_NLPOOL = FC_NL + 4,          // initial long pool: B root-path entries, then the frames' other long paths
     FC_FS = 8 * kFlowLine,          // the launch anatomy: FS_N u64 counters, one 256-byte line each (FlowStat)
-    FC_HDR = FC_FS + 24 * 64,       // then pl[B + 1], pt[B + 1], ps[B + 1]
+    FC_HDR = FC_FS + 28 * 64,       // then pl[B + 1], pt[B + 1], ps[B + 1]
 };
 inline int g_flow_order = 0;  // host: the two launches' order (dofs_debug_flow_order; 0 = side by side)
 // host: constant-key chunks in the long-path loop (flow_long; 1 = on, the default: 96 % of the chunks, one 4K
@@ -94,7 +94,10 @@ enum FlowStat {
     FS_P_NEXT = 20,
     FS_KFAST = 21,     // long-path chunks run with a constant key (no step reaches the carried rank)
     FS_RESTARTS = 22,  // pipelined resolve: stage fills (a run's first chunk, a re-resolve after a park)
-    FS_N = 24
+    // measurement build, wave pairs (flow_pair): C's and H's ticks waiting at the chunk barriers
+    FS_P_CWAIT = 23,
+    FS_P_HWAIT = 24,
+    FS_N = 28
 };
 static_assert(FS_N * kFsStride * 2 == FC_HDR - FC_FS, "FlowStat block size");
 __device__ inline unsigned long long* fs_at(int* ctl, int i) {
@@ -350,6 +353,111 @@ __device__ inline void pipe_restart(const Ws& w, int64_t lb, int q, int top, int
     P.rv1 = pipe_rv(w, lb, P.in1, P.rdy1, q - 64 - lane, top);
 }
 
+// The chain of one 64-step chunk (Forest::merge's running mean and union-by-rank key, graph.cpp:177-213):
+// n steps of the records c[0..n), lane parity h carrying the x (h = 0) or y mean in v, and the key K.
+// fastc (a constant-key chunk: no step's light key reaches K's rank): the mean chain alone — one LDS read,
+// five VALU and a quarter LDS store per step instead of ~16 instructions with the key update — and its
+// values as two rows of 64 floats in ob's storage (x row, y row); else {v, K} per step in ob[2 k + h].
+__device__ __forceinline__ void chain_chunk(const OneRec* c, OneOut* ob, int n, bool fastc, int h, float& v,
+                                            unsigned& K) {
+    auto step = [&](int k, uint4 a, OneHalf b) {  // a = {lk, bm, lkp}, b = {r, wb, fs}
+        v = (float)((double)(v * b.fs + b.wb) * b.r);
+        const unsigned lk = a.x, bm = a.y, lkp = a.z;
+        unsigned eq = (bm & lkp) | (~bm & (K + (1u << kRankShift)));
+        unsigned ne = K > lk ? K : lk;
+        asm volatile("" : "+v"(eq), "+v"(ne));
+        K = (K ^ lk) < (1u << kRankShift) ? eq : ne;
+        OneOut o;
+        o.v = v;
+        o.k = K;
+        ob[2 * k + h] = o;
+    };
+    auto lda = [&](int k) { return *reinterpret_cast<const uint4*>(&c[k]); };
+    if (fastc) {
+        // The mean chain alone: per step one ds_read_b128 of the lane's half record, the five chain
+        // ops, and the value (no key: it is K for the whole chunk) into the chunk's output slot. The
+        // records run through three 4-step register sets: a set is reloaded 4 to 8 steps ahead of
+        // its use (~90-170 cycles against the ~50-cycle LDS latency), and the sched barriers keep
+        // the compiler from sinking those loads next to their uses (round 3's ISA had them issued
+        // one to three steps ahead: the LDS latency was exposed twice per 8 steps).
+        // values only, as two rows of 64 floats in ob's storage (x row, y row): four steps' values
+        // are contiguous, one ds_write_b128 per 4 steps
+        float* fvh = reinterpret_cast<float*>(ob) + 64 * h;
+        const OneHalf* ch = &c[0].h[h];
+        auto ld = [&](int k) { return *reinterpret_cast<const OneHalf*>(reinterpret_cast<const char*>(ch) + k * (int)sizeof(OneRec)); };
+        auto chain = [&](const OneHalf& b) {
+            v = (float)((double)(v * b.fs + b.wb) * b.r);
+            return v;
+        };
+        auto stepf = [&](int k, const OneHalf& b) { fvh[k] = chain(b); };
+        auto step4 = [&](int k, const OneHalf& a0, const OneHalf& a1, const OneHalf& a2, const OneHalf& a3) {
+            float4 o;
+            o.x = chain(a0);
+            o.y = chain(a1);
+            o.z = chain(a2);
+            o.w = chain(a3);
+            *reinterpret_cast<float4*>(fvh + k) = o;
+        };
+        // 8 steps per iteration in two 4-step register sets, each loaded 4 steps (~90 cycles) ahead of
+        // its use; the sched barriers pin the loads there (round 3's ISA had the compiler sink them to
+        // one to three steps ahead of their use: the LDS latency was exposed twice per 8 steps). The
+        // sets are not rotated across iterations (a rotating ring compiled to v_mov_b64 copies, and a
+        // fully unrolled chunk to AGPR spills)
+        OneHalf b0 = ld(0), b1 = ld(1), b2 = ld(2), b3 = ld(3);
+        int k = 0;
+        for (; k + 8 <= n; k += 8) {
+            const OneHalf d0 = ld(k + 4), d1 = ld(k + 5), d2 = ld(k + 6), d3 = ld(k + 7);
+            __builtin_amdgcn_sched_barrier(0);
+            step4(k, b0, b1, b2, b3);
+            __builtin_amdgcn_sched_barrier(0);
+            b0 = ld(k + 8), b1 = ld(k + 9), b2 = ld(k + 10), b3 = ld(k + 11);
+            __builtin_amdgcn_sched_barrier(0);
+            step4(k + 4, d0, d1, d2, d3);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (k + 4 <= n) {
+            const OneHalf d0 = ld(k + 4), d1 = ld(k + 5), d2 = ld(k + 6);
+            step4(k, b0, b1, b2, b3);
+            if (k + 4 < n) stepf(k + 4, d0);
+            if (k + 5 < n) stepf(k + 5, d1);
+            if (k + 6 < n) stepf(k + 6, d2);
+        } else {
+            if (k < n) stepf(k, b0);
+            if (k + 1 < n) stepf(k + 1, b1);
+            if (k + 2 < n) stepf(k + 2, b2);
+        }
+    } else {
+    // two register sets, each reloaded right after its last use (4 steps ahead of its next use): no
+    // loop-carried copies (the single-set form with next-group temporaries compiled to ~4 v_mov per step)
+    int k = 0;
+    uint4 a0 = lda(0), a1 = lda(1), a2 = lda(2), a3 = lda(3);
+    OneHalf b0 = c[0].h[h], b1 = c[1].h[h], b2 = c[2].h[h], b3 = c[3].h[h];
+    for (; k + 8 <= n; k += 8) {
+        const int m = k + 4, m2 = (k + 8) & 63;
+        const uint4 e0 = lda(m), e1 = lda(m + 1), e2 = lda(m + 2), e3 = lda(m + 3);
+        const OneHalf d0 = c[m].h[h], d1 = c[m + 1].h[h], d2 = c[m + 2].h[h], d3 = c[m + 3].h[h];
+        step(k, a0, b0);
+        step(k + 1, a1, b1);
+        step(k + 2, a2, b2);
+        step(k + 3, a3, b3);
+        a0 = lda(m2), a1 = lda(m2 + 1), a2 = lda(m2 + 2), a3 = lda(m2 + 3);
+        b0 = c[m2].h[h], b1 = c[m2 + 1].h[h], b2 = c[m2 + 2].h[h], b3 = c[m2 + 3].h[h];
+        step(k + 4, e0, d0);
+        step(k + 5, e1, d1);
+        step(k + 6, e2, d2);
+        step(k + 7, e3, d3);
+    }
+    if (k + 4 <= n) {
+        step(k, a0, b0);
+        step(k + 1, a1, b1);
+        step(k + 2, a2, b2);
+        step(k + 3, a3, b3);
+        k += 4;
+    }
+    for (; k < n; ++k) step(k, lda(k), c[k].h[h]);
+    }
+}
+
 // A long path (task word t) on this wave, from its cursor: returns the task word of the parent path
 // that was parked on its top (to run next), or -1 (parked itself, or completed with nobody waiting).
 __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut* ob, int keyfast) {
@@ -435,111 +543,15 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
         __builtin_amdgcn_wave_barrier();
         FLOW_PROF_MARK(p_next);  // the next chunk's resolve (its global loads and their waits)
         const OneRec* c = buf[cb];
-        auto step = [&](int k, uint4 a, OneHalf b) {  // a = {lk, bm, lkp}, b = {r, wb, fs}
-            v = (float)((double)(v * b.fs + b.wb) * b.r);
-            const unsigned lk = a.x, bm = a.y, lkp = a.z;
-            unsigned eq = (bm & lkp) | (~bm & (K + (1u << kRankShift)));
-            unsigned ne = K > lk ? K : lk;
-            asm volatile("" : "+v"(eq), "+v"(ne));
-            K = (K ^ lk) < (1u << kRankShift) ? eq : ne;
-            OneOut o;
-            o.v = v;
-            o.k = K;
-            ob[2 * k + h] = o;
-        };
-        auto lda = [&](int k) { return *reinterpret_cast<const uint4*>(&c[k]); };
         // Constant-key chunks: union by rank (graph.cpp:177-182, 210-213) leaves the carried key K
         // unchanged at a step whose light child has a lower rank (max(K, lk) = K). A lane checks its
         // own step against K's rank; when no step of the chunk reaches it (the common case: after
         // a path's first steps its light children are mostly pixels, rank 0), every step's key is K and
-        // the loop carries only the mean chain — one LDS read, five VALU and one LDS store per step
-        // instead of the ~16 instructions with the key update.
+        // the loop carries only the mean chain (chain_chunk)
         const unsigned krank = K & ~((1u << kRankShift) - 1);
         const bool fastc = keyfast && __ballot(lane < n && curlk >= krank) == 0;
-        if (fastc) {
-            ++kfast;
-            // The mean chain alone: per step one ds_read_b128 of the lane's half record, the five chain
-            // ops, and the value (no key: it is K for the whole chunk) into the chunk's output slot. The
-            // records run through three 4-step register sets: a set is reloaded 4 to 8 steps ahead of
-            // its use (~90-170 cycles against the ~50-cycle LDS latency), and the sched barriers keep
-            // the compiler from sinking those loads next to their uses (round 3's ISA had them issued
-            // one to three steps ahead: the LDS latency was exposed twice per 8 steps).
-            // values only, as two rows of 64 floats in ob's storage (x row, y row): four steps' values
-            // are contiguous, one ds_write_b128 per 4 steps
-            float* fvh = reinterpret_cast<float*>(ob) + 64 * h;
-            const OneHalf* ch = &c[0].h[h];
-            auto ld = [&](int k) { return *reinterpret_cast<const OneHalf*>(reinterpret_cast<const char*>(ch) + k * (int)sizeof(OneRec)); };
-            auto chain = [&](const OneHalf& b) {
-                v = (float)((double)(v * b.fs + b.wb) * b.r);
-                return v;
-            };
-            auto stepf = [&](int k, const OneHalf& b) { fvh[k] = chain(b); };
-            auto step4 = [&](int k, const OneHalf& a0, const OneHalf& a1, const OneHalf& a2, const OneHalf& a3) {
-                float4 o;
-                o.x = chain(a0);
-                o.y = chain(a1);
-                o.z = chain(a2);
-                o.w = chain(a3);
-                *reinterpret_cast<float4*>(fvh + k) = o;
-            };
-            // 8 steps per iteration in two 4-step register sets, each loaded 4 steps (~90 cycles) ahead of
-            // its use; the sched barriers pin the loads there (round 3's ISA had the compiler sink them to
-            // one to three steps ahead of their use: the LDS latency was exposed twice per 8 steps). The
-            // sets are not rotated across iterations (a rotating ring compiled to v_mov_b64 copies, and a
-            // fully unrolled chunk to AGPR spills)
-            OneHalf b0 = ld(0), b1 = ld(1), b2 = ld(2), b3 = ld(3);
-            int k = 0;
-            for (; k + 8 <= n; k += 8) {
-                const OneHalf d0 = ld(k + 4), d1 = ld(k + 5), d2 = ld(k + 6), d3 = ld(k + 7);
-                __builtin_amdgcn_sched_barrier(0);
-                step4(k, b0, b1, b2, b3);
-                __builtin_amdgcn_sched_barrier(0);
-                b0 = ld(k + 8), b1 = ld(k + 9), b2 = ld(k + 10), b3 = ld(k + 11);
-                __builtin_amdgcn_sched_barrier(0);
-                step4(k + 4, d0, d1, d2, d3);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            if (k + 4 <= n) {
-                const OneHalf d0 = ld(k + 4), d1 = ld(k + 5), d2 = ld(k + 6);
-                step4(k, b0, b1, b2, b3);
-                if (k + 4 < n) stepf(k + 4, d0);
-                if (k + 5 < n) stepf(k + 5, d1);
-                if (k + 6 < n) stepf(k + 6, d2);
-            } else {
-                if (k < n) stepf(k, b0);
-                if (k + 1 < n) stepf(k + 1, b1);
-                if (k + 2 < n) stepf(k + 2, b2);
-            }
-        } else {
-        // two register sets, each reloaded right after its last use (4 steps ahead of its next use): no
-        // loop-carried copies (the single-set form with next-group temporaries compiled to ~4 v_mov per step)
-        int k = 0;
-        uint4 a0 = lda(0), a1 = lda(1), a2 = lda(2), a3 = lda(3);
-        OneHalf b0 = c[0].h[h], b1 = c[1].h[h], b2 = c[2].h[h], b3 = c[3].h[h];
-        for (; k + 8 <= n; k += 8) {
-            const int m = k + 4, m2 = (k + 8) & 63;
-            const uint4 e0 = lda(m), e1 = lda(m + 1), e2 = lda(m + 2), e3 = lda(m + 3);
-            const OneHalf d0 = c[m].h[h], d1 = c[m + 1].h[h], d2 = c[m + 2].h[h], d3 = c[m + 3].h[h];
-            step(k, a0, b0);
-            step(k + 1, a1, b1);
-            step(k + 2, a2, b2);
-            step(k + 3, a3, b3);
-            a0 = lda(m2), a1 = lda(m2 + 1), a2 = lda(m2 + 2), a3 = lda(m2 + 3);
-            b0 = c[m2].h[h], b1 = c[m2 + 1].h[h], b2 = c[m2 + 2].h[h], b3 = c[m2 + 3].h[h];
-            step(k + 4, e0, d0);
-            step(k + 5, e1, d1);
-            step(k + 6, e2, d2);
-            step(k + 7, e3, d3);
-        }
-        if (k + 4 <= n) {
-            step(k, a0, b0);
-            step(k + 1, a1, b1);
-            step(k + 2, a2, b2);
-            step(k + 3, a3, b3);
-            k += 4;
-        }
-        for (; k < n; ++k) step(k, lda(k), c[k].h[h]);
-        }
+        if (fastc) ++kfast;
+        chain_chunk(c, ob, n, fastc, h, v, K);
         FLOW_PROF_MARK(p_steps);
         B4 obb;
         {  // bbox: inclusive prefix join over the chunk (lane = step), then the carried box
@@ -907,6 +919,408 @@ __global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigne
     }
     if (lane == 0) fs_max(ctl, FS_T_EXIT, fs_now());
 }
+// ---------------------------------------------------------------------------------------------
+// Long paths by a pair of waves (k_replay_flow_pair). A long path's time is its chain: per 64-step chunk the
+// steps (~21 ns each) and, on one wave, the chunk's tail (bbox prefix, record stores, hand-over) and the next
+// chunk's resolve (its global loads) — ~1.1 µs a chunk, 17 ns a step more (profiles/r04/anatomy: p_tail
+// 30.5 + p_next 30.6 of 157 wave-ms at 4K). One wave issues at most one instruction per four cycles, so the
+// tail cannot hide in the chain's idle cycles: it needs a second wave. Here wave C carries the chain alone
+// (chain_chunk over LDS records) and wave H, on another SIMD, does everything else one chunk apart: while C
+// steps chunk i, H builds chunk i + 1 into the other LDS slot (FlowPipe's three-stage resolve) and finishes
+// chunk i - 1 (bbox prefix, records); two workgroup barriers per chunk hand the slots over. A chunk that
+// completes the path or blocks on an incomplete light child is finished by H at once (C waits), which then
+// publishes the top or parks exactly as flow_long does. Task control (queue tickets, help rounds, injected
+// short waiters) is H's; C follows the commands H leaves in LDS.
+// ---------------------------------------------------------------------------------------------
+struct PairShared {
+    OneRec buf[2][64];  // step records of the chunk in each slot (H writes, C reads)
+    OneOut ob[2][128];  // C's outputs per slot: {v, K} per step, or two rows of 64 values (constant-key)
+    int n[2];           // H → C: steps of the chunk in the slot
+    int fin[2];         // H → C: the chunk ends the path (its top); with n < 64 a chunk ends the run (blocked)
+    unsigned maxlk[2];  // H → C: the largest light key among them (the constant-key test)
+    int fast[2];        // C → H: the slot ran as a constant-key chunk ...
+    unsigned k0[2];     // C → H: ... with this key
+    float sv[2];        // C → H: the carried means after C's last chunk
+    unsigned sk;        // C → H: the carried key
+    float iv[2];        // H → C: the state at a (re)start
+    unsigned ik;
+    int cmd;            // H → C: the slot to run next, or kPairEnd
+    int ret;            // H → both: the ended task's waiter (or -1)
+    int task;           // H → both: the worker's next task word (kernel loop)
+};
+constexpr int kPairEnd = -1;
+constexpr int kPairFrames = 8;  // batches of at most this many frames run their long paths on wave pairs
+
+// the chunk descriptor of a resolved chunk (one lane per step): steps n until the first blocked step or
+// through the path's top (finished), and the largest light key among them
+__device__ inline int pair_desc(int meta, unsigned lk, bool* fin, unsigned* maxlk) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long blocked = __ballot(!(meta & kLongOk));
+    const unsigned long long tops = __ballot((meta & kLongOk) && (meta & kStepTop));
+    const int fb = blocked ? __ffsll((long long)blocked) - 1 : 64;
+    const int ft = tops ? __ffsll((long long)tops) - 1 : 64;
+    *fin = ft < fb;
+    const int n = *fin ? ft + 1 : fb;
+    *maxlk = wave_reduce(lane < n ? lk : 0u, [](unsigned x, unsigned y) { return x > y ? x : y; });
+    return n;
+}
+
+// A long path (task word t) on the pair, from its cursor; both waves call it (role 0 = H, 1 = C) and both
+// return the task word of the parent path parked on its top (to run next), or -1. Per chunk both waves pass
+// two workgroup barriers: after the concurrent phase (C's steps of slot s ∥ H's build of the next chunk into
+// slot s ^ 1 and tail of the previous chunk) and after H's decision (the slot C runs next, or the end).
+__device__ int flow_pair(const Ws& w, int* ctl, int t, PairShared& sh, int keyfast, int role) {
+    const Dims& d = w.d;
+    const int lane = threadIdx.x & 63;
+    const int h = lane & 1;
+    const int g = t & kFlowIdMask;
+    const int f = g / (int)d.N, j = g - f * (int)d.N;
+    int* curp = w.cur + f * d.N + j;
+    const int top = w.ptop[f * d.N + j];
+    const int64_t lb = f * d.NL;
+#ifdef DOFS_FLOW_PROF
+    // measurement build: C's steps (p_steps) and its time between chunks (p_tail: barriers, H's decisions);
+    // H's concurrent work per chunk (p_next: the next chunk's build and the previous one's tail)
+    unsigned long long p_steps = 0, p_tail = 0, p_next = 0, p_skip = 0, p_cwait = 0, p_hwait = 0, p_t = wall_clock64();
+#endif
+    if (role == 1) {  // ---- C: the chain of every chunk H hands over ----
+        __syncthreads();  // H's setup
+        if (sh.cmd == kPairEnd) {
+            __syncthreads();
+            return -1;
+        }
+        float v = sh.iv[h];
+        unsigned K = sh.ik, kfast = 0;
+        int sl = 0;
+        for (;;) {
+            const int n = sh.n[sl];
+            const bool cont = n == 64 && !sh.fin[sl];
+            const unsigned krank = K & ~((1u << kRankShift) - 1);
+            const bool fastc = keyfast && sh.maxlk[sl] < krank;
+            const unsigned kstart = K;
+            FLOW_PROF_MARK(p_tail);
+            chain_chunk(sh.buf[sl], sh.ob[sl], n, fastc, h, v, K);
+            FLOW_PROF_MARK(p_steps);
+            kfast += fastc ? 1 : 0;
+            if (lane == 0) {
+                sh.fast[sl] = fastc ? 1 : 0;
+                sh.k0[sl] = kstart;
+                sh.sk = K;
+            }
+            if (lane < 2) sh.sv[lane] = v;
+            FLOW_PROF_MARK(p_tail);
+            __syncthreads();  // the chunk's outputs to H; H has built the next chunk into the other slot
+            FLOW_PROF_MARK(p_cwait);
+            if (cont) {  // H continues too (it decided from the same descriptor)
+                sl ^= 1;
+                continue;
+            }
+            __syncthreads();  // H's decision: the end, or a re-resolved chunk
+            if (sh.cmd == kPairEnd) break;
+            sl = sh.cmd;
+        }
+        const int ret = sh.ret;
+        if (lane == 0) {
+            fs_add(ctl, FS_KFAST, kfast);
+#ifdef DOFS_FLOW_PROF
+            fs_add(ctl, FS_P_STEPS, p_steps);
+            fs_add(ctl, FS_P_TAIL, p_tail);
+            fs_add(ctl, FS_P_CWAIT, p_cwait);
+#endif
+        }
+        __syncthreads();  // both read cmd and ret before H may write the next task's words
+        return ret;
+    }
+    // ---- H: everything but the chain ----
+    // the chunk in slot s (cursor qs): its records' metas, light boxes and descriptor; the pending tail of the
+    // chunk before it (slot p); the carried box; the resolve stages (FlowPipe's, in named registers)
+    int s = 0, qs = f_ld(curp), meta_s = 0, n_s = 0;
+    bool fin_s = false;
+    B4 lbb_s, bb;
+    bool havep = false;
+    int p = 0, qp = 0, metap = 0;
+    B4 lbbp;
+    unsigned chunks = 0, steps = 0, restarts = 1;
+    int ret = -1;
+    // the resolve stages in named registers rotated by unrolling (no register copies: a copy of a register
+    // whose load is in flight waits for it — the rotating form exposed a round trip per chunk). Stage k of
+    // the chunk built now: StepIn records in1 / in2 / in3 (chunks qs - 64, - 128, - 192), state words rdy1 /
+    // rdy2, and rv, the light records of chunk qs - 64; i0 .. i2 and r0 .. r2 hold them in rotation.
+    StepIn i0, i1, i2;
+    int r0, r1, r2;
+    RepVal rv;
+    // (re)fill the stages for the chunks after cursor q, synchronously: the explicit wait leaves no load in
+    // flight at the loop head, where this path meets the back edge (else the compiler's waits at the head
+    // merge both paths' pending loads and expose a round trip per pass)
+    auto restart_stages = [&](int q) {
+        i0 = pipe_in(w, lb, q - 64 - lane, top);
+        i1 = pipe_in(w, lb, q - 128 - lane, top);
+        i2 = pipe_in(w, lb, q - 192 - lane, top);
+        r0 = pipe_rdy(w, lb, i0, q - 64 - lane, top);
+        r1 = pipe_rdy(w, lb, i1, q - 128 - lane, top);
+        rv = pipe_rv(w, lb, i0, r0, q - 64 - lane, top);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    };
+    {
+        float mx, my;
+        int rank, root;
+        flow_start(w, f, qs + 1, &mx, &my, &rank, &root, &bb);
+        if (lane == 0) {
+            sh.iv[0] = mx;
+            sh.iv[1] = my;
+            sh.ik = rk_pack(rank, root);
+        }
+        OneRec rec;
+        meta_s = flow_resolve(w, lb, qs - lane, top, &rec, &lbb_s);
+        sh.buf[0][lane] = rec;
+        unsigned mk;
+        n_s = pair_desc(meta_s, rec.lk, &fin_s, &mk);
+        if (lane == 0) {
+            sh.n[0] = n_s;
+            sh.fin[0] = fin_s ? 1 : 0;
+            sh.maxlk[0] = mk;
+            sh.cmd = qs < top ? kPairEnd : 0;  // (never: a task is handed out only while its path is not complete)
+            sh.ret = -1;
+        }
+        restart_stages(qs);
+    }
+    __syncthreads();
+    if (sh.cmd == kPairEnd) {
+        __syncthreads();
+        return -1;
+    }
+    // H: the tail of the chunk in slot sl (cursor qc, n steps): the bbox prefix joined with the carried box,
+    // then the records the results read; the chunk's last record published if it ends the path or blocks
+    auto tail = [&](int sl, int qc, int n, bool last, const B4& lb4, int meta) {
+        B4 x = lb4;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const B4 y = bb_shfl_up(x, o);
+            if (lane >= o) x = bb_join(x, y);
+        }
+        x = bb_join(x, bb);
+        const int src = n > 0 ? n - 1 : 0;
+        const int lo = __shfl((int)((unsigned short)x.x0 | ((unsigned)(unsigned short)x.y0 << 16)), src, 64);
+        const int hi = __shfl((int)((unsigned short)x.x1 | ((unsigned)(unsigned short)x.y1 << 16)), src, 64);
+        if (n > 0) {
+            bb.x0 = (int16_t)(lo & 0xffff);
+            bb.y0 = (int16_t)(lo >> 16);
+            bb.x1 = (int16_t)(hi & 0xffff);
+            bb.y1 = (int16_t)(hi >> 16);
+        }
+        if (lane < n) {
+            const bool fastc = sh.fast[sl] != 0;
+            const float* fv = reinterpret_cast<const float*>(sh.ob[sl]);
+            const OneOut sx = sh.ob[sl][2 * lane], sy = sh.ob[sl][2 * lane + 1];
+            const float vx = fastc ? fv[lane] : sx.v, vy = fastc ? fv[64 + lane] : sy.v;
+            const unsigned kk = fastc ? sh.k0[sl] : sx.k;
+            const int rank = (int)(kk >> kRankShift), root = (int)(kk & ((1u << kRankShift) - 1));
+            RepVal* dst = w.Rv + lb + qc - lane;
+            if (lane == n - 1 && last) {
+                rv_publish(dst, vx, vy, rank, root, x);
+            } else if (!w.rv_lean || (meta & kStepKeep)) {
+                RepVal o;
+                o.mx = vx;
+                o.my = vy;
+                o.rank = rank;
+                o.root = root;
+                o.bb = x;
+                o.pad0 = o.pad1 = 0;
+                *dst = o;
+            }
+        }
+    };
+    // one chunk of H: 0 = continue (slot s advanced), 1 = the task ended (ret), 2 = restarted (canonical stages)
+    auto iter = [&](StepIn& in1, StepIn& in2, StepIn& in3, int& rdy1, int& rdy2, int& rdy3) -> int {
+        // concurrent phase: the next chunk into the other slot, whether or not this one continues (no branch
+        // around the stage loads), and the pending tail
+        FLOW_PROF_MARK(p_skip);
+        OneRec nrec;
+        B4 nlbb;
+        const int nmeta = pipe_build(in1, rdy1, rv, qs - 64 - lane, top, &nrec, &nlbb);
+        rv = pipe_rv(w, lb, in2, rdy2, qs - 128 - lane, top);  // issued now, used a chunk later
+        rdy3 = pipe_rdy(w, lb, in3, qs - 192 - lane, top);
+        in1 = pipe_in(w, lb, qs - 256 - lane, top);  // (in1 was consumed by pipe_build)
+        sh.buf[s ^ 1][lane] = nrec;
+        unsigned mk;
+        bool nfin;
+        const int nn = pair_desc(nmeta, nrec.lk, &nfin, &mk);
+        if (lane == 0) {
+            sh.n[s ^ 1] = nn;
+            sh.fin[s ^ 1] = nfin ? 1 : 0;
+            sh.maxlk[s ^ 1] = mk;
+        }
+        if (havep) {
+            tail(p, qp, 64, false, lbbp, metap);
+            havep = false;
+        }
+        FLOW_PROF_MARK(p_next);
+        __syncthreads();  // C's outputs of slot s
+        FLOW_PROF_MARK(p_hwait);
+        // decision: continue, or finish the chunk now (the path completes or blocks)
+        int cmd = 0, st = 0;
+        ++chunks;
+        steps += n_s;
+        if (n_s == 64 && !fin_s) {  // continue with the next slot; this chunk's tail overlaps C's next chunk
+            havep = true;
+            p = s;
+            qp = qs;
+            metap = meta_s;
+            lbbp = lbb_s;
+            s ^= 1;
+            qs -= 64;
+            meta_s = nmeta;
+            lbb_s = nlbb;
+            n_s = nn;
+            fin_s = nfin;
+            return 0;  // (C reads the same descriptor: no second barrier)
+        } else {
+            tail(s, qs, n_s, true, lbb_s, meta_s);
+            if (fin_s) {  // publish the top: records drained, then the state word; its waiter runs next
+                f_drain();
+                int old = 0;
+                if (lane == 0) {
+                    f_st(curp, -1);
+                    old = __hip_atomic_exchange(w.ready + lb + top, kFlowDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (t & kFlowLong) atomicAdd(ctl + FC_LDONE, 1);
+                    fs_add(ctl, FS_LDONE, 1);
+                    fs_max(ctl, FS_T_LONG, fs_now());
+                    if (top == 0) fs_max(ctl, FS_T_ROOT, fs_now());
+                }
+                old = __shfl(old, 0, 64);
+                ret = old < kFlowDone ? old : -1;
+                cmd = kPairEnd;
+                st = 1;
+            } else {  // blocked at pb on light child lq: park on it unless it completed meanwhile
+                const int pb = qs - n_s;
+                if (n_s == 0 && w.ord[lb + pb + 1] >= d.N && lane == 0)  // the state at pb + 1: C's carried one
+                    rv_publish(w.Rv + lb + pb + 1, sh.sv[0], sh.sv[1], (int)(sh.sk >> kRankShift),
+                               (int)(sh.sk & ((1u << kRankShift) - 1)), bb);
+                int parked = 0;
+                if (lane == 0) {
+                    f_st(curp, pb);
+                    f_drain();
+                    const int lq = w.In[lb + pb].lb;
+                    const int s0 = f_ld(w.ready + lb + lq);
+                    if (s0 != kFlowDone) parked = atomicCAS(w.ready + lb + lq, s0, t) == s0;
+                }
+                parked = __shfl(parked, 0, 64);
+                if (parked) {
+                    if (lane == 0) {
+                        fs_add(ctl, FS_LPARKS, 1);
+                        if (top == 0) fs_add(ctl, FS_RPARKS, 1);
+                    }
+                    ret = -1;
+                    cmd = kPairEnd;
+                    st = 1;
+                } else {  // completed meanwhile: re-resolve the chunk from the blocked step
+                    qs = pb;
+                    s ^= 1;
+                    OneRec rec;
+                    meta_s = flow_resolve(w, lb, qs - lane, top, &rec, &lbb_s, pb);
+                    sh.buf[s][lane] = rec;
+                    n_s = pair_desc(meta_s, rec.lk, &fin_s, &mk);
+                    if (lane == 0) {
+                        sh.n[s] = n_s;
+                        sh.fin[s] = fin_s ? 1 : 0;
+                        sh.maxlk[s] = mk;
+                    }
+                    ++restarts;
+                    cmd = s;
+                    st = 2;  // (the caller refills the stages)
+                }
+            }
+        }
+        if (lane == 0) {
+            sh.cmd = cmd;
+            sh.ret = ret;
+        }
+        __syncthreads();  // the decision to C
+        return st;
+    };
+    // three chunks per pass: the stages rotate through i0 .. i2 and r0 .. r2. The first pass after a (re)start
+    // is peeled off the steady loop, whose head is then reached only after a third chunk (the compiler's waits
+    // at a loop head merge its predecessors' loads in flight: a restart's would make them all vmcnt(0))
+    auto pass3 = [&]() -> int {
+        int st = iter(i0, i1, i2, r0, r1, r2);
+        if (st) return st;
+        st = iter(i1, i2, i0, r1, r2, r0);
+        if (st) return st;
+        return iter(i2, i0, i1, r2, r0, r1);
+    };
+    for (;;) {
+        int st = pass3();
+        while (st == 0) st = pass3();
+        if (st == 1) break;
+        restart_stages(qs);
+    }
+    if (lane == 0) {
+        fs_add(ctl, FS_LCHUNKS, chunks);
+        fs_add(ctl, FS_LSTEPS, steps);
+        fs_add(ctl, FS_RESTARTS, restarts);
+        if (top == 0) {
+            fs_add(ctl, FS_RCHUNKS, chunks);
+            fs_add(ctl, FS_RSTEPS, steps);
+        }
+#ifdef DOFS_FLOW_PROF
+        fs_add(ctl, FS_P_NEXT, p_next);
+        fs_add(ctl, FS_P_HWAIT, p_hwait);
+        (void)p_skip;
+        (void)p_cwait;
+        (void)p_steps;
+        (void)p_tail;
+#endif
+    }
+    __syncthreads();  // both read cmd and ret before H may write the next task's words
+    return ret;
+}
+
+// Long workers as wave pairs (flow_pair): one workgroup of two waves per worker, H (wave 0) and C (wave 1).
+// The task loop of k_replay_flow<true, ...>, with H taking the decisions and both waves helping with the
+// short pool when H finds no long task (each wave one claim).
+__global__ __launch_bounds__(128) void k_replay_flow_pair(Ws w, int* ctl, unsigned epoch, int keyfast) {
+    __shared__ PairShared sh;
+    const int lane = threadIdx.x & 63;
+    const int role = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nl = ctl[FC_NL];
+    int cb = 0, ce = 0;
+    int ticket = -1;
+    if (lane == 0) fs_min(ctl, FS_T0, fs_now());
+    __builtin_amdgcn_s_setprio(3);
+    for (int it = 0; it < (1 << 26); ++it) {
+        if (role == 0) {
+            const int t0 = flow_next_long(w, ctl, epoch, nl, &ticket);
+            if (lane == 0) sh.task = t0;
+        }
+        __syncthreads();
+        int t = sh.task;
+        if (t == -1) break;
+        if (t == kFlowHelpTask) {  // one claim of the initial short pool per wave, at the short workers' priority
+            __builtin_amdgcn_s_setprio(0);
+            flow_short(w, ctl, epoch, -1, 1, kFlowHelp, &cb, &ce);
+            __builtin_amdgcn_s_setprio(3);
+            __syncthreads();
+            continue;
+        }
+        const unsigned long long t1 = fs_now();
+        while (t >= 0) {
+            if (role == 0 && lane == 0) fs_add(ctl, FS_LRUNS, 1);
+            const int nx = flow_pair(w, ctl, t, sh, keyfast, role);
+            if (nx >= 0 && !(nx & kFlowLong)) {  // a short waiter: a one-lane short round on H (and its waiters)
+                if (role == 0) {
+                    if (lane == 0) fs_add(ctl, FS_INJECT, 1);
+                    flow_short(w, ctl, epoch, nx, 0, 0, &cb, &ce);
+                }
+                break;
+            }
+            t = nx;
+        }
+        __syncthreads();
+        if (role == 0 && lane == 0) fs_add(ctl, FS_LTICKS, fs_now() - t1);
+    }
+    if (lane == 0) fs_max(ctl, FS_T_EXIT, fs_now());
+}
+
 constexpr int kFlowShortW = 8;  // waves per short-worker workgroup
 constexpr int kFlowLongW = 4;    // waves per long-worker workgroup (one per SIMD)
 

@@ -2999,14 +2999,23 @@ struct HipBackend {
             // one stream (long workers first / short workers first) — the replay must complete either way
             const int order = g_flow_order;
             hipStream_t ls = order ? stream : flow_stream;
-            if (order != 2)
-                hipLaunchKernelGGL((k_replay_flow<true, kFlowLongW>), dim3((unsigned)gl), dim3(64 * kFlowLongW), 0, ls,
-                                   w, flow_ctl, flow_epoch, kf);
+            // wave pairs (chain and tail on two waves, flow_pair) for batches of at most kPairFrames frames, where
+            // a frame's longest chain bounds the replay (one 4K frame: replay 59.2 → 43.8 ms); one wave per long
+            // path for larger batches, where the long paths' throughput does and the pairs' extra waves slow the
+            // graph stage beside them (B = 112, same box: 1,860 / 1,861 Mpix/s single waves, 1,826 / 1,825 with
+            // 128 pairs, 1,826 / 1,824 with 256)
+            auto long_launch = [&] {
+                if (w.d.B <= kPairFrames)
+                    hipLaunchKernelGGL(k_replay_flow_pair, dim3((unsigned)std::max(1, flow_long_workers() / 2)),
+                                       dim3(128), 0, ls, w, flow_ctl, flow_epoch, kf);
+                else
+                    hipLaunchKernelGGL((k_replay_flow<true, kFlowLongW>), dim3((unsigned)gl), dim3(64 * kFlowLongW), 0, ls,
+                                       w, flow_ctl, flow_epoch, kf);
+            };
+            if (order != 2) long_launch();
             hipLaunchKernelGGL((k_replay_flow<false, kFlowShortW>), dim3((unsigned)gs), dim3(64 * kFlowShortW), 0, stream,
                                w, flow_ctl, flow_epoch, kf);
-            if (order == 2)
-                hipLaunchKernelGGL((k_replay_flow<true, kFlowLongW>), dim3((unsigned)gl), dim3(64 * kFlowLongW), 0, ls,
-                                   w, flow_ctl, flow_epoch, kf);
+            if (order == 2) long_launch();
             note(hipEventRecord(flow_ev[1], flow_stream), "hipEventRecord");
             note(hipStreamWaitEvent(stream, flow_ev[1], 0), "hipStreamWaitEvent");
         });

@@ -1,6 +1,7 @@
 """GPU: the dataflow replay completes whatever the order of its two worker launches.
 
-k_replay_flow runs as a long-path launch and a short-path launch (dofs_dataflow.h). Neither may wait for
+k_replay_flow runs as a long-path launch (one wave per long path, or wave pairs for batches of at most 8
+frames) and a short-path launch (dofs_dataflow.h). Neither may wait for
 work the other launch has yet to produce: long workers claim queue tickets only below the queue's tail
 (their slots' pushers are running) and help with the initial short pool when idle, and short workers never
 wait. dofs_debug_flow_order runs the two launches one after the other on one stream — long workers first
@@ -41,7 +42,8 @@ def _run(gpu, calib, flows, B, H, W, order):
     return err, ev, res
 
 
-@pytest.mark.parametrize("H,W,B", [(1080, 1920, 12), (270, 480, 24)])
+# B > 8: one wave per long path (k_replay_flow<true>); B <= 8: wave pairs (k_replay_flow_pair)
+@pytest.mark.parametrize("H,W,B", [(1080, 1920, 12), (270, 480, 24), (1080, 1920, 4), (540, 960, 8)])
 def test_flow_orders_complete_and_agree(gpu, calib, H, W, B):
     import torch
 
