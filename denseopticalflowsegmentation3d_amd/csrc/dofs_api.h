@@ -290,6 +290,15 @@ struct Context {
     }
 };
 
+// Waits for batch id `batch` and returns whether its dataflow replay gave up a bounded wait (C_FLOWERR of frame
+// 0): every accessor of the batch's results then fails with kFlowErrMsg instead of returning invalid data
+template <class Backend>
+bool flow_failed(Context<Backend>* cx, int64_t batch) {
+    const int slot = cx->slot_of(batch);
+    cx->be.event_sync(cx->evDone[slot]);
+    return cx->be.read_int(cx->pipe(slot).w.ctr + C_FLOWERR) != 0;
+}
+
 // Enqueue one batch on the context's streams, ordered after the work already on the caller's
 // (current) stream. On return the caller's stream is ordered after phase A, so it may overwrite
 // the input; results are joined by api_fetch / api_events / api_records_copy.
@@ -467,6 +476,7 @@ int api_segment_scores(Context<Backend>* cx, int64_t batch, int frame, double* o
     double* d = (double*)cx->scratch(sizeof(double) * (size_t)N);
     if (!d) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
     Backend& be = cx->be;
+    if (flow_failed(cx, batch)) return cx->fail(DOFS_ERR_DEVICE, kFlowErrMsg);
     cx->join(batch);
     if (P.w.d.M <= 0 || !P.pre)
         be.memset(d, 0, sizeof(double) * (size_t)N);
@@ -490,6 +500,7 @@ int api_final_roots(Context<Backend>* cx, int64_t batch, int frame, int32_t* out
     const Ws& w = P.w;
     const Dims& d = w.d;
     Backend& be = cx->be;
+    if (flow_failed(cx, batch)) return cx->fail(DOFS_ERR_DEVICE, kFlowErrMsg);
     cx->join(batch);
     std::vector<int32_t> rec;
     if (d.M <= 0) {  // one pixel
@@ -531,6 +542,7 @@ int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity
     if (frame < 0 || frame >= cx->meta[slot].B) return cx->fail(DOFS_ERR_INVALID_ARG, "no frame");
     if (cx->meta[slot].lean)
         return cx->fail(DOFS_ERR_INVALID_ARG, "the batch kept no event records: dofs_keep_events(ctx, 1) before it");
+    if (flow_failed(cx, cx->nbatch - 1)) return cx->fail(DOFS_ERR_DEVICE, kFlowErrMsg);
     cx->join(cx->nbatch - 1);
     const Ws& w = cx->pipe(slot).w;
     const Dims& d = w.d;

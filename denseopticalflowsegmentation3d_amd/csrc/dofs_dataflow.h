@@ -1324,9 +1324,11 @@ __global__ __launch_bounds__(128) void k_replay_flow_pair(Ws w, int* ctl, unsign
 constexpr int kFlowShortW = 8;  // waves per short-worker workgroup
 constexpr int kFlowLongW = 4;    // waves per long-worker workgroup (one per SIMD)
 
-// counter C_FLOWERR of frame 0 = a bounded wait of the launch gave up (dofs_batch_counters)
-__global__ void k_flow_report(Ws w, const int* ctl) {
-    if (threadIdx.x == 0 && blockIdx.x == 0 && ctl[FC_ERR]) w.C(0)[C_FLOWERR] = 1;
+// counter C_FLOWERR of frame 0 = a bounded wait of the launch gave up (dofs_batch_counters); force: a test
+// of the error's path through the accessors (dofs_debug_flow_giveup), the replay itself is complete
+__global__ void k_flow_report(Ws w, const int* ctl, int force) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && (ctl[FC_ERR] || force)) w.C(0)[C_FLOWERR] = 1;
 }
+inline int g_flow_giveup = 0;  // host: dofs_debug_flow_giveup (test only)
 
 }  // namespace dofs

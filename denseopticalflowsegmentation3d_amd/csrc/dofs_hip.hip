@@ -3019,7 +3019,7 @@ struct HipBackend {
             note(hipEventRecord(flow_ev[1], flow_stream), "hipEventRecord");
             note(hipStreamWaitEvent(stream, flow_ev[1], 0), "hipStreamWaitEvent");
         });
-        hipLaunchKernelGGL(k_flow_report, dim3(1), dim3(64), 0, stream, w, flow_ctl);
+        hipLaunchKernelGGL(k_flow_report, dim3(1), dim3(64), 0, stream, w, flow_ctl, g_flow_giveup);
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_replay_flow launch");
         return true;
     }
@@ -3261,6 +3261,13 @@ extern "C" int dofs_debug_sort_k32e(int e) {
 // Diagnosis only: fix-up on / off (the truncated order is not Kruskal's: results differ), and a copy of
 // the next packed batch's sorted (key, value) pairs — at most cap — into device buffers.
 extern "C" void dofs_debug_sort_fix(int on) { dofs::g_sort_fix = on != 0; }
+// Test knob: the batches issued while on = 1 report a replay give-up (C_FLOWERR) although their replay
+// completed — the error path through the accessors (records copy, fetch, gather). Returns the previous value.
+extern "C" int dofs_debug_flow_giveup(int on) {
+    const int old = dofs::g_flow_giveup;
+    if (on >= 0) dofs::g_flow_giveup = on ? 1 : 0;
+    return old;
+}
 // Test knob: constant-key chunks of the long-path replay (dofs_dataflow.h g_keyfast; 1 = on, the default).
 // Returns the previous value; on < 0 only reads it.
 extern "C" int dofs_debug_replay_keyfast(int on) {
