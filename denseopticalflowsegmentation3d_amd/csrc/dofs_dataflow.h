@@ -256,7 +256,7 @@ __device__ inline int flow_resolve(const Ws& w, int64_t lb, int p, int top, OneR
     lbb->x0 = lbb->y0 = 0x7fff;
     lbb->x1 = lbb->y1 = -1;
     if (p < top) return 0;
-    const StepIn in = w.In[lb + p];
+    const StepV in = step_v(w.In[lb + p], p, w.d.W);
     int meta = in.meta;
     int lrank = 0, lroot = in.lb;
     if (in.meta & kStepDyn) {
@@ -305,18 +305,20 @@ __device__ inline StepIn pipe_in(const Ws& w, int64_t lb, int p, int top) {
     return w.In[lb + (p >= top ? p : top)];  // (p < top: meta is ignored, pipe_build checks p)
 }
 __device__ inline int pipe_rdy(const Ws& w, int64_t lb, const StepIn& in, int p, int top) {
-    const bool dyn = p >= top && (in.meta & kStepDyn);
-    return f_ld(w.ready + lb + (dyn ? in.lb : top));
+    const bool dyn = p >= top && (step_meta(in) & kStepDyn);
+    return f_ld(w.ready + lb + (dyn ? step_lq(in, p) : top));
 }
 __device__ inline RepVal pipe_rv(const Ws& w, int64_t lb, const StepIn& in, int rdy, int p, int top) {
-    const bool need = p >= top && (in.meta & kStepDyn) && rdy == kFlowDone;
-    return rv_fetch(w.Rv + lb + (need ? in.lb : top));  // read before the state word was seen done: unused
+    const bool need = p >= top && (step_meta(in) & kStepDyn) && rdy == kFlowDone;
+    return rv_fetch(w.Rv + lb + (need ? step_lq(in, p) : top));  // read before the state word was seen done: unused
 }
 // flow_resolve from the pipeline's loaded values (same record, same meta)
-__device__ inline int pipe_build(const StepIn& in, int rdy, const RepVal& lv, int p, int top, OneRec* o, B4* lbb) {
+__device__ inline int pipe_build(const Ws& w, const StepIn& sin, int rdy, const RepVal& lv, int p, int top, OneRec* o,
+                                 B4* lbb) {
     lbb->x0 = lbb->y0 = 0x7fff;
     lbb->x1 = lbb->y1 = -1;
     if (p < top) return 0;
+    const StepV in = step_v(sin, p, w.d.W);
     int meta = in.meta;
     int lrank = 0, lroot = in.lb;
     if (in.meta & kStepDyn) {
@@ -527,7 +529,7 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
         RepVal rv2;
         int rdy3 = kFlowDone;
         StepIn in4;
-        nmeta = pipe_build(P.in1, P.rdy1, P.rv1, q - 64 - lane, top, &nrec, &nlbb);
+        nmeta = pipe_build(w, P.in1, P.rdy1, P.rv1, q - 64 - lane, top, &nrec, &nlbb);
         rv2 = pipe_rv(w, lb, P.in2, P.rdy2, q - 128 - lane, top);  // issued now, used a chunk later
         rdy3 = pipe_rdy(w, lb, P.in3, q - 192 - lane, top);
         in4 = pipe_in(w, lb, q - 256 - lane, top);
@@ -625,7 +627,7 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             if (lane == 0) {
                 f_st(curp, pb);
                 f_drain();
-                const int lq = w.In[lb + pb].lb;
+                const int lq = step_lq(w.In[lb + pb], pb);
                 const int s0 = f_ld(w.ready + lb + lq);
                 if (s0 != kFlowDone)
                     parked = atomicCAS(w.ready + lb + lq, s0, t) == s0;
@@ -729,7 +731,7 @@ __device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch
             break;
         }
         if (t < 0) continue;
-        const StepIn in = w.In[lb + q];
+        const StepV in = step_v(w.In[lb + q], q, d.W);
         float wbx = in.wbx, wby = in.wby;
         int lrank = 0, lroot = in.lb;
         B4 lbb;
@@ -1137,7 +1139,7 @@ __device__ int flow_pair(const Ws& w, int* ctl, int t, PairShared& sh, int keyfa
         FLOW_PROF_MARK(p_skip);
         OneRec nrec;
         B4 nlbb;
-        const int nmeta = pipe_build(in1, rdy1, rv, qs - 64 - lane, top, &nrec, &nlbb);
+        const int nmeta = pipe_build(w, in1, rdy1, rv, qs - 64 - lane, top, &nrec, &nlbb);
         rv = pipe_rv(w, lb, in2, rdy2, qs - 128 - lane, top);  // issued now, used a chunk later
         rdy3 = pipe_rdy(w, lb, in3, qs - 192 - lane, top);
         in1 = pipe_in(w, lb, qs - 256 - lane, top);  // (in1 was consumed by pipe_build)
@@ -1200,7 +1202,7 @@ __device__ int flow_pair(const Ws& w, int* ctl, int t, PairShared& sh, int keyfa
                 if (lane == 0) {
                     f_st(curp, pb);
                     f_drain();
-                    const int lq = w.In[lb + pb].lb;
+                    const int lq = step_lq(w.In[lb + pb], pb);
                     const int s0 = f_ld(w.ready + lb + lq);
                     if (s0 != kFlowDone) parked = atomicCAS(w.ready + lb + lq, s0, t) == s0;
                 }

@@ -1508,9 +1508,10 @@ __device__ __forceinline__ void seq_find(int* par, int (&x)[K], const bool (&act
 struct alignas(16) SeqRec {
     int par, pad, lab, sz;
 };
+static_assert(sizeof(SeqRec) == sizeof(StepIn), "the sweep's records live in the StepIn region, one per position");
 struct KSeqInitRec {
     SeqRec* rec;
-    int64_t NL2;  // records per frame stride (StepIn region: 2 records per StepIn)
+    int64_t NL2;  // records per frame stride (StepIn region: NL records of StepIn's size)
     DOFS_HD void operator()(int f, int64_t x) const {
         SeqRec r;
         r.par = (int)x;
@@ -2798,7 +2799,7 @@ struct HipBackend {
     // constant-key replay (round 3, B = 112, same box) every CU: 256 workgroups 1,593 / 1,586 / 1,584 / 1,587
     // Mpix/s against 240 (1/16 of the CUs left to the replay) 1,551 / 1,543 / 1,549 / 1,544
     void krt_seq(const Ws& w) {
-        launch(w.d.B, w.d.N, KSeqInitRec{reinterpret_cast<SeqRec*>(w.In), 2 * w.d.NL});
+        launch(w.d.B, w.d.N, KSeqInitRec{reinterpret_cast<SeqRec*>(w.In), w.d.NL});
         int nwg = 256;
         (void)hipDeviceGetAttribute(&nwg, hipDeviceAttributeMultiprocessorCount, device);
         Ws wk = w;

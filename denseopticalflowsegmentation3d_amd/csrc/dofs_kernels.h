@@ -25,13 +25,24 @@
 namespace dofs {
 
 // Inputs of the merge at preorder position q (node x, heavy child h, light child l), precomputed in
-// parallel; the replay then only carries the order-dependent state (mean, rank, root).
+// parallel; the replay then only carries the order-dependent state (mean, rank, root). Stored packed, 16 B
+// per position (StepIn, written by KPathInit at random positions and read by the replay in position order);
+// the replay decodes it (step_v) into
 //   fs = (float)size(h)      r = 1 / (double)size(x)
 //   wb = float(mean(l) * (float)size(l))  — static when l is a pixel (la = its x | y << 16,
 //        lb = its id: rank 0, root = itself); when l is a merge node (kStepDyn) its mean, rank,
 //        root and bbox are produced by the replay itself: la holds size(l) and lb its preorder
 //        position, and they are read once l's path has completed.
+// Round 5: the record was these 32 bytes as stored; everything but the pixel's flow and id derives from the
+// two children's sizes and the position (heavy-first preorder: the light child follows the heavy subtree,
+// at q + 2 size(h)), so 16 bytes hold it — half the random stores of KPathInit and the replay's reads.
 struct StepIn {
+    unsigned hs;     // size(h) (bits 0-25, H*W < 2^26) | the kStep* flags << 26
+    int lt;          // a merge light child (kStepDyn): size(l); a pixel: its id
+    float wbx, wby;  // a pixel light child's blurred flow (· size 1); 0 for a merge
+};
+static_assert(sizeof(StepIn) == 16, "StepIn is one 16-byte record");
+struct StepV {  // a decoded StepIn (step_v)
     float fs;
     float wbx, wby;
     int meta;
@@ -39,11 +50,37 @@ struct StepIn {
     int la;
     int lb;
 };
-static_assert(sizeof(StepIn) == 32, "StepIn is one 32-byte record");
 constexpr int kStepB = 1;    // light child is the end side (B) of the merge
 constexpr int kStepTop = 2;  // x is the top of its heavy path
 constexpr int kStepDyn = 4;  // light child is a merge node (value produced by the replay)
 constexpr int kStepKeep = 16;  // (8: kLongOk, dofs_hip.hip) size(x) >= min_size: scoring may read x's replay record (Ws::rv_lean)
+constexpr int kStepShift = 26;  // StepIn::hs: the flags above size(h)
+constexpr unsigned kStepSizeMask = (1u << kStepShift) - 1u;
+DOFS_HD inline int step_meta(const StepIn& in) { return (int)(in.hs >> kStepShift); }
+// a merge light child's preorder position (kStepDyn only)
+DOFS_HD inline int step_lq(const StepIn& in, int64_t q) { return (int)(q + 2 * (int64_t)(in.hs & kStepSizeMask)); }
+// decode the record at position q of a frame W pixels wide: the same values the 32-byte record held
+DOFS_HD inline StepV step_v(const StepIn& in, int64_t q, int W) {
+    StepV v;
+    const int sh = (int)(in.hs & kStepSizeMask);
+    v.meta = step_meta(in);
+    v.fs = (float)sh;
+    if (v.meta & kStepDyn) {
+        const int sl = in.lt;
+        v.r = 1. / (double)(sh + sl);  // size(x)
+        v.wbx = v.wby = 0.f;
+        v.la = sl;
+        v.lb = (int)(q + 2 * (int64_t)sh);
+    } else {
+        const int lt = in.lt;
+        v.r = 1. / (double)(sh + 1);
+        v.wbx = in.wbx;
+        v.wby = in.wby;
+        v.la = (lt % W) | ((lt / W) << 16);
+        v.lb = lt;
+    }
+    return v;
+}
 
 // Workspace: device pointers (frame-major; per-frame strides by size class) + constants.
 struct Ws {
@@ -1183,22 +1220,20 @@ constexpr int kParkBase = kIntMax - 2;  // long path stopped in round r: kParkBa
 DOFS_HD inline StepIn step_in(const Ws& w, int f, int q, bool top, int lt, int lB, unsigned long long hl) {
     const Dims& d = w.d;
     const int sh = (int)(unsigned)(hl & 0xffffffffu), sl = (int)(unsigned)(hl >> 32);
+    (void)q;
+    int meta = (lB ? kStepB : 0) | (top ? kStepTop : 0) | (sh + sl >= w.min_size ? kStepKeep : 0);
     StepIn in;
-    in.fs = (float)sh;
-    in.r = 1. / (double)(sh + sl);  // size(x)
-    in.meta = (lB ? kStepB : 0) | (top ? kStepTop : 0) | (sh + sl >= w.min_size ? kStepKeep : 0);
     if (lt < d.N) {
         const F2 v = w.blur[f * d.N + lt];
         in.wbx = v.x * (float)1;
         in.wby = v.y * (float)1;
-        in.la = (lt % d.W) | ((lt / d.W) << 16);
-        in.lb = lt;
+        in.lt = lt;
     } else {
-        in.meta |= kStepDyn;
+        meta |= kStepDyn;  // (the light child's position q + 2 sh follows from the record's own)
         in.wbx = in.wby = 0.f;
-        in.la = sl;
-        in.lb = q + 2 * sh;  // heavy-first preorder: the light child follows the heavy subtree
+        in.lt = sl;
     }
+    in.hs = (unsigned)sh | ((unsigned)meta << kStepShift);
     return in;
 }
 
@@ -1339,7 +1374,7 @@ struct KReplay {
         RunState s;
         path_start(w, f, q + 1, &s.mx, &s.my, &s.rank, &s.root, &s.bb);
         for (;;) {
-            const StepIn in = w.In[lb + q];
+            const StepV in = step_v(w.In[lb + q], q, d.W);
             float wbx = in.wbx, wby = in.wby;
             int lrank = 0, lroot = in.lb;
             B4 lbb;

@@ -63,9 +63,10 @@ for b in range(NB):
         tops = {int(t): j for j, t in enumerate(ptop[f, :npaths])}
         for j in inc[:6]:
             q, top = int(cur[f, j]), int(ptop[f, j])
-            rec = d2h(in_p, 32 * (f * NL + q), 32, np.uint8)
-            meta = int(rec[12:16].view(np.int32)[0])
-            lb = int(rec[28:32].view(np.int32)[0])
+            rec = d2h(in_p, 16 * (f * NL + q), 16, np.uint8)  # StepIn (16 B): hs = size(h) | flags << 26, lt, wb
+            hs = int(rec[0:4].view(np.uint32)[0])
+            meta = hs >> 26
+            lb = q + 2 * (hs & ((1 << 26) - 1)) if meta & 4 else int(rec[4:8].view(np.int32)[0])
             line = f"  path {j}: top {top} cursor {q} len {q - top + 1} meta {meta}"
             if meta & 4:
                 st = int(d2h(ready_p, 4 * (f * NL + lb), 4, np.int32)[0])
