@@ -35,7 +35,6 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 GATHER_PER_FRAME = 64  # box records per frame in the gathered block
 ROUNDS_MAX = 40        # dofs_common.h kRoundsMax (Borůvka round flags and tile census entries per frame)
 ROUND_FLAG = 16        # counters: C_ACT + r = Borůvka round r found a cross-component edge
-C_LONGM = 57           # counters: merges on long heavy paths
 
 # Algorithmic (compulsory) bytes of the probed kernels, per unit:
 #   k_boruvka_min4 — Borůvka pass 0 (frames of width % 4 == 0). Units: a pixel of a tile the launch
@@ -48,15 +47,21 @@ C_LONGM = 57           # counters: merges on long heavy paths
 #   k_krt_fused — unit: a merge: its endpoints in (8 B), its node size out (4 B), two child seed words
 #     of the preorder's pointer jumping out (16 B), heavy/light and path-top flags out (3 B), and one
 #     16-B union-find record of the sweep read = 47 B.
-#   k_replay_long — unit: a merge on a long heavy path: its step inputs (StepIn, 32 B) in and its
-#     replay record (RepVal, 32 B) out = 64 B (a light merge child's 32-B record read is not counted).
-#   k_replay_flow — the whole replay in one dataflow launch; unit: a merge (every merge of the batch):
-#     StepIn 32 B in, RepVal 32 B out = 64 B.
-# k_replay_flow: the StepIn record read per merge; the 32-byte replay record is stored only where it is read
-# (path tops, parked states, merges of >= min_size pixels: DESIGN.md §2.6c) and not counted — a lower bound
+#   k_replay_flow — the whole replay in one dataflow launch (round 5): its 16-byte StepIn read per merge,
+#     a 32-byte replay record stored per merge the results read (size >= min_size: C_KEEP) and 24 bytes
+#     published per heavy path's top (C_PATHS) = 16 M + 32 keep + 24 paths (parks' states, a few thousand a
+#     batch, are not counted).
+#   KPathInit — per merge its inputs (position 4, path-top flag 1, KRT children 8, light side 1, children's
+#     sizes 8 = 22 B) and its 16-byte StepIn out; a pixel light child's blurred flow (8 B; N - paths of them:
+#     every pixel but a path's bottom is one light child); per path top its bottom (lscan, lposr: 8 B) and
+#     its state word, cursor, top and list entry (16 B) = 38 M + 8 (N - paths) + 24 paths.
+#   k_pre_sweep — per merge its jump word 8, children's sizes 8, KRT children 8 and light side 1 in, its
+#     position 4 out = 29 B (the tops' pushed positions, one per block top, are not counted).
 BYTES = {"k_boruvka_min4": (12, 16), "k_boruvka_pick4": 16, "k_boruvka_min": (24, 16), "k_krt_fused": 47,
-         "k_replay_long": 64, "k_replay_flow": 32}
-PROBES = ("k_boruvka_min4", "k_boruvka_pick4", "k_krt_fused", "k_replay_flow", "k_replay_long")
+         "k_replay_flow": (16, 32, 24), "KPathInit": (38, 8, 24), "k_pre_sweep": 29}
+PROBES = ("k_boruvka_min4", "k_boruvka_pick4", "k_krt_fused", "k_replay_flow", "k_pre_sweep", "KPathInit")
+C_PATHS = 0            # counters: heavy paths
+C_KEEP = 54            # counters: merges whose replay record the lean replay stores
 C_FLOWERR = 58         # counters (frame 0): the dataflow replay gave up a bounded wait
 INPUT_SETS = 3         # distinct resident input batches, rotated over the steps
 # measurement-only knobs of the library that make results invalid (they skip work): refused
@@ -403,20 +408,28 @@ def main(argv=None):
         if name == "k_boruvka_min":
             p0, p1, _ = boruvka_min_units(tiles, cnt, N)
             return p0 * BYTES[name][0] + p1 * BYTES[name][1], {"pass0_px": p0, "pass1_px": p1}
-        if name in ("k_krt_fused", "k_replay_flow"):
-            return BYTES[name] * (N - 1) * B, {"merges": (N - 1) * B}
-        if name == "k_replay_long":
-            lm = int(cnt[:, C_LONGM].sum())
-            return BYTES[name] * lm, {"long_path_merges": lm}
+        M = (N - 1) * B
+        paths, keep = int(cnt[:, C_PATHS].sum()), int(cnt[:, C_KEEP].sum())
+        if name == "k_krt_fused":
+            return BYTES[name] * M, {"merges": M}
+        if name == "k_replay_flow":
+            a, b, c = BYTES[name]
+            return a * M + b * keep + c * paths, {"merges": M, "kept_records": keep, "paths": paths}
+        if name == "KPathInit":
+            a, b, c = BYTES[name]
+            return a * M + b * (N * B - paths) + c * paths, {"merges": M, "paths": paths}
+        if name == "k_pre_sweep":
+            return BYTES[name] * M, {"merges": M}
         return None, None
 
     UNIT_TEXT = {"k_boruvka_min4": "12 per pixel of a processed tile + 16 per record written",
                  "k_boruvka_pick4": "16 per record read",
                  "k_boruvka_min": "24 (pass 0) / 16 (pass 1) per pixel of a processed tile",
                  "k_krt_fused": f"{BYTES['k_krt_fused']} per merge",
-                 "k_replay_flow": f"{BYTES['k_replay_flow']} per merge (StepIn 32 B in; the RepVal stores where "
-                                  "read are not counted)",
-                 "k_replay_long": f"{BYTES['k_replay_long']} per long-path merge"}
+                 "k_replay_flow": "16 per merge (StepIn in) + 32 per stored record (size >= min_size) + 24 per "
+                                  "path top published",
+                 "KPathInit": "38 per merge + 8 per pixel light child + 24 per path top",
+                 "k_pre_sweep": f"{BYTES['k_pre_sweep']} per merge"}
     kern = []
     for name, (ms, launches) in probes.items():
         if not launches:
@@ -434,7 +447,7 @@ def main(argv=None):
             ach = alg / (ms / 1e3) / 1e9
             entry.update({"achieved": round(ach, 3), "frac": round(ach / HBM_PEAK_GBS, 6),
                           "alg_bytes_per_launch": round(alg / launches)})
-            pk = pmc.get(name) or pmc.get(name + "1")  # k_replay_long's one-wave kernel is k_replay_long1
+            pk = pmc.get(name)
             if pk and pk.get("hbm_bytes_per_launch"):
                 entry["traffic"] = round(pk["hbm_bytes_per_launch"])
                 entry["traffic_over_alg"] = round(pk["hbm_bytes_per_launch"] / (alg / launches), 3)

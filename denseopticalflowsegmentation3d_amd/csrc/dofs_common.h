@@ -76,6 +76,7 @@ enum Counter {
     C_TINY = 15,  // short heavy paths of at most kTinyPath merges (listed from the back of list_short)
     C_OVF = 14,   // snapshot count of a frame whose records overflowed the capacity (0: no overflow)
     C_ACT = 16,  // C_ACT + r: Borůvka round r found a cross-component edge (r < kRoundsMax)
+    C_KEEP = 54,     // merges whose replay record the lean replay stores (size >= min_size; KPathInit)
     C_OVF_ANY = 56,  // frame 0 only: 1 if any frame of the batch overflowed its snapshot records
     C_LONGM = 57,    // merges on long heavy paths (replayed by the wave-per-path kernel)
     C_FLOWERR = 58,  // frame 0 only: the dataflow replay gave up a bounded wait (results invalid)
@@ -83,6 +84,8 @@ enum Counter {
     C_SORTFIX = 60,  // frame 0 only, 3 counters: pairs the MST sort fix-up moved, its fallback flag, barrier
     C_BMAX = 63      // the frame's largest |blurred flow component| (float bits, atomicMax by the HIP blur)
 };
+// Borůvka's round flags C_ACT + r use r < ceil(log2(H*W)) + 2 <= 28 (H*W < 2^26): C_KEEP sits above them
+static_assert(C_ACT + 28 < C_KEEP, "counter layout");
 
 constexpr uint32_t kNoEdge = 0xFFFFFFFFu;
 constexpr int kIntMax = 0x7FFFFFFF;

@@ -1268,6 +1268,8 @@ struct KPathInit {  // one lane per merge node x = N + k; path ids and lists thr
         // runs as long as its longest path): tiny ones from the back of list_short, the rest from
         // its front (together at most one per merge < N: the two never meet)
         const bool tiny = top && !islong && qb - q <= kTinyPath;
+        // merges whose replay record the lean replay stores (the replay's byte census, bench.py)
+        (void)t.take(w.C(f) + C_KEEP, valid && w.SZ[lb + x] >= w.min_size);
         int j, jl, js;
         t.take3(w.C(f) + C_PATHS, top, w.C(f) + C_LONG, islong, w.C(f) + C_SHORT, top && !islong && !tiny, &j, &jl,
                 &js);

@@ -161,14 +161,16 @@ struct Pipeline {
         };
         w.tmp = (F2*)take_dead(sizeof(F2) * B * N);  // row blur, Borůvka records
         w.blur = (F2*)take(sizeof(F2) * B * N);
-        w.comp = (int*)take(4 * B * N);  // Borůvka labels; the round-based replay's park lists
+        // Borůvka labels; the emulator's round-based replay's park lists (the HIP replay is one dataflow
+        // launch: dead after phase A there)
+        w.comp = (int*)(Backend::kReplayFlow ? take_dead(4 * B * N) : take(4 * B * N));
         w.bw = (unsigned long long*)take(8 * B * N);  // Borůvka minima; the dataflow replay's queue
         w.bi = (unsigned*)take_dead(4 * B * N);
         w.uf = (int*)take(4 * B * N);
         w.lposr = w.uf;  // the MST's union-find is dead once the KRT starts
         w.mstbits = (int*)take_dead(4 * B * N);
         w.cnt = (int*)take_dead(4 * B * N);
-        w.off = (int*)take(4 * B * N);  // park lists (round-based replay)
+        w.off = (int*)(Backend::kReplayFlow ? take_dead(4 * B * N) : take(4 * B * N));  // MST offsets; park lists (rounds)
         w.key_in = (unsigned long long*)take(8 * B * M);
         w.hls = w.key_in;  // the KRT's children sizes for KPathInit: the sort input is dead by then
         w.val_in = (unsigned*)take_dead(4 * B * M);
