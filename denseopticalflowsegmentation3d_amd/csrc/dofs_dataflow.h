@@ -293,11 +293,6 @@ __device__ inline int flow_resolve(const Ws& w, int64_t lb, int p, int top, OneR
 // d = 1 the records, and chunk q - 64 is built into LDS from them at the next chunk's start. Each stage's
 // loads have one chunk's steps to arrive; a restart (a task's first chunk, or a re-resolve after a park
 // that found its child done) fills the stages synchronously.
-struct FlowPipe {
-    StepIn in1, in2, in3;  // this lane's StepIn in chunks q - 64, q - 128, q - 192
-    int rdy1, rdy2;        // their light children's state words (kFlowDone where not dynamic)
-    RepVal rv1;            // the light child's record (chunk q - 64, dynamic and done)
-};
 // Branch-free loads: a lane that needs none reads a line the wave reads anyway (its path top's), so no
 // loaded register is merged with a constant at a branch join (the merge made the compiler wait for the
 // load right after issuing it).
@@ -344,15 +339,6 @@ __device__ inline int pipe_build(const Ws& w, const StepIn& sin, int rdy, const 
     o->lkp = o->lk + (1u << kRankShift);
     o->bm = (meta & kStepB) ? ~0u : 0u;
     return meta;
-}
-// fill the stages for chunks q - 64 .. q - 192 (synchronous: three round trips)
-__device__ inline void pipe_restart(const Ws& w, int64_t lb, int q, int top, int lane, FlowPipe& P) {
-    P.in1 = pipe_in(w, lb, q - 64 - lane, top);
-    P.in2 = pipe_in(w, lb, q - 128 - lane, top);
-    P.in3 = pipe_in(w, lb, q - 192 - lane, top);
-    P.rdy1 = pipe_rdy(w, lb, P.in1, q - 64 - lane, top);
-    P.rdy2 = pipe_rdy(w, lb, P.in2, q - 128 - lane, top);
-    P.rv1 = pipe_rv(w, lb, P.in1, P.rdy1, q - 64 - lane, top);
 }
 
 // The chain of one 64-step chunk (Forest::merge's running mean and union-by-rank key, graph.cpp:177-213):
@@ -490,8 +476,6 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
     buf[cb][lane] = rec;
     unsigned curlk = rec.lk;  // this lane's step key in the current chunk (valid for lanes < n)
     unsigned chunks = 0, steps = 0, kfast = 0, restarts = 1;  // anatomy, added once per call
-    FlowPipe P;
-    pipe_restart(w, lb, q, top, lane, P);
 #ifdef DOFS_FLOW_PROF
     unsigned long long p_steps = 0, p_tail = 0, p_next = 0, p_t = wall_clock64();
 #define FLOW_PROF_MARK(acc)                                 \
@@ -522,17 +506,32 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             }
         }
     };
-    for (;;) {
+    // the resolve stages in named registers rotated by a three-way unroll (as flow_pair's: a register copy of
+    // an in-flight load waits for it, so the rotating form exposed a memory round trip per chunk): in1 / in2 /
+    // in3 the StepIn records of chunks q - 64 / - 128 / - 192, rdy1 / rdy2 the state words, rv the light
+    // records of chunk q - 64
+    StepIn i0, i1, i2;
+    int r0, r1, r2;
+    RepVal rv;
+    auto restart_stages = [&](int qq) {
+        i0 = pipe_in(w, lb, qq - 64 - lane, top);
+        i1 = pipe_in(w, lb, qq - 128 - lane, top);
+        i2 = pipe_in(w, lb, qq - 192 - lane, top);
+        r0 = pipe_rdy(w, lb, i0, qq - 64 - lane, top);
+        r1 = pipe_rdy(w, lb, i1, qq - 128 - lane, top);
+        rv = pipe_rv(w, lb, i0, r0, qq - 64 - lane, top);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nothing in flight where this path meets the back edge
+    };
+    restart_stages(q);
+    int ret = -1;
+    // one chunk: 0 = continue, 1 = the task ended (ret), 2 = re-resolved after a park found its child done
+    auto iter = [&](StepIn& in1, StepIn& in2, StepIn& in3, int& rdy1, int& rdy2, int& rdy3) -> int {
         OneRec nrec;
         B4 nlbb;
-        int nmeta;
-        RepVal rv2;
-        int rdy3 = kFlowDone;
-        StepIn in4;
-        nmeta = pipe_build(w, P.in1, P.rdy1, P.rv1, q - 64 - lane, top, &nrec, &nlbb);
-        rv2 = pipe_rv(w, lb, P.in2, P.rdy2, q - 128 - lane, top);  // issued now, used a chunk later
-        rdy3 = pipe_rdy(w, lb, P.in3, q - 192 - lane, top);
-        in4 = pipe_in(w, lb, q - 256 - lane, top);
+        const int nmeta = pipe_build(w, in1, rdy1, rv, q - 64 - lane, top, &nrec, &nlbb);
+        rv = pipe_rv(w, lb, in2, rdy2, q - 128 - lane, top);  // issued now, used a chunk later
+        rdy3 = pipe_rdy(w, lb, in3, q - 192 - lane, top);
+        in1 = pipe_in(w, lb, q - 256 - lane, top);  // (in1 was consumed by pipe_build)
         const unsigned long long blocked = __ballot(!(meta & kLongOk));
         const unsigned long long tops = __ballot((meta & kLongOk) && (meta & kStepTop));
         const int fb = blocked ? __ffsll((long long)blocked) - 1 : 64;
@@ -612,8 +611,8 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
                 if (top == 0) fs_max(ctl, FS_T_ROOT, fs_now());
             }
             old = __shfl(old, 0, 64);
-            tally();
-            return old < kFlowDone ? old : -1;
+            ret = old < kFlowDone ? old : -1;
+            return 1;
         }
         if (n < 64) {  // blocked at pb on light child lq: park on it unless it completed meanwhile
             const int pb = q - n;
@@ -629,8 +628,7 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
                 f_drain();
                 const int lq = step_lq(w.In[lb + pb], pb);
                 const int s0 = f_ld(w.ready + lb + lq);
-                if (s0 != kFlowDone)
-                    parked = atomicCAS(w.ready + lb + lq, s0, t) == s0;
+                if (s0 != kFlowDone) parked = atomicCAS(w.ready + lb + lq, s0, t) == s0;
             }
             parked = __shfl(parked, 0, 64);
             if (parked) {
@@ -638,32 +636,42 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
                     fs_add(ctl, FS_LPARKS, 1);
                     if (top == 0) fs_add(ctl, FS_RPARKS, 1);
                 }
-                tally();
-                return -1;
+                ret = -1;
+                return 1;
             }
-            q = pb;  // completed meanwhile: re-resolve the chunk from the blocked step
+            q = pb;  // completed meanwhile: re-resolve the chunk from the blocked step (the caller refills the stages)
             __builtin_amdgcn_wave_barrier();
-            meta = flow_resolve(w, lb, q - lane, top, &rec, &lbb, pb);
-            buf[cb][lane] = rec;
-            curlk = rec.lk;
-            pipe_restart(w, lb, q, top, lane, P);  // the stages were for the old cursor
+            OneRec rec2;
+            meta = flow_resolve(w, lb, q - lane, top, &rec2, &lbb, pb);
+            buf[cb][lane] = rec2;
+            curlk = rec2.lk;
             ++restarts;
-            continue;
+            return 2;
         }
         q -= 64;
         cb ^= 1;
         meta = nmeta;
         lbb = nlbb;
-        P.in1 = P.in2;
-        P.rdy1 = P.rdy2;
-        P.rv1 = rv2;
-        P.in2 = P.in3;
-        P.rdy2 = rdy3;
-        P.in3 = in4;
         FLOW_PROF_MARK(p_tail);
         buf[cb][lane] = nrec;
         curlk = nrec.lk;
+        return 0;
+    };
+    auto pass3 = [&]() -> int {
+        int st = iter(i0, i1, i2, r0, r1, r2);
+        if (st) return st;
+        st = iter(i1, i2, i0, r1, r2, r0);
+        if (st) return st;
+        return iter(i2, i0, i1, r2, r0, r1);
+    };
+    for (;;) {  // the first pass after a (re)start is peeled off the steady loop (see flow_pair)
+        int st = pass3();
+        while (st == 0) st = pass3();
+        if (st == 1) break;
+        restart_stages(q);
     }
+    tally();
+    return ret;
 }
 
 constexpr int kFlowChunk = 256;  // initial short tasks a short worker claims per atomic (its lanes take them in turn)
@@ -928,7 +936,7 @@ __global__ __launch_bounds__(64 * kW) void k_replay_flow(Ws w, int* ctl, unsigne
 // 30.5 + p_next 30.6 of 157 wave-ms at 4K). One wave issues at most one instruction per four cycles, so the
 // tail cannot hide in the chain's idle cycles: it needs a second wave. Here wave C carries the chain alone
 // (chain_chunk over LDS records) and wave H, on another SIMD, does everything else one chunk apart: while C
-// steps chunk i, H builds chunk i + 1 into the other LDS slot (FlowPipe's three-stage resolve) and finishes
+// steps chunk i, H builds chunk i + 1 into the other LDS slot (the three-stage resolve of flow_long) and finishes
 // chunk i - 1 (bbox prefix, records); two workgroup barriers per chunk hand the slots over. A chunk that
 // completes the path or blocks on an incomplete light child is finished by H at once (C waits), which then
 // publishes the top or parks exactly as flow_long does. Task control (queue tickets, help rounds, injected
@@ -1035,7 +1043,7 @@ __device__ int flow_pair(const Ws& w, int* ctl, int t, PairShared& sh, int keyfa
     }
     // ---- H: everything but the chain ----
     // the chunk in slot s (cursor qs): its records' metas, light boxes and descriptor; the pending tail of the
-    // chunk before it (slot p); the carried box; the resolve stages (FlowPipe's, in named registers)
+    // chunk before it (slot p); the carried box; the resolve stages (in named registers)
     int s = 0, qs = f_ld(curp), meta_s = 0, n_s = 0;
     bool fin_s = false;
     B4 lbb_s, bb;

@@ -1,0 +1,19 @@
+# End-of-round evidence in one gpurun call (each GPU step under its own time limit, stop at the first
+# failure): the PMC passes (tools/pmc_round.sh, B = 112), then the bench with that PMC summary, the
+# rocprofv3 kernel stats of the same bench, the serial/pipelined kernel traces, config 5's model and
+# smoke(). Outputs under gpurun_out/evidence/.
+set -u
+export TMPDIR=/tmp
+O=gpurun_out/evidence
+mkdir -p $O
+B=112 KS=k_boruvka_min4,k_boruvka_recs\<false\>,k_krt_fused,k_replay_flow,k_pre_sweep,KPathInit,KLift,KFilter,k_blur_fused bash tools/pmc_round.sh > $O/pmc_round.log 2>&1 || { tail -20 $O/pmc_round.log; exit 1; }
+tail -3 $O/pmc_round.log
+cp gpurun_out/pmc/pmc_kernels.json gpurun_out/pmc/fetch_calib.json $O/
+timeout -k 10 600 python bench.py --pmc $O/pmc_kernels.json > $O/bench_default.json 2> $O/bench_default.err || { tail -5 $O/bench_default.err; exit 1; }
+head -c 300 $O/bench_default.json; echo
+rm -rf $O/rocprof
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/rocprof -o run --output-format csv -- python bench.py --cpu-frames 0 --no-h2d > $O/bench_under_rocprof.json 2> $O/bench_under_rocprof.err || exit 1
+timeout -k 10 300 python tools/bench_intraframe.py --model 4 > $O/intraframe_model.json 2>&1 || exit 1
+tail -1 $O/intraframe_model.json | cut -c1-300
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
