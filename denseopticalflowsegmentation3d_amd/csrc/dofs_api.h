@@ -329,6 +329,10 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
         P.snap_cap = cx->snap_cap;
         P.cap.B = 0;  // force a new layout
     }
+    // the graph's arrays stay readable after the batch for dofs_events, and for a caller's edge list or
+    // edge mask, whose graph may be a forest: dofs_final_roots reads the completion merges' KRT children
+    const bool keep_graph = cx->keep_events || allow || d_edges || n_edges > 0;
+    P.keep_graph = keep_graph;  // (fits() asks for a layout that keeps the graph when set)
     if (!P.fits(d) && cx->used[s]) be.event_sync(cx->evDone[s]);  // reallocation: batch id-2 must be done
     if (!P.reserve(d)) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
     // the workspaces no batch has used yet take this shape now: their first batches then allocate
@@ -337,6 +341,7 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
         Pipeline<Backend>& Q = cx->pipe(k);
         if (k == s || cx->used[k] || Q.fits(d)) continue;
         Q.snap_cap = cx->snap_cap;
+        Q.keep_graph = keep_graph;
         if (!Q.reserve(d)) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
     }
     P.set_params(prm, persp, inv, inv_upper);

@@ -48,15 +48,14 @@ struct NodeVal {
 static_assert(sizeof(NodeVal) == 32, "NodeVal must stay 32 bytes (one gather = 2 x dwordx4)");
 
 // Replay output of the merge at one preorder position (Forest::merge's root state right after it):
-// one 32-byte record (two 16-byte accesses) instead of five arrays — a replay step reads its light
-// child's record and writes its own with two memory instructions each.
-struct alignas(16) RepVal {
+// one 24-byte record (three 8-byte words) instead of five arrays — a replay step reads its light
+// child's record and writes its own with three memory instructions each.
+struct alignas(8) RepVal {
     float mx, my;
     int rank, root;
     B4 bb;
-    int pad0, pad1;
 };
-static_assert(sizeof(RepVal) == 32, "RepVal is one 32-byte record");
+static_assert(sizeof(RepVal) == 24, "RepVal is one 24-byte record");
 
 constexpr int kMaxTaps = 64;
 constexpr int kRoundsMax = 40;        // Borůvka round flags per frame

@@ -127,7 +127,7 @@ __device__ inline unsigned long long f_poll64(unsigned long long* p) {
     return __hip_atomic_fetch_or(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// a RepVal handed to another workgroup: three 8-byte write-through stores / loads (the pads are unused)
+// a RepVal handed to another workgroup: three 8-byte write-through stores / loads
 __device__ inline void rv_publish(RepVal* p, float mx, float my, int rank, int root, B4 bb) {
     unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
     f_st64(q, (unsigned long long)__float_as_uint(mx) | ((unsigned long long)__float_as_uint(my) << 32));
@@ -145,7 +145,6 @@ __device__ inline RepVal rv_fetch(const RepVal* p) {
     r.rank = (int)(unsigned)b;
     r.root = (int)(unsigned)(b >> 32);
     __builtin_memcpy(&r.bb, &c, 8);
-    r.pad0 = r.pad1 = 0;
     return r;
 }
 
@@ -593,7 +592,6 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
                 o.rank = rank;
                 o.root = root;
                 o.bb = obb;
-                o.pad0 = o.pad1 = 0;
                 *dst = o;
             }
         }
@@ -791,7 +789,6 @@ __device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch
             o.rank = s.rank;
             o.root = s.root;
             o.bb = s.bb;
-            o.pad0 = o.pad1 = 0;
             w.Rv[lb + q] = o;
         }
         --q;
@@ -1135,7 +1132,6 @@ __device__ int flow_pair(const Ws& w, int* ctl, int t, PairShared& sh, int keyfa
                 o.rank = rank;
                 o.root = root;
                 o.bb = x;
-                o.pad0 = o.pad1 = 0;
                 *dst = o;
             }
         }

@@ -1467,40 +1467,6 @@ __device__ __forceinline__ int wg_cas(int* p, int expect, int v) {
                                          __HIP_MEMORY_SCOPE_WORKGROUP);
     return expect;
 }
-// union-find finds of K independent chains at once (path halving): each round issues every pending
-// chain's load before waiting, so a thread's K finds cost about one find's latency
-template <int K>
-__device__ __forceinline__ void seq_find(int* par, int (&x)[K], const bool (&act)[K]) {
-    bool pend[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) pend[k] = act[k];
-    for (;;) {
-        int p[K], g[K];
-        bool any = false;
-#pragma unroll
-        for (int k = 0; k < K; ++k) p[k] = pend[k] ? wg_ld(par + x[k]) : 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if (pend[k] && p[k] == x[k]) pend[k] = false;
-            any |= pend[k];
-        }
-        if (!any) return;
-#pragma unroll
-        for (int k = 0; k < K; ++k) g[k] = pend[k] ? wg_ld(par + p[k]) : 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if (!pend[k]) continue;
-            if (g[k] == p[k]) {
-                x[k] = p[k];
-                pend[k] = false;
-            } else {
-                wg_st(par + x[k], g[k]);
-                x[k] = g[k];
-            }
-        }
-    }
-}
-
 // Union-find node of the sweep: parent, and at roots the component's max merge rank (-1: a single
 // pixel) and size — one 16-byte record, so the find that reaches a root also reads its label and
 // size (one memory request per hop). Kept in the StepIn region of the workspace, which KPathInit
@@ -1535,9 +1501,11 @@ __device__ __forceinline__ SeqRec rec_ld(const SeqRec* p) {
 }
 __device__ __forceinline__ void rec_set_par(SeqRec* p, int v) { wg_st(&p->par, v); }
 
-// finds of K chains at once with path halving: each round issues every pending chain's load first;
-// on return x[k] is the root and lab[k] / sz[k] its label and size (only the fields a caller needs
-// stay live, to keep the sweep within 128 VGPRs)
+// finds of K chains at once, two hops per round (read-only: the sweep's phase D hooks every root one hop
+// below its component's root, so paths stay short without compression, and the halving stores cost more
+// than the hops they saved — round 5, same box: KRT −1 ms, +1.5 % end to end): each round issues every
+// pending chain's load first; on return x[k] is the root and lab[k] / sz[k] its label and size (only the
+// fields a caller needs stay live, to keep the sweep within 128 VGPRs)
 template <int K>
 __device__ __forceinline__ void rec_find(SeqRec* rec, int (&x)[K], bool (&pend)[K], int (&lab)[K], int (&sz)[K],
                                          int* rounds = nullptr) {
@@ -1573,7 +1541,6 @@ __device__ __forceinline__ void rec_find(SeqRec* rec, int (&x)[K], bool (&pend)[
                     sz[k] = g.sz;
                     pend[k] = false;
                 } else {
-                    rec_set_par(rec + x[k], g.par);
                     x[k] = g.par;
                 }
             }

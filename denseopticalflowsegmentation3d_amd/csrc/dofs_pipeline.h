@@ -95,10 +95,14 @@ struct Pipeline {
 
     bool layout_packed = false;  // the layout treats key_out as dead (batch-wide sort): batches must sort packed
     bool layout_words = false;   // the layout holds the global-kernel KRT's arrays (P, CS, MX, own)
+    // keep_graph (the context's keep_events): phase A's outputs stay readable after phase B (dofs_events
+    // reads EU / EV; tools/krt_race.py the KRT's); else phase B's arrays reuse them (layout)
+    bool keep_graph = false;
+    bool layout_keep = false;
     bool fits(const Dims& d) const {
         const bool packed = Backend::mst_packed(std::max<int64_t>(d.M, 1), d.B, ceil_log2(4 * d.N));
         return base && cap.B >= d.B && cap.N == d.N && cap.W == d.W && (packed || !layout_packed) &&
-               (layout_words || !(use_dnc(d) || Backend::kKrtLabelWords));
+               (layout_words || !(use_dnc(d) || Backend::kKrtLabelWords)) && (layout_keep || !keep_graph);
     }
 
     // Carve every buffer from one allocation (grow-only). Returns false on allocation failure.
@@ -126,6 +130,10 @@ struct Pipeline {
     // batch and the next batch on this workspace starts only after both, so the phase-B arrays live in
     // regions phase A is done with (first fit; a fresh block when nothing fits), and the arrays of the
     // global-kernel KRT (P, CS, MX, own) exist only where that KRT runs (DOFS_KRT_DNC, the emulator).
+    // The arrays live across the stage boundary come first; then, in one run, those that die inside
+    // phase A and (unless the context keeps the graph: keep_events) phase A's own outputs that only
+    // phase A reads — adjacent dead regions merge, so the replay records (B·NL·32 bytes) fit there.
+    // DESIGN.md §3 tables every array and its life.
     size_t layout(const Dims& d, char* p) {
         size_t off = 0;
         auto take = [&](size_t bytes) {
@@ -137,66 +145,48 @@ struct Pipeline {
         const int64_t B = d.B, N = d.N, M = std::max<int64_t>(d.M, 1), NL = d.NL;
         const bool words = use_dnc(d) || Backend::kKrtLabelWords;
         layout_words = words;
-        struct Region {
-            char* p;
-            size_t n;
+        layout_keep = keep_graph;
+        struct Region {  // [o, o + n) of the allocation, free for phase B
+            size_t o, n;
         };
-        std::vector<Region> dead;  // free for phase B: dead once phase A ended
+        std::vector<Region> dead;
         auto take_dead = [&](size_t bytes) {
+            const size_t start = (off + 255) & ~(size_t)255;
             char* r = take(bytes);
-            dead.push_back(Region{r, bytes});
+            if (!dead.empty() && ((dead.back().o + dead.back().n + 255) & ~(size_t)255) == start)
+                dead.back().n = off - dead.back().o;  // adjacent: one region
+            else
+                dead.push_back(Region{start, bytes});
             return r;
         };
         auto take_b = [&](size_t bytes) {  // a phase-B array: first fit in a dead region
             for (Region& g : dead) {
-                if (g.n >= bytes) {
-                    char* r = g.p;
-                    const size_t used = (bytes + 255) & ~(size_t)255;
-                    g.p = g.p ? g.p + used : nullptr;
-                    g.n = g.n > used ? g.n - used : 0;
-                    return r;
+                const size_t a = (g.o + 255) & ~(size_t)255;
+                if (a + bytes <= g.o + g.n) {
+                    g.n = g.o + g.n - (a + bytes);
+                    g.o = a + bytes;
+                    return p ? p + a : nullptr;
                 }
             }
             return take(bytes);
         };
-        w.tmp = (F2*)take_dead(sizeof(F2) * B * N);  // row blur, Borůvka records
-        w.blur = (F2*)take(sizeof(F2) * B * N);
-        // Borůvka labels; the emulator's round-based replay's park lists (the HIP replay is one dataflow
-        // launch: dead after phase A there)
-        w.comp = (int*)(Backend::kReplayFlow ? take_dead(4 * B * N) : take(4 * B * N));
-        w.bw = (unsigned long long*)take(8 * B * N);  // Borůvka minima; the dataflow replay's queue
-        w.bi = (unsigned*)take_dead(4 * B * N);
-        w.uf = (int*)take(4 * B * N);
-        w.lposr = w.uf;  // the MST's union-find is dead once the KRT starts
-        w.mstbits = (int*)take_dead(4 * B * N);
-        w.cnt = (int*)take_dead(4 * B * N);
-        w.off = (int*)(Backend::kReplayFlow ? take_dead(4 * B * N) : take(4 * B * N));  // MST offsets; park lists (rounds)
-        w.key_in = (unsigned long long*)take(8 * B * M);
-        w.hls = w.key_in;  // the KRT's children sizes for KPathInit: the sort input is dead by then
-        w.val_in = (unsigned*)take_dead(4 * B * M);
+        // phase A's outputs that phase B does not read: dead after phase A (keep_events keeps them for
+        // dofs_events and the diagnosis tools)
+        const bool zone = !keep_graph;
+        auto take_a = [&](size_t bytes) { return zone ? take_dead(bytes) : take(bytes); };
         // the sorted weights: per frame (read by dofs_events) unless the whole batch is sorted at once
         // (run_a: the same predicate), when they are in global order and dead after the sort
         const bool packed = Backend::mst_packed(M, (int)B, ceil_log2(4 * N));
         layout_packed = packed;
-        w.key_out = (unsigned long long*)(packed ? take_dead(8 * B * M) : take(8 * B * M));
-        w.val_out = (unsigned*)take_dead(4 * B * M);
-        w.EU = (int*)take(4 * B * M);
-        w.EV = (int*)take(4 * B * M);
-        w.lu = (int*)take(4 * B * M);
-        w.lv = (int*)take(4 * B * M);
-        w.own = words ? (int*)take(4 * B * M) : nullptr;
-        w.hlB = (unsigned char*)take(B * M);
-        w.P = words ? (unsigned long long*)take(8 * B * NL) : nullptr;
-        w.CS = words ? (int*)take(4 * B * NL) : nullptr;
-        w.MX = words ? (int*)take(4 * B * NL) : nullptr;
-        w.SZ = (int*)take(4 * B * NL);
-        w.J = (unsigned long long*)take_dead(8 * B * NL);  // preorder jump words
-        w.lite = (unsigned char*)take(B * NL);
+
+        // ---- live across the stage boundary: read by phase B or by the result accessors
+        w.blur = (F2*)take(sizeof(F2) * B * N);           // KBlur*; dofs_fetch's blurred field
+        w.bw = (unsigned long long*)take(8 * B * N);      // Borůvka minima; the dataflow replay's queue
+        w.SZ = (int*)take(4 * B * NL);                    // KRT node sizes (scoring)
         w.pre = (int*)take(4 * B * NL);
         w.ord = (int*)take(4 * B * NL);
         w.lscan = (int*)take(4 * B * NL);
-        w.In = (StepIn*)take(sizeof(StepIn) * B * NL);
-        w.Rv = (RepVal*)take(sizeof(RepVal) * B * NL);
+        w.In = (StepIn*)take(sizeof(StepIn) * B * NL);    // (the KRT sweep's union-find records before)
         w.ready = (int*)take(4 * B * NL);
         w.leaf_order = (int*)take(4 * B * N);
         w.cur = (int*)take(4 * B * N);
@@ -204,10 +194,45 @@ struct Pipeline {
         w.ptop = (int*)take(4 * B * N);
         w.list_short = (int*)take(4 * B * N);
         w.list_long = (int*)take(4 * B * N);
-        // phase B only (written by KFilter .. KLabel, read by them and by the result accessors)
+        if (!packed) w.key_out = (unsigned long long*)take(8 * B * M);
+        if (!Backend::kReplayFlow) {  // the emulator's round-based replay's park lists
+            w.comp = (int*)take(4 * B * N);
+            w.off = (int*)take(4 * B * N);
+        }
+        w.own = words ? (int*)take(4 * B * M) : nullptr;
+        w.P = words ? (unsigned long long*)take(8 * B * NL) : nullptr;
+        w.CS = words ? (int*)take(4 * B * NL) : nullptr;
+        w.MX = words ? (int*)take(4 * B * NL) : nullptr;
+        // ---- dead inside phase A (one run of adjacent regions)
+        w.tmp = (F2*)take_dead(sizeof(F2) * B * N);  // row blur, Borůvka records
+        if (Backend::kReplayFlow) {
+            w.comp = (int*)take_dead(4 * B * N);  // Borůvka labels
+            w.off = (int*)take_dead(4 * B * N);   // MST offsets
+        }
+        w.bi = (unsigned*)take_dead(4 * B * N);
+        w.mstbits = (int*)take_dead(4 * B * N);
+        w.cnt = (int*)take_dead(4 * B * N);
+        w.val_in = (unsigned*)take_dead(4 * B * M);
+        if (packed) w.key_out = (unsigned long long*)take_dead(8 * B * M);
+        w.val_out = (unsigned*)take_dead(4 * B * M);
+        w.J = (unsigned long long*)take_dead(8 * B * NL);  // preorder jump words
+        // ---- phase A's own outputs, read by phase A only (the same run, when dead after it)
+        w.uf = (int*)take_a(4 * B * N);
+        w.lposr = w.uf;  // the MST's union-find is dead once the KRT starts
+        w.key_in = (unsigned long long*)take_a(8 * B * M);
+        w.hls = w.key_in;  // the KRT's children sizes for KPathInit: the sort input is dead by then
+        w.EU = (int*)take_a(4 * B * M);  // (dofs_events reads them: keep_events keeps them)
+        w.EV = (int*)take_a(4 * B * M);
+        w.lu = (int*)take_a(4 * B * M);
+        w.lv = (int*)take_a(4 * B * M);
+        w.hlB = (unsigned char*)take_a(B * M);
+        w.lite = (unsigned char*)take_a(B * NL);
+        // ---- phase B only: the replay records (written by the replay, read by the scoring and the result
+        // accessors), then the scoring's arrays (KFilter .. KLabel), largest first
+        w.Rv = (RepVal*)take_b(sizeof(RepVal) * B * NL);
         w.seg = (int*)take_b(4 * B * 2 * d.P2);
         w.sbest = (unsigned long long*)take_b(8 * B * N);
-        w.cscore = (double*)take_b(8 * B * M);  // (largest first: the 4-byte arrays fill the rest)
+        w.cscore = (double*)take_b(8 * B * M);
         w.sevent = (int*)take_b(4 * B * N);
         w.sflag = (int*)take_b(4 * B * N);
         w.soff = (int*)take_b(4 * B * N);

@@ -14,7 +14,7 @@ from denseopticalflowsegmentation3d_amd import runtime  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 NB = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 H, W = 1080, 1920
-ctx = runtime.Dofs(0)
+ctx = runtime.Dofs(0, keep_events=True)  # the graph arrays stay readable after the batch
 L = ctx.lib
 L.dofs_debug_ws_ptrs.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.POINTER(C.c_longlong)]
 path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln)

@@ -46,14 +46,14 @@ def grab(ctx):
 
 
 os.environ["DOFS_KRT_DNC"] = "1"
-ctx = runtime.Dofs(0)
+ctx = runtime.Dofs(0, keep_events=True)  # the graph arrays stay readable after the batch
 ctx.segment_batch_device(fl.data_ptr(), B, H, W, persp, inv, up)
 torch.cuda.synchronize()
 a, ca, dims = grab(ctx)
 print("dnc: flowerr", int(ca[0, 58]), flush=True)
 ctx.close()
 os.environ["DOFS_KRT_DNC"] = "0"
-ctx = runtime.Dofs(0)
+ctx = runtime.Dofs(0, keep_events=True)  # the graph arrays stay readable after the batch
 ctx.segment_batch_device(fl.data_ptr(), B, H, W, persp, inv, up)
 torch.cuda.synchronize()
 b, cb, _ = grab(ctx)
