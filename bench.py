@@ -58,7 +58,7 @@ ROUND_FLAG = 16        # counters: C_ACT + r = Borůvka round r found a cross-co
 #   k_pre_sweep — per merge its jump word 8, children's sizes 8, KRT children 8 and light side 1 in, its
 #     position 4 out = 29 B (the tops' pushed positions, one per block top, are not counted).
 BYTES = {"k_boruvka_min4": (12, 16), "k_boruvka_pick4": 16, "k_boruvka_min": (24, 16), "k_krt_fused": 47,
-         "k_replay_flow": (16, 24, 24), "KPathInit": (38, 8, 24), "k_pre_sweep": 29}
+         "k_replay_flow": (16, 32, 24), "KPathInit": (38, 8, 24), "k_pre_sweep": 29}
 PROBES = ("k_boruvka_min4", "k_boruvka_pick4", "k_krt_fused", "k_replay_flow", "k_pre_sweep", "KPathInit")
 C_PATHS = 0            # counters: heavy paths
 C_KEEP = 54            # counters: merges whose replay record the lean replay stores
@@ -426,7 +426,7 @@ def main(argv=None):
                  "k_boruvka_pick4": "16 per record read",
                  "k_boruvka_min": "24 (pass 0) / 16 (pass 1) per pixel of a processed tile",
                  "k_krt_fused": f"{BYTES['k_krt_fused']} per merge",
-                 "k_replay_flow": "16 per merge (StepIn in) + 24 per stored record (size >= min_size) + 24 per "
+                 "k_replay_flow": "16 per merge (StepIn in) + 32 per stored record (size >= min_size) + 24 per "
                                   "path top published",
                  "KPathInit": "38 per merge + 8 per pixel light child + 24 per path top",
                  "k_pre_sweep": f"{BYTES['k_pre_sweep']} per merge"}

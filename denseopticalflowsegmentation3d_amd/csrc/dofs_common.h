@@ -48,14 +48,19 @@ struct NodeVal {
 static_assert(sizeof(NodeVal) == 32, "NodeVal must stay 32 bytes (one gather = 2 x dwordx4)");
 
 // Replay output of the merge at one preorder position (Forest::merge's root state right after it):
-// one 24-byte record (three 8-byte words) instead of five arrays — a replay step reads its light
-// child's record and writes its own with three memory instructions each.
-struct alignas(8) RepVal {
+// one 32-byte record instead of five arrays. 32 bytes, aligned: a record is one whole 32-byte sector and
+// never shares one with another record. The replay hands records between waves with write-through
+// stores and L2-served loads while other waves' plain stores fill the records around them; a 24-byte
+// form (round 5) let a plain store's sector fill carry a neighbour's old bytes into an XCD's L2, where a
+// later load of the published neighbour found them (an intermittent wrong root: one illegal address and
+// one wrong snapshot count in about fifty GPU runs, none in the 32-byte form).
+struct alignas(16) RepVal {
     float mx, my;
     int rank, root;
     B4 bb;
+    int pad0, pad1;
 };
-static_assert(sizeof(RepVal) == 24, "RepVal is one 24-byte record");
+static_assert(sizeof(RepVal) == 32, "RepVal is one 32-byte record");
 
 constexpr int kMaxTaps = 64;
 constexpr int kRoundsMax = 40;        // Borůvka round flags per frame

@@ -127,7 +127,7 @@ __device__ inline unsigned long long f_poll64(unsigned long long* p) {
     return __hip_atomic_fetch_or(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// a RepVal handed to another workgroup: three 8-byte write-through stores / loads
+// a RepVal handed to another workgroup: three 8-byte write-through stores / loads (the pads are unused)
 __device__ inline void rv_publish(RepVal* p, float mx, float my, int rank, int root, B4 bb) {
     unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
     f_st64(q, (unsigned long long)__float_as_uint(mx) | ((unsigned long long)__float_as_uint(my) << 32));
@@ -145,6 +145,7 @@ __device__ inline RepVal rv_fetch(const RepVal* p) {
     r.rank = (int)(unsigned)b;
     r.root = (int)(unsigned)(b >> 32);
     __builtin_memcpy(&r.bb, &c, 8);
+    r.pad0 = r.pad1 = 0;
     return r;
 }
 
@@ -592,6 +593,7 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
                 o.rank = rank;
                 o.root = root;
                 o.bb = obb;
+                o.pad0 = o.pad1 = 0;
                 *dst = o;
             }
         }
@@ -601,7 +603,6 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             f_drain();
             int old = 0;
             if (lane == 0) {
-                f_st(curp, -1);
                 old = __hip_atomic_exchange(w.ready + lb + top, kFlowDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (t & kFlowLong) atomicAdd(ctl + FC_LDONE, 1);
                 fs_add(ctl, FS_LDONE, 1);
@@ -767,7 +768,6 @@ __device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch
         step_merge(s, in.fs, wbx, wby, in.r, in.meta, lrank, lroot, lbb);
         if (in.meta & kStepTop) {  // path complete: publish its top, then continue its waiter
             rv_publish(w.Rv + lb + q, s.mx, s.my, s.rank, s.root, s.bb);
-            f_st(curp, -1);
             f_drain();
             const int old = __hip_atomic_exchange(w.ready + lb + q, kFlowDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             t = -1;
@@ -789,6 +789,7 @@ __device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch
             o.rank = s.rank;
             o.root = s.root;
             o.bb = s.bb;
+            o.pad0 = o.pad1 = 0;
             w.Rv[lb + q] = o;
         }
         --q;
@@ -1132,6 +1133,7 @@ __device__ int flow_pair(const Ws& w, int* ctl, int t, PairShared& sh, int keyfa
                 o.rank = rank;
                 o.root = root;
                 o.bb = x;
+                o.pad0 = o.pad1 = 0;
                 *dst = o;
             }
         }
@@ -1186,7 +1188,6 @@ __device__ int flow_pair(const Ws& w, int* ctl, int t, PairShared& sh, int keyfa
                 f_drain();
                 int old = 0;
                 if (lane == 0) {
-                    f_st(curp, -1);
                     old = __hip_atomic_exchange(w.ready + lb + top, kFlowDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (t & kFlowLong) atomicAdd(ctl + FC_LDONE, 1);
                     fs_add(ctl, FS_LDONE, 1);

@@ -1403,6 +1403,7 @@ struct KReplay {
             o.rank = s.rank;
             o.root = s.root;
             o.bb = s.bb;
+            o.pad0 = o.pad1 = 0;
             w.Rv[lb + q] = o;
             if (in.meta & kStepTop) {
                 w.ready[lb + q] = phase;

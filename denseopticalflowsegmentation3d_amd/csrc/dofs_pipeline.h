@@ -187,6 +187,7 @@ struct Pipeline {
         w.ord = (int*)take(4 * B * NL);
         w.lscan = (int*)take(4 * B * NL);
         w.In = (StepIn*)take(sizeof(StepIn) * B * NL);    // (the KRT sweep's union-find records before)
+        const Region in_region{(size_t)(off - sizeof(StepIn) * B * NL), sizeof(StepIn) * (size_t)B * (size_t)NL};
         w.ready = (int*)take(4 * B * NL);
         w.leaf_order = (int*)take(4 * B * N);
         w.cur = (int*)take(4 * B * N);
@@ -228,8 +229,10 @@ struct Pipeline {
         w.hlB = (unsigned char*)take_a(B * M);
         w.lite = (unsigned char*)take_a(B * NL);
         // ---- phase B only: the replay records (written by the replay, read by the scoring and the result
-        // accessors), then the scoring's arrays (KFilter .. KLabel), largest first
+        // accessors), then the scoring's arrays (KFilter .. KLabel), largest first — those also in the replay
+        // inputs (StepIn), dead once the replay ends (kept with the graph: tools/flow_dump.py reads them)
         w.Rv = (RepVal*)take_b(sizeof(RepVal) * B * NL);
+        if (zone) dead.insert(dead.begin(), in_region);
         w.seg = (int*)take_b(4 * B * 2 * d.P2);
         w.sbest = (unsigned long long*)take_b(8 * B * N);
         w.cscore = (double*)take_b(8 * B * M);
@@ -475,10 +478,18 @@ struct Pipeline {
     void run_b() {
         if (w.d.M <= 0) return;
         preorder();
+#ifdef DOFS_POISON_RV
+        // check build: every replay record starts as zeros (in-range indices), so a read of a record the replay did not write
+        // in this batch shows (results or an index fault) instead of reading an earlier batch's value
+        be.memset(w.Rv, 0, sizeof(RepVal) * (size_t)w.d.B * (size_t)w.d.NL);
+#endif
         be.mark(5);
         // K5 bottom-up replay of Forest::merge along heavy paths: one dataflow launch (HIP), else rounds
         if constexpr (Backend::kReplayFlow) {
-            if (!(skip_mask & 3)) be.replay_flow(w);
+            if (!(skip_mask & 3))
+                be.replay_flow(w);
+            else  // (measurement: the scoring then reads zeros, in-range indices, not whatever shares the memory)
+                be.memset(w.Rv, 0, sizeof(RepVal) * (size_t)w.d.B * (size_t)w.d.NL);
         } else {
             replay_rounds();
         }

@@ -56,7 +56,9 @@ for b in range(NB):
     shown = 0
     for f in range(Bd):
         npaths = int(c[f, 0])
-        inc = np.flatnonzero(cur[f, :npaths] >= 0)
+        ready = d2h(ready_p, 4 * f * NL, 4 * NL, np.int32)
+        # a path is complete once its top's state word says so (a completed path leaves its cursor as it was)
+        inc = np.flatnonzero(ready[ptop[f, :npaths]] != 0x7FFFFFF0)  # kFlowDone (dofs_dataflow.h)
         if len(inc) == 0:
             continue
         print(f"frame {f}: {len(inc)} incomplete paths of {npaths}; long {int(c[f, 7])} rootl {int(c[f, 59])}")

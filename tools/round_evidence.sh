@@ -17,3 +17,8 @@ timeout -k 10 300 python tools/bench_intraframe.py --model 4 > $O/intraframe_mod
 tail -1 $O/intraframe_model.json | cut -c1-300
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
+# one B = 112 batch per step with the two stages back to back (DOFS_SERIAL=1): every kernel's duration is
+# its own work, not time queued behind the other stage (stage-B kernels in particular)
+rm -rf $O/rocprof_serial
+DOFS_SERIAL=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/rocprof_serial -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --cpu-frames 0 --no-h2d --no-stages > $O/bench_serial.json 2> $O/bench_serial.err || exit 1
+head -c 300 $O/bench_serial.json; echo
