@@ -15,7 +15,7 @@
 // for a long path (>= long_path merges, run by a whole wave as in k_replay_long1: 64 steps resolved in
 // parallel per chunk, both mean chains in one instruction stream); short paths run one per lane.
 //
-// State word of a path top (ready[] at top positions): open (kIntMax / kPendLong from KPathInit) → the
+// State word of a path top (state_at(): the top's record's first pad word): open (kIntMax / kPendLong from KPathInit) → the
 // task word of the parent path parked on it (a light child has one parent position, so one waiter) →
 // kFlowDone. The parker publishes its cursor and running state, then CASes its task word in; the
 // completer publishes the top's record, then exchanges kFlowDone in and continues the waiter it got
@@ -261,7 +261,7 @@ __device__ inline int flow_resolve(const Ws& w, int64_t lb, int p, int top, OneR
     int lrank = 0, lroot = in.lb;
     if (in.meta & kStepDyn) {
         const int lq = in.lb;
-        if (p != accept && f_ld(w.ready + lb + lq) != kFlowDone) return meta;  // accept: seen done by a CAS
+        if (p != accept && f_ld(state_at(w, lb + lq)) != kFlowDone) return meta;  // accept: seen done by a CAS
         const RepVal lv = rv_fetch(w.Rv + lb + lq);
         o->h[0].wb = lv.mx * (float)in.la;
         o->h[1].wb = lv.my * (float)in.la;
@@ -301,7 +301,7 @@ __device__ inline StepIn pipe_in(const Ws& w, int64_t lb, int p, int top) {
 }
 __device__ inline int pipe_rdy(const Ws& w, int64_t lb, const StepIn& in, int p, int top) {
     const bool dyn = p >= top && (step_meta(in) & kStepDyn);
-    return f_ld(w.ready + lb + (dyn ? step_lq(in, p) : top));
+    return f_ld(state_at(w, lb + (dyn ? step_lq(in, p) : top)));
 }
 __device__ inline RepVal pipe_rv(const Ws& w, int64_t lb, const StepIn& in, int rdy, int p, int top) {
     const bool need = p >= top && (step_meta(in) & kStepDyn) && rdy == kFlowDone;
@@ -603,7 +603,7 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
             f_drain();
             int old = 0;
             if (lane == 0) {
-                old = __hip_atomic_exchange(w.ready + lb + top, kFlowDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                old = __hip_atomic_exchange(state_at(w, lb + top), kFlowDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (t & kFlowLong) atomicAdd(ctl + FC_LDONE, 1);
                 fs_add(ctl, FS_LDONE, 1);
                 fs_max(ctl, FS_T_LONG, fs_now());
@@ -626,8 +626,8 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
                 f_st(curp, pb);
                 f_drain();
                 const int lq = step_lq(w.In[lb + pb], pb);
-                const int s0 = f_ld(w.ready + lb + lq);
-                if (s0 != kFlowDone) parked = atomicCAS(w.ready + lb + lq, s0, t) == s0;
+                const int s0 = f_ld(state_at(w, lb + lq));
+                if (s0 != kFlowDone) parked = atomicCAS(state_at(w, lb + lq), s0, t) == s0;
             }
             parked = __shfl(parked, 0, 64);
             if (parked) {
@@ -744,13 +744,13 @@ __device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch
         B4 lbb;
         if (in.meta & kStepDyn) {
             const int lq = in.lb;
-            int st = f_ld(w.ready + lb + lq);
+            int st = f_ld(state_at(w, lb + lq));
             if (st != kFlowDone) {  // park on the light child: publish the state below q, the cursor
                 if (w.ord[lb + q + 1] >= d.N) rv_publish(w.Rv + lb + q + 1, s.mx, s.my, s.rank, s.root, s.bb);
                 f_st(curp, q);
                 f_drain();
-                st = f_ld(w.ready + lb + lq);
-                if (st != kFlowDone && atomicCAS(w.ready + lb + lq, st, t) == st) {
+                st = f_ld(state_at(w, lb + lq));
+                if (st != kFlowDone && atomicCAS(state_at(w, lb + lq), st, t) == st) {
                     t = -1;
                     continue;
                 }
@@ -769,7 +769,7 @@ __device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch
         if (in.meta & kStepTop) {  // path complete: publish its top, then continue its waiter
             rv_publish(w.Rv + lb + q, s.mx, s.my, s.rank, s.root, s.bb);
             f_drain();
-            const int old = __hip_atomic_exchange(w.ready + lb + q, kFlowDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int old = __hip_atomic_exchange(state_at(w, lb + q), kFlowDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             t = -1;
             if (old < kFlowDone) {
                 if (old & kFlowLong) {
@@ -1188,7 +1188,7 @@ __device__ int flow_pair(const Ws& w, int* ctl, int t, PairShared& sh, int keyfa
                 f_drain();
                 int old = 0;
                 if (lane == 0) {
-                    old = __hip_atomic_exchange(w.ready + lb + top, kFlowDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    old = __hip_atomic_exchange(state_at(w, lb + top), kFlowDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (t & kFlowLong) atomicAdd(ctl + FC_LDONE, 1);
                     fs_add(ctl, FS_LDONE, 1);
                     fs_max(ctl, FS_T_LONG, fs_now());
@@ -1208,8 +1208,8 @@ __device__ int flow_pair(const Ws& w, int* ctl, int t, PairShared& sh, int keyfa
                     f_st(curp, pb);
                     f_drain();
                     const int lq = step_lq(w.In[lb + pb], pb);
-                    const int s0 = f_ld(w.ready + lb + lq);
-                    if (s0 != kFlowDone) parked = atomicCAS(w.ready + lb + lq, s0, t) == s0;
+                    const int s0 = f_ld(state_at(w, lb + lq));
+                    if (s0 != kFlowDone) parked = atomicCAS(state_at(w, lb + lq), s0, t) == s0;
                 }
                 parked = __shfl(parked, 0, 64);
                 if (parked) {

@@ -3338,14 +3338,14 @@ extern "C" int dofs_flow_workers(dofs_ctx* ctx, int* long_waves, int* short_wave
 }
 
 // Diagnosis only (tools/flow_dump.py): device pointers of the last batch's workspace arrays, after a sync:
-// out = {cur, ptop, list_long, In, ready, ord, lite, ctr, Rv, pre, flow control block, bw, lu, lv, SZ, hls,
-// hlB, lscan}, and the batch's B, N, NL in dims.
+// out = {cur, ptop, list_long, In, the path-top state words (Rv + 24 bytes: stride 32), ord, lite, ctr, Rv, pre,
+// flow control block, bw, lu, lv, SZ, hls, hlB, lscan}, and the batch's B, N, NL in dims.
 extern "C" int dofs_debug_ws_ptrs(dofs_ctx* ctx, unsigned long long* out, long long* dims) {
     if (!ctx || !out || !dims || !ctx->have_batch()) return DOFS_ERR_INVALID_ARG;
     const int slot = ctx->last_slot();
     ctx->drain();
     const dofs::Ws& w = ctx->pipe(slot).w;
-    const void* p[18] = {w.cur, w.ptop, w.list_long, w.In, w.ready, w.ord, w.lite, w.ctr, w.Rv,
+    const void* p[18] = {w.cur, w.ptop, w.list_long, w.In, reinterpret_cast<const char*>(w.Rv) + offsetof(dofs::RepVal, pad0), w.ord, w.lite, w.ctr, w.Rv,
                          w.pre, ctx->be.flow_ctl, w.bw, w.lu, w.lv, w.SZ, w.hls, w.hlB, w.lscan};
     for (int i = 0; i < 18; ++i) out[i] = (unsigned long long)(uintptr_t)p[i];
     dims[0] = w.d.B;

@@ -125,7 +125,6 @@ struct Ws {
     int* lscan;
     StepIn* In;
     RepVal* Rv;  // replay outputs by preorder position
-    int* ready;
     // per pixel (stride N)
     int* leaf_order;
     int* lposr;  // per frame (stride N): preorder position of the leaf of each leaf rank (aliases uf,
@@ -181,6 +180,13 @@ struct Ws {
 
     DOFS_HD int* C(int f) const { return ctr + (int64_t)f * kCounters; }
 };
+
+// The replay state word of the path top at preorder position pos (graph.cpp:184-190's dependency, made
+// explicit): the first pad word of the top's replay record. One 32-byte sector holds both, so a waiting
+// path's state poll and record fetch read one sector and the completer's publish and state exchange write
+// one (a separate state array cost a second random sector per light child: round 5). Only path tops have
+// a state; the other positions' pads are free (their plain 32-byte stores write zeros there).
+DOFS_HD inline int* state_at(const Ws& w, int64_t pos) { return &w.Rv[pos].pad0; }
 
 // ---------------------------------------------------------------------------------------------
 // Implicit 8-neighbour grid graph (graph.cpp:62-93): pixel p emits edge k∈{0:left, 1:up,
@@ -1209,7 +1215,7 @@ struct KLeafOrder {  // one lane per preorder position: leaf ranks rise with the
 
 constexpr int kTinyPath = 8;    // short heavy paths of at most this many merges form round 0's first list
 constexpr int kLongPath = 256;  // default: heavy paths at least this long go to the wave-cooperative replay
-// ready[] at a heavy-path top: the replay phase its path completed in, or one of these pending
+// state_at() at a heavy-path top: the replay phase its path completed in, or one of these pending
 // states (all compare >= any phase, i.e. "not ready")
 constexpr int kPendLong = kIntMax - 1;  // long path, not complete
 constexpr int kParkBase = kIntMax - 2;  // long path stopped in round r: kParkBase - r
@@ -1261,7 +1267,7 @@ struct KPathInit {  // one lane per merge node x = N + k; path ids and lists thr
                 qb = w.lposr[f * d.N + w.lscan[lb + q]];
                 islong = qb - q >= w.long_path;
             }
-            if (top) w.ready[lb + q] = islong ? kPendLong : kIntMax;  // read at path tops only
+            if (top) *state_at(w, lb + q) = islong ? kPendLong : kIntMax;  // read at path tops only
             if (islong) dofs_aadd(w.C(f) + C_LONGM, qb - q);
         }
         // short paths in two lists by length, so round 0's waves hold paths of like length (a wave
@@ -1382,7 +1388,7 @@ struct KReplay {
             B4 lbb;
             if (in.meta & kStepDyn) {
                 const int lq = in.lb;
-                if (w.ready[lb + lq] >= phase) {
+                if (*state_at(w, lb + lq) >= phase) {
                     *curp = q;
                     return true;
                 }
@@ -1406,7 +1412,7 @@ struct KReplay {
             o.pad0 = o.pad1 = 0;
             w.Rv[lb + q] = o;
             if (in.meta & kStepTop) {
-                w.ready[lb + q] = phase;
+                *state_at(w, lb + q) = phase;
                 *curp = -1;
                 return false;
             }

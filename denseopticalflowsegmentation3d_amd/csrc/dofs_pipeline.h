@@ -159,10 +159,12 @@ struct Pipeline {
                 dead.push_back(Region{start, bytes});
             return r;
         };
-        auto take_b = [&](size_t bytes) {  // a phase-B array: first fit in a dead region
+        // a phase-B array: first fit in a dead region, below `limit` (the replay records: memory no kernel of
+        // phase B reads once KPathInit, which writes their state words, starts)
+        auto take_b = [&](size_t bytes, size_t limit = ~(size_t)0) {
             for (Region& g : dead) {
                 const size_t a = (g.o + 255) & ~(size_t)255;
-                if (a + bytes <= g.o + g.n) {
+                if (a + bytes <= g.o + g.n && a + bytes <= limit) {
                     g.n = g.o + g.n - (a + bytes);
                     g.o = a + bytes;
                     return p ? p + a : nullptr;
@@ -188,7 +190,6 @@ struct Pipeline {
         w.lscan = (int*)take(4 * B * NL);
         w.In = (StepIn*)take(sizeof(StepIn) * B * NL);    // (the KRT sweep's union-find records before)
         const Region in_region{(size_t)(off - sizeof(StepIn) * B * NL), sizeof(StepIn) * (size_t)B * (size_t)NL};
-        w.ready = (int*)take(4 * B * NL);
         w.leaf_order = (int*)take(4 * B * N);
         w.cur = (int*)take(4 * B * N);
         w.slast = w.cur;  // the replay's cursors are dead when KSlotInit fills it
@@ -217,21 +218,24 @@ struct Pipeline {
         if (packed) w.key_out = (unsigned long long*)take_dead(8 * B * M);
         w.val_out = (unsigned*)take_dead(4 * B * M);
         w.J = (unsigned long long*)take_dead(8 * B * NL);  // preorder jump words
-        // ---- phase A's own outputs, read by phase A only (the same run, when dead after it)
+        // ---- phase A's own outputs, read by phase A only (the same run, when dead after it): first those the
+        // preorder and KPathInit do not read
+        w.EU = (int*)take_a(4 * B * M);  // (dofs_events reads them: keep_events keeps them)
+        w.EV = (int*)take_a(4 * B * M);
+        const size_t rv_limit = off;
         w.uf = (int*)take_a(4 * B * N);
         w.lposr = w.uf;  // the MST's union-find is dead once the KRT starts
         w.key_in = (unsigned long long*)take_a(8 * B * M);
         w.hls = w.key_in;  // the KRT's children sizes for KPathInit: the sort input is dead by then
-        w.EU = (int*)take_a(4 * B * M);  // (dofs_events reads them: keep_events keeps them)
-        w.EV = (int*)take_a(4 * B * M);
         w.lu = (int*)take_a(4 * B * M);
         w.lv = (int*)take_a(4 * B * M);
         w.hlB = (unsigned char*)take_a(B * M);
         w.lite = (unsigned char*)take_a(B * NL);
-        // ---- phase B only: the replay records (written by the replay, read by the scoring and the result
-        // accessors), then the scoring's arrays (KFilter .. KLabel), largest first — those also in the replay
-        // inputs (StepIn), dead once the replay ends (kept with the graph: tools/flow_dump.py reads them)
-        w.Rv = (RepVal*)take_b(sizeof(RepVal) * B * NL);
+        // ---- phase B only: the replay records and path-top state words (state_at: KPathInit writes the
+        // states, the replay the records; read by the scoring and the result accessors), then the scoring's
+        // arrays (KFilter .. KLabel), largest first — those also in the replay inputs (StepIn), dead once the
+        // replay ends (kept with the graph: tools/flow_dump.py reads them)
+        w.Rv = (RepVal*)take_b(sizeof(RepVal) * B * NL, rv_limit);
         if (zone) dead.insert(dead.begin(), in_region);
         w.seg = (int*)take_b(4 * B * 2 * d.P2);
         w.sbest = (unsigned long long*)take_b(8 * B * N);
@@ -445,10 +449,6 @@ struct Pipeline {
     // K4 heavy-first preorder (pointer jumping) and the replay's per-position inputs. It runs at the start of
     // phase B: phase A bounds the step and phase B has slack (round 4, B = 112, same box: in phase A
     // 1,736-1,746 Mpix/s, in phase B 1,758-1,761)
-    void preorder() {
-        preorder_pos();
-        path_init();
-    }
     void preorder_pos() {
         const Dims& d = w.d;
         const int B = d.B;
@@ -477,12 +477,13 @@ struct Pipeline {
     // frame), so the HIP backend overlaps it with the next batch's phase A on a second stream.
     void run_b() {
         if (w.d.M <= 0) return;
-        preorder();
+        preorder_pos();
 #ifdef DOFS_POISON_RV
         // check build: every replay record starts as zeros (in-range indices), so a read of a record the replay did not write
         // in this batch shows (results or an index fault) instead of reading an earlier batch's value
         be.memset(w.Rv, 0, sizeof(RepVal) * (size_t)w.d.B * (size_t)w.d.NL);
 #endif
+        path_init();
         be.mark(5);
         // K5 bottom-up replay of Forest::merge along heavy paths: one dataflow launch (HIP), else rounds
         if constexpr (Backend::kReplayFlow) {

@@ -56,7 +56,7 @@ for b in range(NB):
     shown = 0
     for f in range(Bd):
         npaths = int(c[f, 0])
-        ready = d2h(ready_p, 4 * f * NL, 4 * NL, np.int32)
+        ready = d2h(ready_p, 32 * f * NL, 32 * NL - 24, np.int32)[::8]  # state words: one per 32-byte record
         # a path is complete once its top's state word says so (a completed path leaves its cursor as it was)
         inc = np.flatnonzero(ready[ptop[f, :npaths]] != 0x7FFFFFF0)  # kFlowDone (dofs_dataflow.h)
         if len(inc) == 0:
@@ -71,7 +71,7 @@ for b in range(NB):
             lb = q + 2 * (hs & ((1 << 26) - 1)) if meta & 4 else int(rec[4:8].view(np.int32)[0])
             line = f"  path {j}: top {top} cursor {q} len {q - top + 1} meta {meta}"
             if meta & 4:
-                st = int(d2h(ready_p, 4 * (f * NL + lb), 4, np.int32)[0])
+                st = int(d2h(ready_p, 32 * (f * NL + lb), 4, np.int32)[0])
                 x = int(d2h(ord_p, 4 * (f * NL + lb), 4, np.int32)[0])
                 lite = int(d2h(lite_p, f * NL + x, 1, np.uint8)[0])
                 jj = tops.get(lb, -1)
