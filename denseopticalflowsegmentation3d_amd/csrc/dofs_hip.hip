@@ -2929,7 +2929,10 @@ struct HipBackend {
     hipStream_t flow_stream = nullptr;
     hipEvent_t flow_ev[2] = {nullptr, nullptr};
     unsigned flow_epoch = 0;
-    static constexpr int flow_grid() { return 2048; }  // short-path workers (waves; 1,024 and 4,096 measured equal)
+    // short-path workers (waves). Round 5, B = 112, same box, two runs each: 512 → 1,749 / 1,750 Mpix/s (replay
+    // 42 ms), 1,024 → 1,822 / 1,819 (29 ms), 2,048 → 1,889 / 1,896 (21 ms), 3,072 → 1,876 / 1,877, 4,096 → 1,876 /
+    // 1,868: the short paths' lanes are the replay's parallelism until about 2,048 waves
+    static constexpr int flow_grid() { return 2048; }
     // long-path workers (waves): DOFS_FLOW_LONG, default 256 (round 5, B = 112, same box, two runs each:
     // 128 → 1,816 / 1,823 Mpix/s, replay stage 36.7 ms; 256 → 1,869 / 1,869, 22.4 ms; 512 → 1,830 / 1,828)
     int flow_long_workers() const { return kn.flow_long > 0 ? kn.flow_long : 256; }

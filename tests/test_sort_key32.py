@@ -88,7 +88,7 @@ def test_key32_keeps_27_mantissa_bits_in_the_window(L):
 
 @pytest.mark.parametrize("m,e", [(19, 5), (21, 3), (16, 8)])
 def test_narrow_keys_monotone_and_capped(L, m, e):
-    """Keys of m + e < 32 bits (DOFS_SORT_K32E: three sort digits at 24 bits) stay monotone and below 2^(m+e),
+    """Keys of m + e < 32 bits (dofs_debug_sort_k32e: three sort digits at 24 bits) stay monotone and below 2^(m+e),
     the sign-bit NaN and weights above the window at the largest one."""
     rng = np.random.default_rng(31 + m)
     M = 9.25

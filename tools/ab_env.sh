@@ -1,6 +1,6 @@
 # Same-box comparison of (library, environment) variants, alternating bench runs so box-to-box variance
 # cancels. VARIANTS="name=libdir[,VAR=value...] ..." (libdir under exp/), e.g.
-#   VARIANTS="A=A B=B Bp0=B,DOFS_PRIO=0 B128=B,@--batch=128" N=2 bash tools/ab_env.sh  (@: a bench argument)
+#   VARIANTS="A=A B=B B256=B,DOFS_FLOW_LONG=256 B128=B,@--batch=128" N=2 bash tools/ab_env.sh  (@: a bench argument)
 set -u
 N=${N:-2}
 mkdir -p gpurun_out

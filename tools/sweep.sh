@@ -4,9 +4,9 @@
 # value, the median step and the stage times of each run. Replaces the round-1 one-off sweep scripts.
 #   VAR=DOFS_LONG_PATH VALUES="256 128 512" bash tools/sweep.sh
 #   VAR=B VALUES="64 96 128" bash tools/sweep.sh          (B: frames per batch, passed as --batch)
-#   VAR=DOFS_PRIO VALUES="0 2" BENCH_ARGS="--steps 6 --warmup 2" REPS=2 PARITY=1 bash tools/sweep.sh
-# Knobs read by the library: DOFS_LONG_PATH, DOFS_LONG_GRID, DOFS_LONG_WAVES, DOFS_LONG_WAIT,
-# DOFS_PRIO, DOFS_FUSED_EXTRA, DOFS_GRID_CAP, DOFS_KRT_DNC, DOFS_BORUVKA_REC, DOFS_SKIPMASK.
+#   VAR=DOFS_FLOW_LONG VALUES="128 512" BENCH_ARGS="--steps 6 --warmup 2" REPS=2 PARITY=1 bash tools/sweep.sh
+# Knobs read by the library: dofs_knobs.h (DESIGN.md §5 "Runtime knobs"); any other DOFS_* name makes
+# dofs_create fail.
 set -u
 : "${VAR:?VAR=knob name}" "${VALUES:?VALUES=space-separated values}"
 REPS=${REPS:-1}
