@@ -1678,11 +1678,18 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
         KT(0);
         // ---- B (after a barrier: the previous block's key clears precede the inserts; LDS only)
         lds_barrier();
+        // A run of lanes holding the same root (consecutive merges of one component: late in a frame most
+        // endpoints are the frame's largest component) inserts it once, by its first lane, and the others
+        // find the slot with plain reads afterwards: CASes on one LDS word serialise, reads broadcast
+        const int lane = __lane_id();
         int sl[K2];
+        bool lead[K2];
 #pragma unroll
         for (int k = 0; k < K2; ++k) {
+            const int cp = __shfl_up(act2[k] ? c[k] : -1, 1, 64);
+            lead[k] = act2[k] && !(lane > 0 && cp == c[k]);
             sl[k] = 0;
-            if (!act2[k]) continue;
+            if (!lead[k]) continue;
             int h = (int)(uf_prio(c[k]) % (unsigned)kSeqHT);
             for (;;) {
                 int old = -1;
@@ -1698,6 +1705,15 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
             }
             sl[k] = h;
         }
+        // (the leaders' CASes have returned: their keys are in LDS, and a probe from the key's hash meets no
+        // empty slot before it — keys are only set during this phase)
+#pragma unroll
+        for (int k = 0; k < K2; ++k) {
+            if (!act2[k] || lead[k]) continue;
+            int h = (int)(uf_prio(c[k]) % (unsigned)kSeqHT);
+            while (lds_ld(key + h) != c[k]) h = h + 1 == kSeqHT ? 0 : h + 1;
+            sl[k] = h;
+        }
         __syncthreads();
         KT(1);
         // ---- C, L half (the merges t < kDeepS): unions, then per LDS root the max L rank
@@ -1705,14 +1721,16 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
         for (int k = 0; k < K; ++k)
             if (act2[2 * k] && tid + k * kSeqT < kDeepS) swp_union(pm, hsz, sl[2 * k], sl[2 * k + 1]);
         __syncthreads();
+        // per LDS root the max rank: within a run of lanes of one root only the last (highest rank) lane's
+        // atomic can raise it
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int t = tid + k * kSeqT;
-            if (act2[2 * k] && t < kDeepS) {
-                const int r = swp_find(pm, sl[2 * k]);
-                atomicMax(pm + r, r | ((t + 1) << 16));
-                if (t == kDeepS - 1) sh.rlast = r;
-            }
+            const bool a = act2[2 * k] && t < kDeepS;  // (t < kDeepS is uniform over a wave)
+            const int r = a ? swp_find(pm, sl[2 * k]) : -1;
+            const int rn = __shfl_down(r, 1, 64);
+            if (a && !(lane < 63 && rn == r)) atomicMax(pm + r, r | ((t + 1) << 16));
+            if (a && t == kDeepS - 1) sh.rlast = r;
         }
         if (tid == 0) sh.zlast = 0;
         __syncthreads();
@@ -1761,10 +1779,10 @@ __device__ void krt_sweep(const Ws& w, int f, SweepShared& sh, int* progress) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int t = tid + k * kSeqT;
-            if (act2[2 * k] && t >= kDeepS) {
-                const int r = swp_find(pm, sl[2 * k]);
-                atomicMax(pm + r, r | ((t + 1) << 16));
-            }
+            const bool a = act2[2 * k] && t >= kDeepS;
+            const int r = a ? swp_find(pm, sl[2 * k]) : -1;
+            const int rn = __shfl_down(r, 1, 64);
+            if (a && !(lane < 63 && rn == r)) atomicMax(pm + r, r | ((t + 1) << 16));
         }
         for (int x = tid; x < kSeqHT; x += kSeqT) {
             if (key[x] < 0) continue;

@@ -1,2 +1,2 @@
 cd $GRAFT_REPO_ROOT
-VARIANTS="E=E G4=G4096 G3=G3072" N=2 bash tools/ab_env.sh
+VARIANTS="E=E L1=L1 L2=L2" N=2 bash tools/ab_env.sh
