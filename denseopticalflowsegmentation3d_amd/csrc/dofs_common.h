@@ -50,10 +50,9 @@ static_assert(sizeof(NodeVal) == 32, "NodeVal must stay 32 bytes (one gather = 2
 // Replay output of the merge at one preorder position (Forest::merge's root state right after it):
 // one 32-byte record instead of five arrays. 32 bytes, aligned: a record is one whole 32-byte sector and
 // never shares one with another record. The replay hands records between waves with write-through
-// stores and L2-served loads while other waves' plain stores fill the records around them; a 24-byte
-// form (round 5) let a plain store's sector fill carry a neighbour's old bytes into an XCD's L2, where a
-// later load of the published neighbour found them (an intermittent wrong root: one illegal address and
-// one wrong snapshot count in about fifty GPU runs, none in the 32-byte form).
+// stores and L2-served loads; a 24-byte form (round 5) failed intermittently (one illegal address and one
+// wrong snapshot count in about fifty GPU runs, none in the 32-byte form) — likely a load of one record
+// bringing a neighbour's not-yet-published bytes of a shared sector into the reader's L2.
 struct alignas(16) RepVal {
     float mx, my;
     int rank, root;
