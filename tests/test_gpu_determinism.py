@@ -15,9 +15,11 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_repeated_batches_give_identical_records():
-    # its own process: the tool's context and workspaces are fresh, as bench.py's are
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "stress_determinism.py"), "8"],
+@pytest.mark.parametrize("keep", ["1", "0"])
+def test_repeated_batches_give_identical_records(keep):
+    # its own process: the tool's context and workspaces are fresh, as bench.py's are. keep "0": a default
+    # context, whose stage B reuses stage A's dead arrays and the replay inputs
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "stress_determinism.py"), "8", "-", keep],
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "differed 0 of 7" in r.stdout

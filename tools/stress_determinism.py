@@ -3,7 +3,8 @@ tests/test_gpu_bench_config.py (180x320, three simulated ranks, chunks of 8 and 
 frames.Pipelined over one keep_events context), repeated; between repetitions a larger batch re-lays out the
 workspaces (as the GPU suite's earlier tests do). Every repetition's gathered records must equal the first's
 byte for byte. Prints one line per repetition and the number that differed.
-usage: python tools/stress_determinism.py [reps] [lib]"""
+usage: python tools/stress_determinism.py [reps] [lib] [keep]   (keep 0: a default context, whose stage B reuses
+stage A's dead arrays; 1, the default: keep_events, whose layout keeps the graph)"""
 import os
 import sys
 
@@ -16,9 +17,10 @@ from denseopticalflowsegmentation3d_amd.abi import default_params  # noqa: E402
 from denseopticalflowsegmentation3d_amd.frames import FrameParallel, Pipelined, decode_records, job_plan  # noqa: E402
 
 REPS = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-LIB = sys.argv[2] if len(sys.argv) > 2 else None
+LIB = sys.argv[2] if len(sys.argv) > 2 and sys.argv[2] not in ("", "-") else None
+KEEP = (sys.argv[3] != "0") if len(sys.argv) > 3 else True
 H, W, F, WORLD, BATCH, PER = 180, 320, 40, 3, 8, 64
-ctx = runtime.Dofs(0, lib=LIB, keep_events=True)
+ctx = runtime.Dofs(0, lib=LIB, keep_events=KEEP)
 persp, inv, up = runtime.calib()
 prm = default_params()
 prm.min_size = 300
