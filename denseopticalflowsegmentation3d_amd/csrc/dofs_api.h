@@ -377,6 +377,9 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     // completion merges join, and a heavy child below min_size would not have one
     const bool lean = !cx->keep_events && mreal >= d.M;
     P.w.rv_lean = lean ? 1 : 0;
+#ifdef DOFS_MEASURE
+    if (be.kn.b_delay_us > 0) be.delay_us(be.kn.b_delay_us);  // (measurement: where stage B sits in the step)
+#endif
     if (!cx->skip_b) P.run_b();
     be.record(cx->evDone[s], sb);
     be.wait(caller, own_in ? cx->evA[s] : cx->evRead[s]);

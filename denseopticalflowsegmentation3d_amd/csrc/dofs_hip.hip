@@ -146,6 +146,13 @@ namespace dofs {
 
 constexpr int kBlock = 256;
 
+#ifdef DOFS_MEASURE
+// measurement build: one wave that waits `us` microseconds (s_memrealtime: 100 MHz), holding nothing else
+__global__ void k_delay(int us) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * (unsigned long long)us) __builtin_amdgcn_s_sleep(127);
+}
+#endif
 template <class F>
 __global__ __launch_bounds__(kBlock) void k_generic(F f, int64_t n) {
     const int fr = blockIdx.y;
@@ -2534,6 +2541,9 @@ struct HipBackend {
         if (p) note(hipFree(p), "hipFree");
     }
     void memset(void* p, int v, size_t bytes) { note(hipMemsetAsync(p, v, bytes, stream), "hipMemsetAsync"); }
+#ifdef DOFS_MEASURE
+    void delay_us(int us) { hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, stream, us); }
+#endif
     void h2d(void* d, const void* h, size_t bytes) {
         note(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream), "hipMemcpyAsync H2D");
         sync();

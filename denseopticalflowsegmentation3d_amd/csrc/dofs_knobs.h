@@ -21,6 +21,9 @@ struct Knobs {
     int pre_jump = 8;    // DOFS_PRE_JUMP: batches of at most this many frames take the chip-wide preorder
     int skip_b = 0;      // DOFS_SKIP_B (measurement builds only, -DDOFS_MEASURE): the graph stage alone
     int skip_mask = 0;   // DOFS_SKIPMASK (measurement builds only): 1 short replay, 2 long replay, 4 lift
+#ifdef DOFS_MEASURE
+    int b_delay_us = 0;  // DOFS_B_DELAY (measurement builds only): stage B of each batch starts this much later
+#endif
 };
 
 inline Knobs& knobs() {
@@ -66,6 +69,8 @@ inline bool knobs_load(std::string* err) {
             ok = knob_int(v, 0, 1, &k.skip_b);
         else if (name == "DOFS_SKIPMASK")
             ok = knob_int(v, 0, 7, &k.skip_mask);
+        else if (name == "DOFS_B_DELAY")
+            ok = knob_int(v, 0, 200000, &k.b_delay_us);
 #endif
         else {
             if (err) *err = name + " is not a knob of this library (DESIGN.md §5 lists them)";
