@@ -22,6 +22,7 @@ def emu_lib():
     ("DOFS_FUSED", "0", "not a knob"),
     ("DOFS_KEYFAST", "0", "not a knob"),          # a test entry now (dofs_debug_replay_keyfast)
     ("DOFS_SKIP_B", "1", "not a knob"),           # measurement builds only (-DDOFS_MEASURE)
+    ("DOFS_B_DELAY", "1000", "not a knob"),       # measurement builds only
     ("DOFS_FLOW_LONG", "abc", "not a valid value"),
     ("DOFS_FLOW_LONG", "2", "not a valid value"),
     ("DOFS_FLOW_LONG", "100000", "not a valid value"),
@@ -58,4 +59,4 @@ def test_only_the_listed_knobs_are_read():
     names = set(re.findall(r'name == "(DOFS_[A-Z_0-9]+)"', open(os.path.join(
         ROOT, "denseopticalflowsegmentation3d_amd", "csrc", "dofs_knobs.h")).read()))
     assert names == {"DOFS_SERIAL", "DOFS_FLOW_LONG", "DOFS_LONG_PATH", "DOFS_KRT_DNC", "DOFS_PRE_JUMP",
-                     "DOFS_LIB", "DOFS_SKIP_B", "DOFS_SKIPMASK"}
+                     "DOFS_LIB", "DOFS_SKIP_B", "DOFS_SKIPMASK", "DOFS_B_DELAY"}
