@@ -1348,7 +1348,7 @@ DOFS_HD inline void path_start(const Ws& w, int f, int64_t qb, float* mx, float*
 }
 
 // Replay kernels run in phases: round r's short-path pass is phase 2r, its long-path pass 2r+1
-// (a path top's ready[] = the phase it completed in). A pass sees completions of earlier phases.
+// (a path top's state word, state_at(), = the phase it completed in). A pass sees completions of earlier phases.
 // Advances heavy paths bottom-up until they complete or block on a light child whose path has not
 // completed yet. A parked path is appended to `out` (the next round's list; one block-aggregated
 // counter atomic per block), so later rounds only visit the paths still pending. out == nullptr:
