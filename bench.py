@@ -350,7 +350,7 @@ def main(argv=None):
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     # every timed batch's records were copied through FrameParallel.collect, which fails on a batch whose
-    # replay gave up (dofs_batch_records_copy: DOFS_ERR_DEVICE); this counts the batches it checked
+    # results are invalid (dofs_batch_records_copy: DOFS_ERR_INVALID_RESULT); this counts the batches it checked
     checked = fp.checked - checked0
     if checked != a.steps * len(chunks):
         raise RuntimeError(f"{checked} of {a.steps * len(chunks)} timed batches were checked")

@@ -172,8 +172,13 @@ struct KSynth {
 
 // ---- context -----------------------------------------------------------------------------------
 
-// the error of every result accessor on a batch whose dataflow replay gave up a bounded wait (C_FLOWERR)
-constexpr const char* kFlowErrMsg = "the replay of this batch gave up a bounded wait: its results are invalid";
+// the message of DOFS_ERR_INVALID_RESULT, which every result accessor returns for a batch whose C_FLOWERR is set
+inline std::string result_err_msg(int bits) {
+    std::string m = "the results of this batch are invalid:";
+    if (bits & kErrGiveUp) m += " its replay gave up a bounded wait;";
+    if (bits & kErrRecord) m += " a replay record held a union-find root outside its frame (refused on the device);";
+    return m;
+}
 
 template <class Backend>
 struct Context {
@@ -220,8 +225,8 @@ struct Context {
     // the results read — path tops, parked states, merges of >= min_size pixels; Ws::rv_lean)
     bool keep_events = false;
 
-    explicit Context(int device) : be(device), p0(be), p1(be), p2(be), pband(be) {
-        const Knobs& kn = be.kn;  // the knobs dofs_create validated (dofs_knobs.h), kept by the backend
+    Context(int device, const Knobs& knobs) : be(device, knobs), p0(be), p1(be), p2(be), pband(be) {
+        const Knobs& kn = be.kn;  // the knobs dofs_create read for this context (dofs_knobs.h), kept by the backend
         serial = kn.serial != 0;
         skip_b = kn.skip_b != 0;
         p0.skip_mask = p1.skip_mask = p2.skip_mask = kn.skip_mask;
@@ -290,13 +295,18 @@ struct Context {
     }
 };
 
-// Waits for batch id `batch` and returns whether its dataflow replay gave up a bounded wait (C_FLOWERR of frame
-// 0): every accessor of the batch's results then fails with kFlowErrMsg instead of returning invalid data
+// Waits for batch id `batch` and returns its result error bits (C_FLOWERR of frame 0: the replay gave up a
+// bounded wait, or a record held an out-of-range root): every accessor of the batch's results then fails with
+// DOFS_ERR_INVALID_RESULT instead of returning invalid data
 template <class Backend>
-bool flow_failed(Context<Backend>* cx, int64_t batch) {
+int result_err(Context<Backend>* cx, int64_t batch) {
     const int slot = cx->slot_of(batch);
     cx->be.event_sync(cx->evDone[slot]);
-    return cx->be.read_int(cx->pipe(slot).w.ctr + C_FLOWERR) != 0;
+    return cx->be.read_int(cx->pipe(slot).w.ctr + C_FLOWERR);
+}
+template <class Backend>
+int fail_result(Context<Backend>* cx, int bits) {
+    return cx->fail(DOFS_ERR_INVALID_RESULT, result_err_msg(bits));
 }
 
 // Enqueue one batch on the context's streams, ordered after the work already on the caller's
@@ -310,9 +320,8 @@ int api_run(Context<Backend>* cx, const F2* d_flow, int64_t fstride, int B, int 
     if (B <= 0 || H <= 0 || W <= 0 || !persp || !inv || !inv_upper) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
     if (H > 32767 || W > 32767) return cx->fail(DOFS_ERR_INVALID_ARG, "H and W must be < 32768");
     if ((int64_t)H * W >= (1 << 26)) return cx->fail(DOFS_ERR_INVALID_ARG, "H*W must be < 2^26");
-    // the dataflow replay's task words hold frame * H*W + path in 30 bits (dofs_dataflow.h); such a batch
-    // (B >= 518 at 1080p) would not fit a workspace in HBM either
-    if ((int64_t)B * H * W >= ((int64_t)1 << 30)) return cx->fail(DOFS_ERR_INVALID_ARG, "B*H*W must be < 2^30");
+    // the dataflow replay's task words (frame * H*W + path, dofs_dataflow.h) must stay below its state words
+    if ((int64_t)B * H * W > kMaxBatchPixels) return cx->fail(DOFS_ERR_INVALID_ARG, "B*H*W must be <= 2^30 - 16");
     dofs_params prm;
     if (params)
         prm = *params;
@@ -445,9 +454,9 @@ int api_fetch(Context<Backend>* cx, int frame, dofs_result* out, int64_t batch =
     be.d2h(ctr, w.ctr + (int64_t)frame * kCounters, sizeof(ctr));
     be.d2h(ctr0, w.ctr, sizeof(ctr0));
     be.sync();
-    // the dataflow replay gave up a bounded wait: the batch's results are invalid (never seen with the
-    // default KRT; dofs_dataflow.h), reported rather than returned
-    if (ctr0[C_FLOWERR]) return cx->fail(DOFS_ERR_DEVICE, kFlowErrMsg);
+    // the batch's results are invalid (a replay give-up or a refused record; never seen), reported rather than
+    // returned
+    if (ctr0[C_FLOWERR]) return fail_result(cx, ctr0[C_FLOWERR]);
     const int ns = ctr[C_SNAP];
     out->n_snapshots = ns;
     out->stats.n_edges = m.n_edges;
@@ -484,7 +493,7 @@ int api_segment_scores(Context<Backend>* cx, int64_t batch, int frame, double* o
     double* d = (double*)cx->scratch(sizeof(double) * (size_t)N);
     if (!d) return cx->fail(DOFS_ERR_OOM, "device allocation failed");
     Backend& be = cx->be;
-    if (flow_failed(cx, batch)) return cx->fail(DOFS_ERR_DEVICE, kFlowErrMsg);
+    if (int e = result_err(cx, batch)) return fail_result(cx, e);
     cx->join(batch);
     if (P.w.d.M <= 0 || !P.pre)
         be.memset(d, 0, sizeof(double) * (size_t)N);
@@ -508,7 +517,7 @@ int api_final_roots(Context<Backend>* cx, int64_t batch, int frame, int32_t* out
     const Ws& w = P.w;
     const Dims& d = w.d;
     Backend& be = cx->be;
-    if (flow_failed(cx, batch)) return cx->fail(DOFS_ERR_DEVICE, kFlowErrMsg);
+    if (int e = result_err(cx, batch)) return fail_result(cx, e);
     cx->join(batch);
     std::vector<int32_t> rec;
     if (d.M <= 0) {  // one pixel
@@ -520,6 +529,7 @@ int api_final_roots(Context<Backend>* cx, int64_t batch, int frame, int32_t* out
         be.sync();
         be.d2h(&r, w.Rv + (int64_t)frame * d.NL + q, sizeof(RepVal));
         be.sync();
+        if ((unsigned)r.root >= (unsigned)d.N) return fail_result(cx, kErrRecord);
         rec = {r.root, r.bb.x0, r.bb.y0, r.bb.x1, r.bb.y1};
     } else {  // a forest: the components joined by the completion merges
         const int64_t k = d.M - w.mreal + 1;
@@ -529,6 +539,7 @@ int api_final_roots(Context<Backend>* cx, int64_t batch, int frame, int32_t* out
         rec.resize(5 * (size_t)k);
         be.d2h(rec.data(), dv, sizeof(int32_t) * rec.size());
         be.sync();
+        if (int e = be.read_int(w.ctr + C_FLOWERR)) return fail_result(cx, e);  // (KFinalRoots checks every root)
         std::vector<int64_t> idx((size_t)k);
         for (int64_t i = 0; i < k; ++i) idx[(size_t)i] = i;
         std::sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return rec[5 * a] < rec[5 * b]; });
@@ -550,7 +561,7 @@ int api_events(Context<Backend>* cx, int frame, dofs_event* ev, int64_t capacity
     if (frame < 0 || frame >= cx->meta[slot].B) return cx->fail(DOFS_ERR_INVALID_ARG, "no frame");
     if (cx->meta[slot].lean)
         return cx->fail(DOFS_ERR_INVALID_ARG, "the batch kept no event records: dofs_keep_events(ctx, 1) before it");
-    if (flow_failed(cx, cx->nbatch - 1)) return cx->fail(DOFS_ERR_DEVICE, kFlowErrMsg);
+    if (int e = result_err(cx, cx->nbatch - 1)) return fail_result(cx, e);
     cx->join(cx->nbatch - 1);
     const Ws& w = cx->pipe(slot).w;
     const Dims& d = w.d;
@@ -747,7 +758,7 @@ template <class Backend>
 int check_overflow(Context<Backend>* cx, int64_t batch) {
     const int slot = cx->slot_of(batch);
     cx->be.event_sync(cx->evDone[slot]);
-    if (cx->be.read_int(cx->pipe(slot).w.ctr + C_FLOWERR)) return cx->fail(DOFS_ERR_DEVICE, kFlowErrMsg);
+    if (int e = cx->be.read_int(cx->pipe(slot).w.ctr + C_FLOWERR)) return fail_result(cx, e);
     const int ovf = cx->be.read_int(cx->pipe(slot).w.ctr + C_OVF_ANY);
     if (ovf) return cx->fail(DOFS_ERR_CAPACITY, "snapshot records overflowed the per-frame capacity");
     return cx->check();
@@ -760,9 +771,10 @@ int check_overflow(Context<Backend>* cx, int64_t batch) {
 // frame-parallel gather never sees one rank drop out.
 // The copy waits for the batch (one host wait per collect; the pipelined caller collects batch k after
 // submitting k + slots - 1, whose graph stage it then overlaps anyway) and reads the batch's replay flag:
-// a replay that gave up a bounded wait (C_FLOWERR, dofs_dataflow.h) returns DOFS_ERR_DEVICE — after
-// writing the block with every count DOFS_RECORDS_INVALID, so a collective gather that follows still
-// moves equal blocks and every receiver sees which rank's frames are invalid.
+// a batch whose results are invalid (C_FLOWERR: a replay give-up or a refused record) returns
+// DOFS_ERR_INVALID_RESULT — after writing the block with every count DOFS_RECORDS_INVALID, so a collective
+// gather that follows still moves equal blocks and every receiver sees which rank's frames are invalid. Any
+// other failure (a HIP error: DOFS_ERR_DEVICE) leaves the block undefined, and the caller must not send it.
 template <class Backend>
 int api_records_copy(Context<Backend>* cx, int64_t batch, void* dst, int per_frame, void* stream) {
     if (!cx->live(batch) || !dst || per_frame < 0) return cx->fail(DOFS_ERR_INVALID_ARG, "bad args");
@@ -772,18 +784,18 @@ int api_records_copy(Context<Backend>* cx, int64_t batch, void* dst, int per_fra
     if (per_frame > w.snap_cap)
         return cx->fail(DOFS_ERR_CAPACITY, "per_frame exceeds the snapshot capacity (dofs_set_snapshot_capacity)");
     cx->be.event_sync(cx->evDone[slot]);
-    const bool gave_up = cx->be.read_int(w.ctr + C_FLOWERR) != 0;
+    const int invalid = cx->be.read_int(w.ctr + C_FLOWERR);
     cx->be.set_stream(stream);
     cx->join(batch);
     cx->be.copy2d(dst, sizeof(int), w.ctr + C_SNAP, sizeof(int) * kCounters, sizeof(int), B);
     if (per_frame > 0)
         cx->be.copy2d((char*)dst + sizeof(int) * B, sizeof(dofs_box_record) * per_frame, w.recs,
                       sizeof(dofs_box_record) * w.snap_cap, sizeof(dofs_box_record) * per_frame, B);
-    if (gave_up) {
+    if (invalid) {
         static_assert(DOFS_RECORDS_INVALID == -1, "counts are filled with 0xFF bytes");
         cx->be.memset(dst, 0xFF, sizeof(int) * (size_t)B);
         if (int rc = cx->check()) return rc;
-        return cx->fail(DOFS_ERR_DEVICE, kFlowErrMsg);
+        return fail_result(cx, invalid);
     }
     return cx->check();
 }

@@ -7,7 +7,7 @@
 #include "dofs_api.h"
 
 struct dofs_ctx : dofs::Context<DofsBackend> {
-    explicit dofs_ctx(int device) : dofs::Context<DofsBackend>(device) {}
+    dofs_ctx(int device, const dofs::Knobs& kn) : dofs::Context<DofsBackend>(device, kn) {}
     std::shared_ptr<void> flow_engine;  // the optical-flow stage (HIP build; created on first use)
     std::shared_ptr<void> video;        // the clip pipeline's buffers and streams (HIP build)
 };
@@ -61,16 +61,18 @@ int32_t dofs_obj_size(int32_t cls, double out[2]) {
     return DOFS_OK;
 }
 
-// why the last dofs_create returned NULL (dofs_last_error(NULL))
-static std::string g_create_err = "null context";
+// why this thread's last dofs_create returned NULL (dofs_last_error(NULL)); per thread, so concurrent
+// dofs_create calls neither race on it nor invalidate each other's strings
+static thread_local std::string g_create_err = "null context";
 
 dofs_ctx* dofs_create(int32_t device) {
-    if (!dofs::knobs_load(&g_create_err)) return nullptr;  // an unknown DOFS_* knob or an invalid value
+    dofs::Knobs kn;  // the context's own knobs (dofs_knobs.h)
+    if (!dofs::knobs_load(&kn, &g_create_err)) return nullptr;  // an unknown DOFS_* knob or an invalid value
     if (!DofsBackend::device_ok(device)) {
         g_create_err = "no gfx950 device " + std::to_string(device);
         return nullptr;
     }
-    dofs_ctx* c = new dofs_ctx(device);
+    dofs_ctx* c = new dofs_ctx(device, kn);
     if (!c->be.ok()) {
         g_create_err = c->be.error();
         delete c;
@@ -81,6 +83,19 @@ dofs_ctx* dofs_create(int32_t device) {
 }
 
 void dofs_destroy(dofs_ctx* ctx) { delete ctx; }
+
+// Test entry (not in dofs.h): the knobs this context was created with (dofs_knobs.h) — {serial, flow_long,
+// long_path, krt_dnc, pre_jump}; 0 for flow_long / long_path = the backend's default
+int32_t dofs_debug_knobs(dofs_ctx* ctx, int32_t out[5]) {
+    if (!ctx || !out) return DOFS_ERR_INVALID_ARG;
+    const dofs::Knobs& k = ctx->be.kn;
+    out[0] = k.serial;
+    out[1] = k.flow_long;
+    out[2] = k.long_path;
+    out[3] = k.krt_dnc;
+    out[4] = k.pre_jump;
+    return DOFS_OK;
+}
 
 const char* dofs_last_error(dofs_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
 

@@ -82,7 +82,7 @@ enum Counter {
     C_KEEP = 54,     // merges whose replay record the lean replay stores (size >= min_size; KPathInit)
     C_OVF_ANY = 56,  // frame 0 only: 1 if any frame of the batch overflowed its snapshot records
     C_LONGM = 57,    // merges on long heavy paths (replayed by the wave-per-path kernel)
-    C_FLOWERR = 58,  // frame 0 only: the dataflow replay gave up a bounded wait (results invalid)
+    C_FLOWERR = 58,  // frame 0 only: the batch's results are invalid (bits kErrGiveUp, kErrRecord; dofs_kernels.h)
     C_ROOTL = 59,    // 1 + position in list_long of the frame's root heavy path (0: the root path is short)
     C_SORTFIX = 60,  // frame 0 only, 3 counters: pairs the MST sort fix-up moved, its fallback flag, barrier
     C_BMAX = 63      // the frame's largest |blurred flow component| (float bits, atomicMax by the HIP blur)
@@ -92,6 +92,10 @@ static_assert(C_ACT + 28 < C_KEEP, "counter layout");
 
 constexpr uint32_t kNoEdge = 0xFFFFFFFFu;
 constexpr int kIntMax = 0x7FFFFFFF;
+// Pixels of a batch (B * H * W) at most: the dataflow replay's task words hold frame * H*W + path below
+// kFlowLong = 2^30 and stay below its state words (kFlowDone = 2^31 - 16 and the open words above it) with
+// the long bit set (static_assert in dofs_dataflow.h). 1080p: 517 frames (205 GB of input, which fits in HBM).
+constexpr int64_t kMaxBatchPixels = ((int64_t)1 << 30) - 16;
 
 // Linear dimensions of one frame and of the batch.
 struct Dims {

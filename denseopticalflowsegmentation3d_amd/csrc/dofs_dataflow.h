@@ -36,6 +36,9 @@ namespace dofs {
 constexpr int kFlowDone = 0x7FFFFFF0;  // state word of a completed path top (open words are above it)
 constexpr int kFlowLong = 1 << 30;     // task word bit: a long path (run by a whole wave)
 constexpr int kFlowIdMask = kFlowLong - 1;
+// every task word (< kMaxBatchPixels, | kFlowLong for a long path) is below every state word (api_run refuses
+// larger batches)
+static_assert(kMaxBatchPixels <= (long long)kFlowDone - kFlowLong, "task words must stay below kFlowDone");
 
 // control block (ints), zeroed and filled by k_flow_prep each launch; per-frame prefix sums follow. Every
 // word that waves update or poll sits on a 256-byte line of its own: thousands of waves touch them, and
@@ -242,6 +245,18 @@ __global__ void k_flow_prep(Ws w, int* ctl) {
     ctl[FC_QCAP] = (int)(B * w.d.N);
 }
 
+// The waiter a completion's exchange returned from its top's state word: -1 if none was parked there (open
+// words are above kFlowDone), else a task word of this batch — a word outside it (never seen) is a give-up, not
+// a task to index by
+__device__ inline int flow_waiter(const Ws& w, int* ctl, int old) {
+    if (old >= kFlowDone) return -1;
+    if (old < 0 || (long long)(old & kFlowIdMask) >= (long long)w.d.B * w.d.N) {
+        f_st(ctl + FC_ERR, 1);
+        return -1;
+    }
+    return old;
+}
+
 __device__ inline void flow_push(const Ws& w, int* ctl, unsigned epoch, int t) {
     const int s = atomicAdd(ctl + FC_QTAIL, 1);
     if (s >= ctl[FC_QCAP]) {  // (never: a push resumes a path parked on a completed top, < B * N of them)
@@ -293,19 +308,23 @@ __device__ inline int flow_resolve(const Ws& w, int64_t lb, int p, int top, OneR
 // d = 1 the records, and chunk q - 64 is built into LDS from them at the next chunk's start. Each stage's
 // loads have one chunk's steps to arrive; a restart (a task's first chunk, or a re-resolve after a park
 // that found its child done) fills the stages synchronously.
-// Branch-free loads: a lane that needs none reads a line the wave reads anyway (its path top's), so no
-// loaded register is merged with a constant at a branch join (the merge made the compiler wait for the
-// load right after issuing it).
+// Branch-free loads: a lane that needs none still loads (no loaded register is merged with a constant at a
+// branch join — the merge made the compiler wait for the load right after issuing it). Its StepIn load reads
+// its path top's record, a line the wave reads anyway; its state-word and record loads read g_flow_none, a
+// line that is never written, so no wave ever loads a handed-off sector (a path top's state word and record)
+// before it is published — only the lanes whose light child it is load it, the record after its state word
+// read done (round 5 pointed these don't-care loads at the path's own unpublished top).
+__device__ RepVal g_flow_none;  // zero, never written
 __device__ inline StepIn pipe_in(const Ws& w, int64_t lb, int p, int top) {
     return w.In[lb + (p >= top ? p : top)];  // (p < top: meta is ignored, pipe_build checks p)
 }
 __device__ inline int pipe_rdy(const Ws& w, int64_t lb, const StepIn& in, int p, int top) {
     const bool dyn = p >= top && (step_meta(in) & kStepDyn);
-    return f_ld(state_at(w, lb + (dyn ? step_lq(in, p) : top)));
+    return f_ld(dyn ? state_at(w, lb + step_lq(in, p)) : &g_flow_none.pad0);
 }
 __device__ inline RepVal pipe_rv(const Ws& w, int64_t lb, const StepIn& in, int rdy, int p, int top) {
     const bool need = p >= top && (step_meta(in) & kStepDyn) && rdy == kFlowDone;
-    return rv_fetch(w.Rv + lb + (need ? step_lq(in, p) : top));  // read before the state word was seen done: unused
+    return rv_fetch(need ? w.Rv + lb + step_lq(in, p) : &g_flow_none);
 }
 // flow_resolve from the pipeline's loaded values (same record, same meta)
 __device__ inline int pipe_build(const Ws& w, const StepIn& sin, int rdy, const RepVal& lv, int p, int top, OneRec* o,
@@ -610,7 +629,7 @@ __device__ int flow_long(const Ws& w, int* ctl, int t, OneRec (*buf)[64], OneOut
                 if (top == 0) fs_max(ctl, FS_T_ROOT, fs_now());
             }
             old = __shfl(old, 0, 64);
-            ret = old < kFlowDone ? old : -1;
+            ret = flow_waiter(w, ctl, old);
             return 1;
         }
         if (n < 64) {  // blocked at pb on light child lq: park on it unless it completed meanwhile
@@ -769,9 +788,10 @@ __device__ __forceinline__ void flow_short(const Ws& w, int* ctl, unsigned epoch
         if (in.meta & kStepTop) {  // path complete: publish its top, then continue its waiter
             rv_publish(w.Rv + lb + q, s.mx, s.my, s.rank, s.root, s.bb);
             f_drain();
-            const int old = __hip_atomic_exchange(state_at(w, lb + q), kFlowDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int old = flow_waiter(
+                w, ctl, __hip_atomic_exchange(state_at(w, lb + q), kFlowDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             t = -1;
-            if (old < kFlowDone) {
+            if (old >= 0) {
                 if (old & kFlowLong) {
                     flow_push(w, ctl, epoch, old);
                     fs_add(ctl, FS_PUSH, 1);
@@ -1195,7 +1215,7 @@ __device__ int flow_pair(const Ws& w, int* ctl, int t, PairShared& sh, int keyfa
                     if (top == 0) fs_max(ctl, FS_T_ROOT, fs_now());
                 }
                 old = __shfl(old, 0, 64);
-                ret = old < kFlowDone ? old : -1;
+                ret = flow_waiter(w, ctl, old);
                 cmd = kPairEnd;
                 st = 1;
             } else {  // blocked at pb on light child lq: park on it unless it completed meanwhile
@@ -1334,8 +1354,18 @@ constexpr int kFlowLongW = 4;    // waves per long-worker workgroup (one per SIM
 // counter C_FLOWERR of frame 0 = a bounded wait of the launch gave up (dofs_batch_counters); force: a test
 // of the error's path through the accessors (dofs_debug_flow_giveup), the replay itself is complete
 __global__ void k_flow_report(Ws w, const int* ctl, int force) {
-    if (threadIdx.x == 0 && blockIdx.x == 0 && (ctl[FC_ERR] || force)) w.C(0)[C_FLOWERR] = 1;
+    if (threadIdx.x == 0 && blockIdx.x == 0 && (ctl[FC_ERR] || force)) w.C(0)[C_FLOWERR] = kErrGiveUp;
 }
 inline int g_flow_giveup = 0;  // host: dofs_debug_flow_giveup (test only)
+// test only (dofs_debug_bad_root): a root outside the frame written into each frame's last merge record (the
+// KRT root: size H*W, a scoring candidate's record) after the replay, as a stale or torn record would hold one
+__global__ void k_bad_root(Ws w) {
+    if (blockIdx.x != 0 || w.d.M <= 0) return;
+    for (int f = threadIdx.x; f < w.d.B; f += blockDim.x) {
+        const int64_t lb = f * w.d.NL;
+        w.Rv[lb + w.pre[lb + w.d.N + w.d.M - 1]].root = (int)w.d.N + 7;
+    }
+}
+inline int g_bad_root = 0;  // host: dofs_debug_bad_root (test only)
 
 }  // namespace dofs

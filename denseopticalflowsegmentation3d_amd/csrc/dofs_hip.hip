@@ -2470,7 +2470,7 @@ struct HipBackend {
     }
 
     Knobs kn;  // the context's runtime knobs (dofs_knobs.h), read when it was created
-    explicit HipBackend(int dev) : device(dev), kn(knobs()) {
+    HipBackend(int dev, const Knobs& k) : device(dev), kn(k) {
         note(hipSetDevice(dev), "hipSetDevice");
         note(hipStreamCreateWithFlags(&own, hipStreamNonBlocking), "hipStreamCreate");
         stream = own;
@@ -2965,8 +2965,8 @@ struct HipBackend {
     // 128 → 1,816 / 1,823 Mpix/s, replay stage 36.7 ms; 256 → 1,869 / 1,869, 22.4 ms; 512 → 1,830 / 1,828)
     int flow_long_workers() const { return kn.flow_long > 0 ? kn.flow_long : 256; }
     bool replay_flow(const Ws& w) {
-        if ((int64_t)w.d.B * w.d.N >= (int64_t)kFlowLong) {  // (api_run refuses such batches)
-            note(hipErrorInvalidValue, "batch too large for the replay's 30-bit task words");
+        if ((int64_t)w.d.B * w.d.N > kMaxBatchPixels) {  // (api_run refuses such batches)
+            note(hipErrorInvalidValue, "batch too large for the replay's task words");
             return false;
         }
         const size_t n = FC_HDR + 3 * (size_t)(w.d.B + 1);
@@ -3019,6 +3019,7 @@ struct HipBackend {
             note(hipStreamWaitEvent(stream, flow_ev[1], 0), "hipStreamWaitEvent");
         });
         hipLaunchKernelGGL(k_flow_report, dim3(1), dim3(64), 0, stream, w, flow_ctl, g_flow_giveup);
+        if (g_bad_root) hipLaunchKernelGGL(k_bad_root, dim3(1), dim3(64), 0, stream, w);
         if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_replay_flow launch");
         return true;
     }
@@ -3265,6 +3266,14 @@ extern "C" void dofs_debug_sort_fix(int on) { dofs::g_sort_fix = on != 0; }
 extern "C" int dofs_debug_flow_giveup(int on) {
     const int old = dofs::g_flow_giveup;
     if (on >= 0) dofs::g_flow_giveup = on ? 1 : 0;
+    return old;
+}
+// Test knob: the batches issued while on = 1 have an out-of-range union-find root written into every frame's
+// last merge record after the replay (k_bad_root) — the scoring's guards must refuse it (DOFS_ERR_INVALID_RESULT
+// from every accessor) instead of using it as an index. Returns the previous value.
+extern "C" int dofs_debug_bad_root(int on) {
+    const int old = dofs::g_bad_root;
+    if (on >= 0) dofs::g_bad_root = on ? 1 : 0;
     return old;
 }
 // Test knob: constant-key chunks of the long-path replay (dofs_dataflow.h g_keyfast; 1 = on, the default).

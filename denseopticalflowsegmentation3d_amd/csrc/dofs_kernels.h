@@ -188,6 +188,19 @@ struct Ws {
 // a state; the other positions' pads are free (their plain 32-byte stores write zeros there).
 DOFS_HD inline int* state_at(const Ws& w, int64_t pos) { return &w.Rv[pos].pad0; }
 
+// The batch's sticky result error, C_FLOWERR of frame 0 (bits; every result accessor reports it as
+// DOFS_ERR_INVALID_RESULT): kErrGiveUp, the dataflow replay gave up a bounded wait; kErrRecord, a replay
+// record's union-find root used as an index (the scoring's slot arrays) lay outside its frame. A lane that
+// finds such a root skips the access, so a wrong record can cost the batch its results but never an
+// out-of-range atomic or gather.
+constexpr int kErrGiveUp = 1;
+constexpr int kErrRecord = 2;
+DOFS_HD inline bool root_ok(const Ws& w, int root) {
+    if ((unsigned)root < (unsigned)w.d.N) return true;
+    dofs_aor(w.C(0) + C_FLOWERR, kErrRecord);
+    return false;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Implicit 8-neighbour grid graph (graph.cpp:62-93): pixel p emits edge k∈{0:left, 1:up,
 // 2:up-left, 3:down-left}; emission index idx = 4p + k orders edges exactly like the reference's
@@ -1465,7 +1478,8 @@ struct KFilter {  // appends candidates through the backend's list taker (called
         if (valid && i < w.mreal && w.SZ[f * d.NL + d.N + i] >= w.min_size) {
             const NodeVal v = node_val(w, pre, f, d.N + i);
             const int y = v.root / d.W;
-            c = v.size >= w.min_size && y >= d.H / 10 && !(vec_norm(v.mx, v.my) < 3 * (y + 1) / (double)d.H);
+            c = root_ok(w, v.root) && v.size >= w.min_size && y >= d.H / 10 &&
+                !(vec_norm(v.mx, v.my) < 3 * (y + 1) / (double)d.H);
         }
         const int k = t.take(w.C(f) + C_CAND, c);
         if (c) w.cand[f * d.M + k] = (int)i;
@@ -1499,6 +1513,10 @@ struct KLift {
             score = event_score(w, v, &cls, nullptr);
             root = v.root;
             scored = score != -1;
+            if (!root_ok(w, root)) {  // (KFilter admitted it: a record rewritten since is refused, not used)
+                root = 0;
+                scored = false;
+            }
             qual = scored && !(convexity < w.min_convexity[cls]) && score > w.score_threshold;
             w.cscore[f * d.M + j] = qual ? score : -1.0;
         }
@@ -1531,6 +1549,7 @@ struct KSlotEvent {  // first event reaching the slot's maximum wins (strict '<'
         if (!(s > w.score_threshold)) return;
         const int i = w.cand[f * d.M + j];
         const int root = w.Rv[f * d.NL + pre[f * d.NL + d.N + i]].root;
+        if (!root_ok(w, root)) return;
         if (dbits(s) == w.sbest[f * d.N + root]) dofs_amin(w.sevent + f * d.N + root, i);
     }
 };
@@ -1627,6 +1646,7 @@ struct KFinalRoots {
                 o[2] = o[4] = c[t] / d.W;
             } else {
                 const RepVal r = w.Rv[frame * d.NL + pre[frame * d.NL + c[t]]];
+                root_ok(w, r.root);  // (an output, not an index here: reported through the batch's error)
                 o[0] = r.root;
                 o[1] = r.bb.x0;
                 o[2] = r.bb.y0;

@@ -26,11 +26,6 @@ struct Knobs {
 #endif
 };
 
-inline Knobs& knobs() {
-    static Knobs k;
-    return k;
-}
-
 // integer value of v in [lo, hi] (the whole string), else false
 inline bool knob_int(const char* v, int lo, int hi, int* out) {
     if (!v || !*v) return false;
@@ -41,9 +36,11 @@ inline bool knob_int(const char* v, int lo, int hi, int* out) {
     return true;
 }
 
-// Read every DOFS_* variable of the environment into knobs(); false (and *err) on an unknown name or an
-// invalid value. DOFS_LIB (the Python loader's library path) is not the library's and is passed over.
-inline bool knobs_load(std::string* err) {
+// Read every DOFS_* variable of the environment into *out (the new context's own copy: no process-global
+// state, so concurrent dofs_create calls and contexts created under different environments keep their own
+// knobs); false (and *err) on an unknown name or an invalid value. DOFS_LIB (the Python loader's library
+// path) is not the library's and is passed over.
+inline bool knobs_load(Knobs* out, std::string* err) {
     Knobs k;
     for (char** e = environ; e && *e; ++e) {
         const char* s = *e;
@@ -81,7 +78,7 @@ inline bool knobs_load(std::string* err) {
             return false;
         }
     }
-    knobs() = k;
+    *out = k;
     return true;
 }
 

@@ -150,10 +150,11 @@ int32_t dofs_gather_records(dofs_ctx* ctx, dofs_comm* comm, int32_t per_frame, i
         comm->cap = bytes;
     }
     const int rc = dofs_batch_records_copy(ctx, comm->buf, per_frame, stream);
-    // DOFS_ERR_DEVICE: the batch's replay gave up and its block holds DOFS_RECORDS_INVALID counts. The
-    // collective still runs (the other ranks are in it), so every receiver sees the invalid frames; the
-    // error is returned after it. Other errors leave no block to send.
-    if (rc && rc != DOFS_ERR_DEVICE) return fail(comm, rc, std::string("dofs_batch_records_copy: ") + dofs_last_error(ctx));
+    // DOFS_ERR_INVALID_RESULT: the batch's results are invalid and its block holds DOFS_RECORDS_INVALID counts.
+    // The collective still runs (the other ranks are in it), so every receiver sees the invalid frames; the
+    // error is returned after it. Other errors (DOFS_ERR_DEVICE: a HIP call failed) leave no block to send.
+    if (rc && rc != DOFS_ERR_INVALID_RESULT)
+        return fail(comm, rc, std::string("dofs_batch_records_copy: ") + dofs_last_error(ctx));
     const std::string copy_err = rc ? std::string("dofs_batch_records_copy: ") + dofs_last_error(ctx) : std::string();
     if (int g = dofs_gather_bytes(comm, comm->buf, bytes, root, d_recv, stream)) return g;
     return rc ? fail(comm, rc, copy_err) : DOFS_OK;

@@ -14,8 +14,8 @@ import torch.distributed as dist
 from .abi import DofsBoxRecord
 
 RECORD_DTYPE = DofsBoxRecord.np_dtype()
-RECORDS_INVALID = -1  # include/dofs.h DOFS_RECORDS_INVALID: the frame's batch failed (its replay gave up)
-DOFS_ERR_DEVICE = 3
+RECORDS_INVALID = -1  # include/dofs.h DOFS_RECORDS_INVALID: the frame's batch failed (its results are invalid)
+DOFS_ERR_INVALID_RESULT = 6  # include/dofs.h: the block was written with RECORDS_INVALID counts
 
 
 def frame_shard(total: int, rank: int, world: int) -> range:
@@ -117,10 +117,11 @@ class FrameParallel:
         nb = records_nbytes(B, self.per_frame)
         if self.block is None or self.block.numel() != nb:
             self.block = torch.empty(nb, dtype=torch.uint8, device=device)
-        # every batch collected is checked: a replay that gave up fails here (after the gather, which the
-        # other ranks are in; its block carries RECORDS_INVALID counts so the receivers see it too)
+        # every batch collected is checked: a batch whose results are invalid (a replay give-up or a refused
+        # record) fails here, after the gather, which the other ranks are in — its block carries RECORDS_INVALID
+        # counts, so the receivers see it too. Any other error leaves the block undefined: it is not sent.
         rc = self.ctx.records_copy(self.block.data_ptr(), self.per_frame, stream=stream, batch=bid, check=False)
-        if rc not in (0, DOFS_ERR_DEVICE):
+        if rc not in (0, DOFS_ERR_INVALID_RESULT):
             raise RuntimeError(f"dofs_batch_records_copy failed ({rc}): {self.ctx.last_error()}")
         out = gather_records(self.block, self.world)
         self.checked += 1

@@ -147,7 +147,7 @@ def load(path: str | None = None) -> C.CDLL:
     L.dofs_overlay_batch_device.restype = C.c_int32
     L.dofs_overlay.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(C.c_uint8)]
     L.dofs_overlay.restype = C.c_int32
-    if L.dofs_abi_version() != 2:
+    if L.dofs_abi_version() != 3:
         raise RuntimeError("dofs ABI version mismatch")
     _LIBS[path] = L
     return L
@@ -415,6 +415,15 @@ class Dofs:
 
     def last_error(self) -> str:
         return self.lib.dofs_last_error(self.ctx).decode()
+
+    def knobs(self) -> dict:
+        """The runtime knobs this context was created with (csrc/dofs_knobs.h; 0 = the backend's default)."""
+        f = self.lib.dofs_debug_knobs
+        f.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
+        f.restype = C.c_int32
+        out = (C.c_int32 * 5)()
+        self._err(f(self.ctx, out), "dofs_debug_knobs")
+        return dict(zip(("serial", "flow_long", "long_path", "krt_dnc", "pre_jump"), list(out)))
 
     def flow_workers(self) -> dict | None:
         """The dataflow replay's worker waves {"long": .., "short": ..} (HIP library only)."""

@@ -48,6 +48,9 @@
  *   - Every entry point returns a dofs_status; no exceptions cross the ABI. An invalid `neighbor`
  *     falls back to the 4-neighbourhood exactly like segment.cpp:38-43 (not an error).
  *   - One dofs_ctx per host thread; each context owns one HIP stream unless a stream is passed.
+ *     dofs_create may be called from several threads at once. Each context keeps the DOFS_* runtime knobs
+ *      of the environment it was created in. dofs_last_error(NULL) reports the calling
+ *     thread's last failed dofs_create; the string stays valid until that thread's next dofs_create.
  *   - The GPU library (libdofs_hip.so) requires a gfx950 device; there is no CPU fallback.
  */
 #ifndef DOFS_H
@@ -60,7 +63,7 @@
 extern "C" {
 #endif
 
-#define DOFS_ABI_VERSION 2
+#define DOFS_ABI_VERSION 3
 
 typedef enum dofs_status {
     DOFS_OK = 0,
@@ -68,7 +71,11 @@ typedef enum dofs_status {
     DOFS_ERR_NO_DEVICE = 2,
     DOFS_ERR_DEVICE = 3,      /* a HIP runtime call failed; see dofs_last_error() */
     DOFS_ERR_CAPACITY = 4,    /* result capacity too small; n_snapshots holds the required count */
-    DOFS_ERR_OOM = 5
+    DOFS_ERR_OOM = 5,
+    DOFS_ERR_INVALID_RESULT = 6 /* the batch ran, but its results are invalid: its replay gave up a bounded
+                                   wait, or a replay record held a root outside its frame (never seen; the
+                                   device refused to use it) — dofs_last_error() says which. No HIP call
+                                   failed. ABI version 3: version 2 returned DOFS_ERR_DEVICE here. */
 } dofs_status;
 
 /* Constants of the path; dofs_default_params() fills the reference values. */
@@ -268,10 +275,12 @@ int32_t dofs_batch_records_device(dofs_ctx* ctx, void** d_records, void** d_coun
  * dofs_snapshot_capacity() records (default 4096), so per_frame must not exceed that capacity:
  * DOFS_ERR_CAPACITY (nothing copied) otherwise, whatever the data — ranks of one configuration
  * therefore all copy or all fail. The labels are exact in every case.
- * Waits on the host for the batch (one wait per copy) and checks its replay: a batch whose replay gave up
- * a bounded wait (never seen) is copied with every count = DOFS_RECORDS_INVALID and the
- * call returns DOFS_ERR_DEVICE, so a gather that follows still moves equal blocks and every receiver can
- * tell which frames are invalid. */
+ * Waits on the host for the batch (one wait per copy) and checks its results: a batch whose results are
+ * invalid (DOFS_ERR_INVALID_RESULT: its replay gave up a bounded wait, or a replay record held an
+ * out-of-range root; never seen) is copied with every count = DOFS_RECORDS_INVALID and the
+ * call returns DOFS_ERR_INVALID_RESULT, so a gather that follows still moves equal blocks and every receiver
+ * can tell which frames are invalid. Any other error (DOFS_ERR_DEVICE: a HIP call failed) leaves the block
+ * undefined: do not send it. */
 #define DOFS_RECORDS_INVALID (-1)
 int32_t dofs_batch_records_copy(dofs_ctx* ctx, void* d_dst, int32_t per_frame, void* stream);
 /* Same for batch id `batch` (one of the last three issued); ordered after that batch on `stream`. */

@@ -49,8 +49,10 @@ size_t dofs_records_block_bytes(int32_t frames, int32_t per_frame);
  * root >= 0: ncclGather to rank `root`, d_recv (nranks blocks in rank order) is only written there and may be
  * NULL elsewhere; root < 0: ncclAllGather, every rank's d_recv receives all blocks. Returns what
  * dofs_batch_records_copy returns (DOFS_ERR_CAPACITY when a frame overflowed the snapshot capacity, before any
- * collective is issued — every rank sees its own overflow, so a host should agree on it before gathering), or
- * DOFS_ERR_DEVICE if RCCL fails (dofs_comm_last_error). */
+ * collective is issued — every rank sees its own overflow, so a host should agree on it before gathering;
+ * DOFS_ERR_INVALID_RESULT after the collective, whose block from this rank then carries DOFS_RECORDS_INVALID
+ * counts; any other copy error before it, with nothing sent), or DOFS_ERR_DEVICE if RCCL fails
+ * (dofs_comm_last_error). */
 int32_t dofs_gather_records(dofs_ctx* ctx, dofs_comm* comm, int32_t per_frame, int32_t root, void* d_recv,
                             void* stream);
 

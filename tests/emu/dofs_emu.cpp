@@ -66,7 +66,7 @@ inline void dofs_agg_min(int* base, int key, int val, bool act) {
 
 namespace dofs {
 struct HostBackend {
-    explicit HostBackend(int) {}
+    HostBackend(int, const Knobs& k) : kn(k) {}
     static bool device_ok(int) { return true; }
     bool ok() const { return true; }
     std::string error() const { return std::string(); }
@@ -242,7 +242,7 @@ struct HostBackend {
     bool pre_sweep(const Ws&) { return false; }  // KJump (the emulator's KRT has no block epilogue)
     static bool pairs_in_relabel(const Ws&) { return false; }  // KBoruvkaPairs
     bool pre_jump(const Dims&) const { return false; }  // (KDncParent writes every word itself)
-    Knobs kn = knobs();  // the context's runtime knobs (dofs_knobs.h)
+    Knobs kn;  // the context's runtime knobs (dofs_knobs.h), read when it was created
     static constexpr bool kSingleFlags = false;  // its sweep model reads EU / EV as plain endpoints
     static constexpr bool kLeanReplay = true;  // (its replay stores every record; dofs_events follows the HIP rule)
     void sort_mst(Ws& w, int64_t n, int nf, int value_bits, bool) {

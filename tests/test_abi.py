@@ -40,7 +40,7 @@ def test_rccl_library_exports_every_declared_symbol():
 def test_abi_version_and_struct_layouts():
     from denseopticalflowsegmentation3d_amd import abi, runtime
     lib = runtime.load()
-    assert lib.dofs_abi_version() == 2
+    assert lib.dofs_abi_version() == 3
     p = abi.DofsParams()
     lib.dofs_default_params(ctypes.byref(p))
     ref = abi.default_params()

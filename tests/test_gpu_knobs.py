@@ -54,3 +54,19 @@ def test_knob_changes_nothing_but_speed(monkeypatch, calib, batch_and_default, e
         assert ev[f].tobytes() == ev0[f].tobytes(), (env, f)
         assert np.array_equal(res[f].labels, r0[f].labels), (env, f)
         assert res[f].snapshots.tobytes() == r0[f].snapshots.tobytes(), (env, f)
+
+
+def test_two_contexts_keep_their_own_workers(monkeypatch):
+    """Knobs are per context: two live contexts created under different DOFS_FLOW_LONG each
+    launch their own long-worker count."""
+    from denseopticalflowsegmentation3d_amd import runtime
+    monkeypatch.setenv("DOFS_FLOW_LONG", "64")
+    a = runtime.Dofs(0)
+    monkeypatch.setenv("DOFS_FLOW_LONG", "512")
+    b = runtime.Dofs(0)
+    try:
+        assert a.flow_workers()["long"] == 64
+        assert b.flow_workers()["long"] == 512
+    finally:
+        a.close()
+        b.close()

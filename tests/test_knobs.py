@@ -60,3 +60,61 @@ def test_only_the_listed_knobs_are_read():
         ROOT, "denseopticalflowsegmentation3d_amd", "csrc", "dofs_knobs.h")).read()))
     assert names == {"DOFS_SERIAL", "DOFS_FLOW_LONG", "DOFS_LONG_PATH", "DOFS_KRT_DNC", "DOFS_PRE_JUMP",
                      "DOFS_LIB", "DOFS_SKIP_B", "DOFS_SKIPMASK", "DOFS_B_DELAY"}
+
+
+def test_knobs_are_per_context(monkeypatch, emu_lib):
+    """Each context keeps the knobs of the environment it was created in: a context created
+    later under another DOFS_FLOW_LONG does not change an earlier one's."""
+    from denseopticalflowsegmentation3d_amd.runtime import Dofs
+    monkeypatch.setenv("DOFS_FLOW_LONG", "64")
+    monkeypatch.setenv("DOFS_LONG_PATH", "128")
+    a = Dofs(0, lib=emu_lib)
+    monkeypatch.setenv("DOFS_FLOW_LONG", "512")
+    monkeypatch.delenv("DOFS_LONG_PATH")
+    b = Dofs(0, lib=emu_lib)
+    try:
+        assert a.knobs()["flow_long"] == 64 and a.knobs()["long_path"] == 128
+        assert b.knobs()["flow_long"] == 512 and b.knobs()["long_path"] == 0
+        monkeypatch.delenv("DOFS_FLOW_LONG")
+        c = Dofs(0, lib=emu_lib)
+        assert c.knobs()["flow_long"] == 0 and a.knobs()["flow_long"] == 64
+        c.close()
+    finally:
+        a.close()
+        b.close()
+
+
+def test_create_error_is_per_thread(monkeypatch, emu_lib):
+    """dofs_last_error(NULL) is the calling thread's last failed dofs_create: a create on another
+    thread neither changes nor invalidates it, and creates on many threads at once do not race."""
+    import ctypes as C
+    import threading
+
+    from denseopticalflowsegmentation3d_amd.runtime import Dofs, load
+    lib = load(emu_lib)
+    lib.dofs_create.restype = C.c_void_p
+    lib.dofs_last_error.argtypes = [C.c_void_p]
+    lib.dofs_last_error.restype = C.c_char_p
+    monkeypatch.setenv("DOFS_SERIAL", "7")
+    assert not lib.dofs_create(0)
+    mine = lib.dofs_last_error(None).decode()
+    assert "DOFS_SERIAL=7" in mine
+    monkeypatch.delenv("DOFS_SERIAL")
+    errs, others = [], []
+
+    def worker():
+        try:
+            for _ in range(20):
+                Dofs(0, lib=emu_lib).close()
+            others.append(lib.dofs_last_error(None).decode())
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    ts = [threading.Thread(target=worker) for _ in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    assert others == ["null context"] * 4
+    assert lib.dofs_last_error(None).decode() == mine
