@@ -130,14 +130,21 @@ __device__ inline unsigned long long f_poll64(unsigned long long* p) {
     return __hip_atomic_fetch_or(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// a RepVal handed to another workgroup: three 8-byte write-through stores / loads (the pads are unused)
+// a 16-byte write-through (sc1) store: one global_store_dwordx4 (HIP has no 16-byte atomic store). It
+// returns nothing, so the compiler needs no wait for it; f_drain's explicit vmcnt(0) covers it like any store
+__device__ inline void f_st128(void* p, unsigned a, unsigned b, unsigned c, unsigned e) {
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    const u4 v = {a, b, c, e};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+// a RepVal handed to another workgroup: its 24 bytes as one 16-byte and one 8-byte write-through store (two
+// sector writes; three 8-byte stores were three), never touching the pads — the first is a path top's state
+// word (state_at), which a parker may be CASing meanwhile. Read back by three 8-byte loads (rv_fetch).
 __device__ inline void rv_publish(RepVal* p, float mx, float my, int rank, int root, B4 bb) {
-    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
-    f_st64(q, (unsigned long long)__float_as_uint(mx) | ((unsigned long long)__float_as_uint(my) << 32));
-    f_st64(q + 1, (unsigned long long)(unsigned)rank | ((unsigned long long)(unsigned)root << 32));
+    f_st128(p, __float_as_uint(mx), __float_as_uint(my), (unsigned)rank, (unsigned)root);
     unsigned long long b;
     __builtin_memcpy(&b, &bb, 8);
-    f_st64(q + 2, b);
+    f_st64(reinterpret_cast<unsigned long long*>(p) + 2, b);
 }
 __device__ inline RepVal rv_fetch(const RepVal* p) {
     const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);

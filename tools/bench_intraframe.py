@@ -30,7 +30,7 @@ from denseopticalflowsegmentation3d_amd.bands import IntraFrame, band_bounds  # 
 
 def model(a):
     """Projected N-GPU time of the row-band path from single-GPU measurements of its parts."""
-    from denseopticalflowsegmentation3d_amd.bands import add_cut_edges, blur_radius, halo_bounds
+    from denseopticalflowsegmentation3d_amd.bands import add_cut_edges, blur_radius, halo_bounds, split_gain_ms
     H, W, n = a.height, a.width, a.model
     ctx = runtime.Dofs(0)
     persp, inv, up = runtime.calib()
@@ -81,13 +81,26 @@ def model(a):
     gather_bytes = (n - 1) * per_band * W * (1 + 8)  # edge-bit mask + flow rows of every other band
     t_gather = 1e3 * gather_bytes / (a.xgmi_gbs * 1e9)
     t_n = max(band_ms) + t_gather + t_masked
+    # the policy IntraFrame(split="auto") takes for this shape (the frame resident on rank 0, as here): the
+    # split only where its cost model says it saves time, else the frame on rank 0 alone (= one GPU)
+    split = split_gain_ms(H, W, n, a.xgmi_gbs, resident=True) > 0
+    t_pol = t_n if split else t_one
+    # the single-frame latency floor: the replay's dependency chain (profiles/r05/critical_path_4k_emu.json:
+    # 1,536,516 merges at 4K, seed 1) at the measured 21.5 ns per long-path step — no split shortens it
+    floor = 1536516 * 21.5e-6 if (H, W) == (2160, 3840) else None
     print(json.dumps({"config": f"{W}x{H} synthetic, {n} row bands, projected from one GPU",
                       "band_msf_ms": [round(x, 3) for x in band_ms], "gather_ms_est": round(t_gather, 3),
                       "gather_bytes": gather_bytes, "xgmi_gbs_assumed": a.xgmi_gbs,
                       "rank0_masked_ms": round(t_masked, 3),
                       "rank0_stage_ms": {k: round(v / max(nb, 1), 3) for k, v in ms.items()},
-                      "projected_ms_per_frame": round(t_n, 3), "one_gpu_ms_per_frame": round(t_one, 3),
-                      "projected_speedup": round(t_one / t_n, 3)}), flush=True)
+                      "split_model_gain_ms": round(split_gain_ms(H, W, n, a.xgmi_gbs, resident=True), 3),
+                      "policy": "split" if split else "replica (rank 0 alone)",
+                      "projected_ms_per_frame_split": round(t_n, 3), "projected_speedup_split": round(t_one / t_n, 3),
+                      "projected_ms_per_frame": round(t_pol, 3), "one_gpu_ms_per_frame": round(t_one, 3),
+                      "projected_speedup": round(t_one / t_pol, 3),
+                      "latency_floor_ms": round(floor, 1) if floor else None,
+                      "latency_floor": "the replay's dependency chain, 1,536,516 merges x 21.5 ns (one 4K frame)"}),
+          flush=True)
     ctx.close()
 
 
@@ -99,6 +112,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", type=int, default=0, help="one GPU: project the N-band sharded time (N = value)")
     ap.add_argument("--xgmi-gbs", type=float, default=64.0, help="assumed gather bandwidth to rank 0 (GB/s)")
+    ap.add_argument("--split", default="auto", help="row-band split: auto (IntraFrame's cost model), 1 or 0")
     a = ap.parse_args()
     if a.model:
         return model(a)
@@ -118,10 +132,11 @@ def main():
     r0, r1 = band_bounds(H, world, rank)
     band = full[0, r0:r1].contiguous()
     rec = torch.empty(4 + 64 * 96, dtype=torch.uint8, device="cuda")
-    shard = IntraFrame(ctx, world, rank, prm)
+    shard = IntraFrame(ctx, world, rank, prm, split=a.split if a.split == "auto" else a.split == "1",
+                       xgmi_gbs=a.xgmi_gbs)
 
-    def step():
-        bid = shard.step(band, H, W, persp, inv, up, stream=sh)
+    def step():  # (the frame is resident on every rank here: rank 0 passes it, so "auto" may skip the split)
+        bid = shard.step(band, H, W, persp, inv, up, stream=sh, frame=full[0] if rank == 0 else None)
         if rank == 0:
             ctx.records_copy(rec.data_ptr(), 64, stream=sh, batch=bid)
 
@@ -152,6 +167,7 @@ def main():
         torch.cuda.synchronize()
         t_one = (time.perf_counter() - t0) / a.steps
         print(json.dumps({"config": f"{W}x{H} synthetic, row bands over {world} GPU(s), MST sharded",
+                          "split": bool(shard.did_split),
                           "frames_per_sec": round(1 / t_shard, 3), "mpix_per_sec": round(H * W / t_shard / 1e6, 3),
                           "ms_per_frame": round(t_shard * 1e3, 3), "one_gpu_ms_per_frame": round(t_one * 1e3, 3),
                           "n_gpus": world}), flush=True)

@@ -14,6 +14,9 @@
 //       sc1-stores its flag;
 //   C: polls P's flag (sc1 loads), then re-loads word `b` (sc1, or plain for the positive control):
 //       stale = the value before P's store.
+// A last case has C plain-store a neighbouring word of the same sector before signalling (a 24-byte record's
+// neighbour written by another wave), and the host then checks every line in memory: a write-back of C's
+// copy of the line must not undo P's bytes (lost = a line whose P word or C word does not hold its value).
 // Pairs are (block 2k, 2k+1) (dealt to different XCDs) or (block k, k+8) (the same XCD); every block
 // records its XCC id, so each trial is classified by the XCDs it actually ran on. Every wait is bounded
 // (a timeout is counted, never a hang). Build: hipcc --offload-arch=gfx950 -O3 -o tools/_build/stale_sector_micro
@@ -44,6 +47,7 @@ struct Cfg {
     int a, b;     // word C loads first, word P republishes (same line)
     int reload;   // 1 sc1 re-load, 2 plain re-load (positive control: L1 keeps the line)
     int dist;     // pair distance in blocks: 1 (different XCDs) or 8 (same XCD)
+    int cst;      // >= 0: C plain-stores this word of the line before signalling (a neighbour record's store)
 };
 
 // out[blk] = XCC id; res[pair * 4 + {0 stale, 1 timeouts, 2 trials}]
@@ -66,6 +70,7 @@ __global__ void probe(int* lines, int* flags, int* xcc, int* res, int trials, Cf
             if (c.first == 2) v0 = line[c.a];
             drain();
             if (c.cas) atomicCAS(line + 4, -7, -8);  // (fails: word 4 holds 0; still an agent atomic on the sector)
+            if (c.cst >= 0) line[c.cst] = 77 + t;
             drain();
             fc[1] = v0;  // keeps the first load live (on the flag's line, never on the probed line)
             st_sc1(fc, t + 1);
@@ -112,15 +117,17 @@ int main(int argc, char** argv) {
         Cfg c;
     };
     const Named cfgs[] = {
-        {"no first load, sc1 reload (baseline)", {0, 0, 0, 0, 1, 1}},
-        {"sc1 first load of the same word, sc1 reload", {1, 0, 0, 0, 1, 1}},
-        {"sc1 first load of the same word, CAS, sc1 reload", {1, 1, 0, 0, 1, 1}},
-        {"sc1 load of word 0, P writes word 2 (same sector)", {1, 0, 0, 2, 1, 1}},
-        {"sc1 load of word 0, P writes word 8 (next sector, same line)", {1, 0, 0, 8, 1, 1}},
-        {"plain first load, sc1 reload", {2, 0, 0, 0, 1, 1}},
-        {"plain first load, plain reload (positive control)", {2, 0, 0, 0, 2, 1}},
-        {"same XCD: sc1 first load, sc1 reload", {1, 0, 0, 0, 1, 8}},
-        {"same XCD: plain first load, plain reload (positive control)", {2, 0, 0, 0, 2, 8}},
+        {"no first load, sc1 reload (baseline)", {0, 0, 0, 0, 1, 1, -1}},
+        {"sc1 first load of the same word, sc1 reload", {1, 0, 0, 0, 1, 1, -1}},
+        {"sc1 first load of the same word, CAS, sc1 reload", {1, 1, 0, 0, 1, 1, -1}},
+        {"sc1 load of word 0, P writes word 2 (same sector)", {1, 0, 0, 2, 1, 1, -1}},
+        {"sc1 load of word 0, P writes word 8 (next sector, same line)", {1, 0, 0, 8, 1, 1, -1}},
+        {"plain first load, sc1 reload", {2, 0, 0, 0, 1, 1, -1}},
+        {"plain first load, plain reload (positive control)", {2, 0, 0, 0, 2, 1, -1}},
+        {"same XCD: sc1 first load, sc1 reload", {1, 0, 0, 0, 1, 8, -1}},
+        {"same XCD: plain first load, plain reload (positive control)", {2, 0, 0, 0, 2, 8, -1}},
+        {"plain load of word 0, C plain-stores word 6, P writes word 0 (same sector)", {2, 0, 0, 0, 1, 1, 6}},
+        {"sc1 load of word 6, C plain-stores word 6, P writes word 2 (same sector)", {1, 0, 6, 2, 1, 1, 6}},
     };
     std::vector<int> hx(2 * kPairs), hr(kPairs * 4);
     printf("{\"trials_per_pair\": %d, \"pairs\": %d, \"results\": [\n", trials, kPairs);
@@ -137,7 +144,16 @@ int main(int argc, char** argv) {
             }
             (void)hipMemcpy(hx.data(), xcc, 2 * kPairs * 4, hipMemcpyDeviceToHost);
             (void)hipMemcpy(hr.data(), res, kPairs * 4 * 4, hipMemcpyDeviceToHost);
-            long long st_cross = 0, n_cross = 0, st_same = 0, n_same = 0, tmo = 0;
+            long long st_cross = 0, n_cross = 0, st_same = 0, n_same = 0, tmo = 0, lost = 0;
+            {  // the lines in memory after the launch: P's word (and C's, where it stored one) hold their values
+                std::vector<int> hl(line_bytes / 4);
+                (void)hipMemcpy(hl.data(), lines, line_bytes, hipMemcpyDeviceToHost);
+                for (int p = 0; p < kPairs; ++p)
+                    for (int t = 0; t < trials; ++t) {
+                        const int* L = hl.data() + ((size_t)p * trials + t) * kLineInts;
+                        if (L[cfgs[k].c.b] != 1000 + t || (cfgs[k].c.cst >= 0 && L[cfgs[k].c.cst] != 77 + t)) ++lost;
+                    }
+            }
             const int dist = cfgs[k].c.dist;
             for (int p = 0; p < kPairs; ++p) {
                 const int grp = p / dist, o = p % dist;
@@ -148,8 +164,8 @@ int main(int argc, char** argv) {
                 tmo += hr[p * 4 + 1] + hr[p * 4 + 3];
             }
             printf("  {\"case\": \"%s\", \"rep\": %d, \"cross_xcd_trials\": %lld, \"cross_xcd_stale\": %lld, "
-                   "\"same_xcd_trials\": %lld, \"same_xcd_stale\": %lld, \"timeouts\": %lld}%s\n",
-                   cfgs[k].name, rep, n_cross, st_cross, n_same, st_same, tmo,
+                   "\"same_xcd_trials\": %lld, \"same_xcd_stale\": %lld, \"timeouts\": %lld, \"lost_in_memory\": %lld}%s\n",
+                   cfgs[k].name, rep, n_cross, st_cross, n_same, st_same, tmo, lost,
                    (k + 1 == sizeof(cfgs) / sizeof(cfgs[0]) && rep == 1) ? "" : ",");
         }
     }
