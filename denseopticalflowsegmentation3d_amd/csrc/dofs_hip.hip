@@ -2446,6 +2446,26 @@ struct KLeafPos {
 
 #include "dofs_sortfix.h"
 
+// The batch sort's onesweep shape: 512-thread sort blocks of 12 items per thread instead of rocPRIM's gfx950
+// default (1024 x 16). The sort runs beside stage B of the previous batch (the replay's persistent workers, the
+// scoring); a 1,024-thread block needs a quarter of a CU's wave slots free at once, and one pass's decoupled
+// look-back chain waited behind such blocks (one pass 1.5 ms alone, 14.4 ms beside KLift / KLabel in the
+// round-5 pipelined trace). Same box, B = 112, two runs each (round 6): default 1,874 / 1,902 Mpix/s, 512 x 12
+// 1,928 / 1,945, with the default 1024 x 16 histogram blocks 1,943 / 1,945; 256 x 12 1,889 / 1,888, 512 x 16
+// 1,895 / 1,904, 512 x 8 1,917 / 1,926. Build-time knobs for that A/B: DOFS_SORT_BS x DOFS_SORT_IPT per sort
+// block, DOFS_SORT_HBS x DOFS_SORT_HIPT per histogram block.
+#ifndef DOFS_SORT_BS
+#define DOFS_SORT_BS 512
+#define DOFS_SORT_IPT 12
+#define DOFS_SORT_HBS 1024
+#define DOFS_SORT_HIPT 16
+#endif
+using SortCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<DOFS_SORT_HBS, DOFS_SORT_HIPT>,
+                                        rocprim::kernel_config<DOFS_SORT_BS, DOFS_SORT_IPT>, 8,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+
 struct HipBackend {
     int device = 0;
     hipStream_t own = nullptr;
@@ -3125,6 +3145,16 @@ struct HipBackend {
     // Packed: w.EU (written later by KEdgeInit) is the scratch between the two passes.
     static int sort_k32() { return g_sort_k32; }  // KMstEmit's 32-bit keys for the packed sort (0: 64-bit)
     static int sort_k32_bits() { return dofs::sort_k32_bits(); }
+    // the batch sort's (u32 key, u32 value) pair passes and the frame pass, through rocPRIM's onesweep with
+    // SortCfg's block shape
+    hipError_t sort_pairs32(void* t, size_t& b, const unsigned* kin, unsigned* kout, const unsigned* vin, unsigned* vout,
+                            int n, int bit0, int bit1) {
+        return rocprim::radix_sort_pairs<SortCfg>(t, b, kin, kout, vin, vout, (size_t)n, (unsigned)bit0, (unsigned)bit1,
+                                                  stream);
+    }
+    hipError_t sort_keys32(void* t, size_t& b, const unsigned* kin, unsigned* kout, int n, int bit0, int bit1) {
+        return rocprim::radix_sort_keys<SortCfg>(t, b, kin, kout, (size_t)n, (unsigned)bit0, (unsigned)bit1, stream);
+    }
     void sort_mst(Ws& w, int64_t n, int nf, int value_bits, bool packed) {
         if (!packed) {
             sort_pairs(w.key_in, w.key_out, w.val_in, w.val_out, n, nf, value_bits);
@@ -3138,12 +3168,10 @@ struct HipBackend {
             unsigned* vmid = reinterpret_cast<unsigned*>(w.EU);
             size_t b1 = 0, b2 = 0;
             const int kb = sort_k32_bits();
-            note(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, k32_in, k32_out, w.val_in, vmid, tot, 0, kb, stream),
-                 "sort size");
-            note(hipcub::DeviceRadixSort::SortKeys(nullptr, b2, vmid, w.val_out, tot, value_bits, value_bits + fb, stream),
-                 "sort size");
+            note(sort_pairs32(nullptr, b1, k32_in, k32_out, w.val_in, vmid, tot, 0, kb), "sort size");
+            note(sort_keys32(nullptr, b2, vmid, w.val_out, tot, value_bits, value_bits + fb), "sort size");
             void* t = temp(std::max(b1, b2));
-            note(hipcub::DeviceRadixSort::SortPairs(t, b1, k32_in, k32_out, w.val_in, vmid, tot, 0, kb, stream), "sort");
+            note(sort_pairs32(t, b1, k32_in, k32_out, w.val_in, vmid, tot, 0, kb), "sort");
             if (g_sort_fix) sort_fixup32(w, vmid, tot, value_bits);
             if (g_sort_dump[0]) {  // diagnosis: 32-bit keys (4 bytes each) and values after the fix-up
                 const size_t m = (size_t)std::min<int64_t>(tot, g_sort_dump_cap);
@@ -3151,8 +3179,7 @@ struct HipBackend {
                 note(hipMemcpyAsync(g_sort_dump[1], vmid, 4 * m, hipMemcpyDeviceToDevice, stream), "dump");
                 g_sort_dump[0] = g_sort_dump[1] = nullptr;
             }
-            note(hipcub::DeviceRadixSort::SortKeys(t, b2, vmid, w.val_out, tot, value_bits, value_bits + fb, stream),
-                 "sort frames");
+            note(sort_keys32(t, b2, vmid, w.val_out, tot, value_bits, value_bits + fb), "sort frames");
             return;
         }
         const int cut = g_sort_cut;
