@@ -1355,7 +1355,10 @@ __global__ __launch_bounds__(128) void k_replay_flow_pair(Ws w, int* ctl, unsign
     if (lane == 0) fs_max(ctl, FS_T_EXIT, fs_now());
 }
 
-constexpr int kFlowShortW = 8;  // waves per short-worker workgroup
+#ifndef DOFS_FLOW_SHORT_W
+#define DOFS_FLOW_SHORT_W 8
+#endif
+constexpr int kFlowShortW = DOFS_FLOW_SHORT_W;  // waves per short-worker workgroup
 constexpr int kFlowLongW = 4;    // waves per long-worker workgroup (one per SIMD)
 
 // counter C_FLOWERR of frame 0 = a bounded wait of the launch gave up (dofs_batch_counters); force: a test

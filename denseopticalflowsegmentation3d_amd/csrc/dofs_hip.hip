@@ -233,8 +233,11 @@ __global__ __launch_bounds__(kBlock) void k_generic_take(F f, int64_t n) {
 // shrinking list costs only the blocks it needs (the others exit at once)
 // (at least three waves per SIMD: KLift's lifting needed 169 VGPRs, two waves per SIMD, beside the graph
 // stage's sort passes)
+#ifndef DOFS_COUNTED_WPE
+#define DOFS_COUNTED_WPE 3
+#endif
 template <class F>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_counted_take(F f, int64_t n, int cidx,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DOFS_COUNTED_WPE))) void k_counted_take(F f, int64_t n, int cidx,
                                                                                                   int zidx) {
     __shared__ int wsum[3 * kBlock / 64];
     __shared__ int base[3];
