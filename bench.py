@@ -115,7 +115,7 @@ def parse(argv=None):
     ap.add_argument("--no-stages", action="store_true", help="skip the per-stage event timing pass")
     ap.add_argument("--no-h2d", action="store_true", help="skip the with-H2D (host input) pass")
     ap.add_argument("--probe", default=",".join(PROBES), help="kernels timed with device events (comma list)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05", "pmc_kernels.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r06", "pmc_kernels.json"),
                     help="PMC summary JSON (tools/pmc_kernels.py via tools/pmc_round.sh) for the roofline traffic; "
                          "used only when its lib_sha256 is the loaded library's")
     ap.add_argument("--cpu-worker", nargs=4, metavar=("OPT", "H", "W", "SEED"), help=argparse.SUPPRESS)

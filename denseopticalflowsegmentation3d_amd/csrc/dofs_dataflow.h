@@ -1,6 +1,6 @@
 // dofs_dataflow.h — K5, the replay of Forest::merge (graph.cpp:170-218) along heavy paths, as ONE
-// dataflow launch per batch (included by dofs_hip.hip after the round-based kernels it replaces;
-// DOFS_REPLAY_FLOW=0 selects those).
+// dataflow launch per batch (included by dofs_hip.hip; the test emulator keeps the round-based form,
+// KReplay in dofs_kernels.h).
 //
 // Why: a heavy path advances until it meets a light child whose own path is not complete. The round
 // launches park such a path until the next round, so a round lasts as long as the longest advance

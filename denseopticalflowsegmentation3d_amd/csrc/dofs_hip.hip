@@ -1904,8 +1904,8 @@ __global__ __launch_bounds__(256) void k_boruvka_relabel4(Ws w, int r) {
     }
 }
 
-// Round 0's KBoruvkaPairs and the first half of its relabel, per 64 x 32 tile (DOFS_TILE0, default;
-// k_boruvka_relabel4 over comp finishes). KBoruvkaFirst left each pixel's pointer along its minimum edge
+// Round 0's KBoruvkaPairs and the first half of its relabel, per 64 x 32 tile (k_boruvka_relabel4 over
+// comp finishes). KBoruvkaFirst left each pixel's pointer along its minimum edge
 // in uf: a forest whose only cycles are the mutual pairs, each rooted at its smaller pixel. The tile and a
 // 4-pixel halo are staged in LDS as cell pointers (a pointer goes to one of the eight neighbours, so only
 // a halo cell can point out of the region: then the cell keeps the target pixel, encoded negative). The
@@ -2806,8 +2806,8 @@ struct HipBackend {
     // slot-table race in k_dnc_compress, fixed there; tests/test_gpu_krt_dnc.py holds the two modes equal.
     static constexpr bool kDncAuto = true;
     static constexpr bool kSingleFlags = true;  // KMstEmit / KEdgeInit mark single-pixel endpoints (Ws::single)
-    // Ws::rv_lean is honoured (the dataflow replay; DOFS_REPLAY_FLOW=0's rounds still store every record,
-    // but a lean batch refuses dofs_events either way)
+    // Ws::rv_lean is honoured (the dataflow replay; the emulator's rounds store every record, but a lean
+    // batch refuses dofs_events either way)
     static constexpr bool kLeanReplay = true;
     // longest pointer chain the preorder's global jumping starts from: every word leaves its block
     // or goes to the block's top, so at most two words per block on any path
