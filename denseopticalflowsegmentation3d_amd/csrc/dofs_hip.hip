@@ -1368,15 +1368,31 @@ __global__ __launch_bounds__(256) void k_boruvka_recs(Ws w, int r, RecBufs rb) {
             if (wb != bw[key]) continue;
             if (!kHook) {
                 if (ix < bi[key]) atomicMin(bi + key, ix);
-            } else if (ix == bi[key]) {  // the component's minimum edge: hook along it (boruvka_hook_root)
+            } else if (ix == bi[key]) {  // the component's minimum edge: hook along it
                 bw[key] = ~0ull;
                 bi[key] = kNoEdge;
                 const int64_t p = ix >> 2;
                 const int e = ix & 3;
                 const int64_t q = edge_end(d, p, e);
-                reinterpret_cast<unsigned char*>(w.mstbits + f * d.N + p)[e] = 1;
                 const int* comp = w.comp + f * d.N;
-                uf_union(w.uf + f * d.N, comp[p], comp[q]);
+                const int cp = comp[p], cq = comp[q];  // current roots: both ends lie in active tiles
+                const int o = cp == key ? cq : cp;     // the component across the edge
+                // Borůvka's hooking graph under a strict edge order is a forest plus one 2-cycle per tree
+                // (two components whose minimum edge is the same edge), so the root points at the other
+                // component directly — no finds, no CAS — and the edge's MST flag, set by an atomic OR, tells
+                // the second of a mutual pair to root the pair at its smaller label (its partner's pointer
+                // store was drained before the partner's OR). Round 6, same box: MST stage 29.4 → 27.5 ms,
+                // 1,955 / 1,968 / 1,967 → 1,987 / 1,986 / 1,967 Mpix/s against the CAS union (uf_union)
+                int* P = w.uf + f * d.N;
+                dofs_st(P + key, o);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const unsigned bit = 1u << (8 * e);
+                const unsigned old = __hip_atomic_fetch_or(reinterpret_cast<unsigned*>(w.mstbits + f * d.N + p), bit,
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (old & bit) {
+                    const int m = key < o ? key : o;
+                    dofs_st(P + m, m);
+                }
             }
         }
     }

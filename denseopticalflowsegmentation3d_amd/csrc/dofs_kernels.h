@@ -99,7 +99,8 @@ struct Ws {
     unsigned long long* bw;
     unsigned* bi;
     int* uf;
-    int* mstbits;  // per pixel: byte k != 0 <=> its emitted edge k is an MST edge (plain byte stores)
+    int* mstbits;  // per pixel: byte k != 0 <=> its emitted edge k is an MST edge (plain byte stores; the
+                   // HIP record hook sets its byte by an atomic OR on the word)
     int* cnt;
     int* off;
     // MST edges (stride M)
