@@ -2016,9 +2016,11 @@ __global__ __launch_bounds__(kT0T) void k_boruvka_tile0(Ws w) {
 
 // KBoruvkaRelabelFind of rounds >= 1 on the record path, one wave per 32x8 tile (four pixels per lane):
 // a tile is relabelled only while it or one of its eight neighbours is active. Pass 0 reads a tile's
-// labels only for the tile itself or as the halo of a neighbour, the hook resolves the labels it
-// reads by finds, and nothing reads them after the MST — so a done tile among done tiles keeps its
-// stale labels (tile flags: the round that found the tile done, written by this round's pass 0).
+// labels only for the tile itself or as the halo of a neighbour, the hook reads the labels of its
+// edge's two ends (both ends have a cross-component edge, so both tiles were active in the last round
+// too and were relabelled at its end), and nothing reads them after the MST — so a done tile among
+// done tiles keeps its stale labels (tile flags: the round that found the tile done, written by this
+// round's pass 0).
 __global__ __launch_bounds__(256) void k_boruvka_relabel_t(Ws w, int r, RecBufs rb) {
     const Dims& d = w.d;
     const int f = blockIdx.y;
