@@ -2014,6 +2014,105 @@ __global__ __launch_bounds__(kT0T) void k_boruvka_tile0(Ws w) {
     }
 }
 
+// Round 0's KBoruvkaInit + KBoruvkaFirst per 64 x 16 tile, for frames of width % 4 == 0 (at least 4) without
+// an edge mask: the tile's blurred flows and a 2-pixel halo are staged in LDS once (one coalesced load per
+// pixel instead of nine), every pixel of the tile and of its 1-pixel ring takes its minimum-edge slot
+// (first_min_slot, as KBoruvkaFirst), and each tile pixel writes its whole MST-flag word — byte k set when
+// its edge k is its own minimum (slot k) or the minimum of the neighbour that edge leads to (slot 4 + k
+// there) — so no pass clears the words first; pointer, minima words and flags as 16-byte stores of four
+// pixels per lane. Labels need no initialisation: k_boruvka_tile0 writes every pixel's.
+constexpr int kF1X = 64, kF1Y = 16, kF1T = 256;
+constexpr int kF1BX = kF1X + 4, kF1BY = kF1Y + 4;  // staged flows: a 2-pixel halo
+constexpr int kF1SX = kF1X + 2, kF1SY = kF1Y + 2;  // slots: the tile and a 1-pixel ring
+static_assert(kF1T == kF1Y * (kF1X / 4), "one lane per four pixels of the tile");
+__global__ __launch_bounds__(kF1T) void k_boruvka_first_t(Ws w) {
+    __shared__ F2 fb[kF1BY * kF1BX];
+    __shared__ unsigned char sj[kF1SY * kF1SX];
+    const Dims& d = w.d;
+    const int f = blockIdx.y;
+    const int W = d.W, H = d.H;
+    const int64_t W64 = W;
+    const F2* b = w.blur + f * d.N;
+    const int tx = (W + kF1X - 1) / kF1X, ty = (H + kF1Y - 1) / kF1Y;
+    const int tid = threadIdx.x;
+    for (int64_t t = blockIdx.x; t < (int64_t)tx * ty; t += gridDim.x) {
+        const int x0 = (int)(t % tx) * kF1X, y0 = (int)(t / tx) * kF1Y;
+        // flows of [x0 - 2, x0 + 66) x [y0 - 2, y0 + 18), addresses clamped into the frame (a clamped cell
+        // stands for no pixel: the slots' ok[] never reads it)
+        for (int e = tid; e < kF1BY * kF1BX; e += kF1T) {
+            int gx = x0 - 2 + e % kF1BX, gy = y0 - 2 + e / kF1BX;
+            gx = gx < 0 ? 0 : (gx >= W ? W - 1 : gx);
+            gy = gy < 0 ? 0 : (gy >= H ? H - 1 : gy);
+            fb[e] = b[(int64_t)gy * W64 + gx];
+        }
+        __syncthreads();
+        for (int e = tid; e < kF1SY * kF1SX; e += kF1T) {
+            const int cx = e % kF1SX, cy = e / kF1SX;  // pixel (x0 - 1 + cx, y0 - 1 + cy)
+            const int x = x0 - 1 + cx, y = y0 - 1 + cy;
+            int jb = 0xFF;
+            if (x >= 0 && x < W && y >= 0 && y < H) {
+                const int64_t p = (int64_t)y * W64 + x;
+                const bool xl = x > 0, xr = x + 1 < W, yu = y > 0, yd = y + 1 < H;
+                const bool ok[8] = {xl, yu, d.nbr8 && xl && yu, d.nbr8 && xl && yd,
+                                    xr, yd, d.nbr8 && xr && yd, d.nbr8 && xr && yu};
+                const int64_t nb[8] = {p - 1, p - W64, p - W64 - 1, p + W64 - 1, p + 1, p + W64, p + W64 + 1, p - W64 + 1};
+                const int c = (cy + 1) * kF1BX + cx + 1;
+                const int nc[8] = {c - 1, c - kF1BX, c - kF1BX - 1, c + kF1BX - 1, c + 1, c + kF1BX, c + kF1BX + 1, c - kF1BX + 1};
+                int64_t q[8];
+                F2 bq[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    q[j] = ok[j] ? nb[j] : p;
+                    bq[j] = fb[ok[j] ? nc[j] : c];
+                }
+                unsigned bidx;
+                jb = first_min_slot(fb[c], bq, ok, 0xffu, p, q, &bidx);
+            }
+            sj[e] = (unsigned char)jb;
+        }
+        __syncthreads();
+        const int ly = tid >> 4, lx = (tid & 15) * 4;
+        const int x = x0 + lx, y = y0 + ly;
+        if (x < W && y < H) {  // W % 4 == 0: the lane's four pixels are all in the frame
+            const int64_t p = (int64_t)y * W64 + x;
+            int far[4], jbs[4];
+            unsigned mb[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int cx = lx + i + 1, cy = ly + 1;
+                const int jb = sj[cy * kF1SX + cx];
+                const int64_t pi = p + i;
+                const int64_t nb[8] = {pi - 1, pi - W64, pi - W64 - 1, pi + W64 - 1, pi + 1, pi + W64, pi + W64 + 1, pi - W64 + 1};
+                int64_t fa = pi;
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (jb == j) fa = nb[j];
+                far[i] = (int)fa;
+                jbs[i] = jb;
+                // edge k leads to the neighbour left, up, up-left, down-left, where it is slot 4 + k
+                const int n0 = sj[cy * kF1SX + cx - 1], n1 = sj[(cy - 1) * kF1SX + cx];
+                const int n2 = sj[(cy - 1) * kF1SX + cx - 1], n3 = sj[(cy + 1) * kF1SX + cx - 1];
+                mb[i] = ((jb == 0 || n0 == 4) ? 1u : 0u) | ((jb == 1 || n1 == 5) ? 1u << 8 : 0u) |
+                        ((jb == 2 || n2 == 6) ? 1u << 16 : 0u) | ((jb == 3 || n3 == 7) ? 1u << 24 : 0u);
+            }
+            const int64_t o = f * d.N + p;  // 16-byte aligned: N and p are multiples of 4
+            *reinterpret_cast<int4*>(w.uf + o) = make_int4(far[0], far[1], far[2], far[3]);
+            *reinterpret_cast<int4*>(w.mstbits + o) = make_int4((int)mb[0], (int)mb[1], (int)mb[2], (int)mb[3]);
+            const unsigned long long none = ~0ull;
+            reinterpret_cast<ulonglong2*>(w.bw + o)[0] = make_ulonglong2(none, none);
+            reinterpret_cast<ulonglong2*>(w.bw + o)[1] = make_ulonglong2(none, none);
+            *reinterpret_cast<uint4*>(w.bi + o) = make_uint4(kNoEdge, kNoEdge, kNoEdge, kNoEdge);
+            if (w.single) {
+                unsigned char* lt = w.lite + f * d.NL + p;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) lt[i] = (unsigned char)jbs[i];
+            }
+            if (p == 0 && jbs[0] != 0xFF) w.C(f)[C_ACT + 0] = 1;
+        }
+        __syncthreads();  // the next tile's staging reuses fb and sj
+    }
+}
+
 // KBoruvkaRelabelFind of rounds >= 1 on the record path, one wave per 32x8 tile (four pixels per lane):
 // a tile is relabelled only while it or one of its eight neighbours is active. Pass 0 reads a tile's
 // labels only for the tile itself or as the halo of a neighbour, the hook reads the labels of its
@@ -2909,6 +3008,19 @@ struct HipBackend {
             return;
         }
         pixel4(w, r, k_boruvka_relabel4<false>, "KBoruvkaRelabelFind");
+    }
+    // round 0's init + minimum edges per LDS tile (k_boruvka_first_t) on the record path's frames, whose
+    // round 0 relabels by k_boruvka_tile0 (it writes every pixel's label); false: KBoruvkaInit + KBoruvkaFirst
+    bool boruvka_first(const Ws& w) {
+        if (!rec_path(w) || w.d.W < 4 || !pairs_in_relabel(w)) return false;
+        const int64_t tiles = (int64_t)((w.d.W + kF1X - 1) / kF1X) * ((w.d.H + kF1Y - 1) / kF1Y);
+        const int64_t cap = std::max<int64_t>(1, grid_cap() / w.d.B);
+        timed("k_boruvka_first_t", [&] {
+            hipLaunchKernelGGL(k_boruvka_first_t, dim3((unsigned)std::min(tiles, cap), (unsigned)w.d.B), dim3(kF1T), 0,
+                               stream, w);
+        });
+        if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_boruvka_first_t launch");
+        return true;
     }
     // round 0's pairs and relabel per LDS tile (k_boruvka_tile0) on frames at least 3 wide; narrower ones
     // take KBoruvkaPairs + k_boruvka_relabel4 over uf

@@ -419,6 +419,47 @@ struct KBoruvkaInit {
     }
 };
 
+// The minimum incident edge of pixel p in round 0 (every pixel its own component), as its slot 0-7 (0xFF:
+// none) and emission index: slots 0-3 the edges p emits (left, up, up-left, down-left), 4-7 the edges its
+// right, lower, lower-right and upper-right neighbours q[4..7] emit towards it; bq[j] the neighbours'
+// blurred flows, ok[j] the slot's edge exists, allow_bits the edges the MST may use. The lexicographic
+// minimum (weight, index): edge_weight(b, s, e) = sqrt(sq) with s the emitting pixel (float differences,
+// double squares). sqrt is monotone and correctly rounded, so the minimum weight is sqrt of the minimum
+// sq, and only edges whose sq lies within 2^-48 (relative) of it can tie with it (a weight's rounding
+// interval is 2^-52 wide): one sqrt per pixel, not eight (as k_boruvka_min4 does in the later rounds).
+// (KBoruvkaFirst, and k_boruvka_first_t's tile of LDS-staged flows in the HIP build.)
+DOFS_HD inline int first_min_slot(F2 bp, const F2* bq, const bool* ok, unsigned allow_bits, int64_t p,
+                                  const int64_t* q, unsigned* bidx_out) {
+    unsigned long long sqb[8];
+    unsigned long long msq = ~0ull;  // bits of non-negative doubles order like the values
+DOFS_UNROLL
+    for (int j = 0; j < 8; ++j) {
+        const F2 bs = j < 4 ? bp : bq[j], be = j < 4 ? bq[j] : bp;
+        const double dx = bs.x - be.x, dy = bs.y - be.y;
+        sqb[j] = (ok[j] && ((allow_bits >> j) & 1)) ? dbits(sq_len(dx, dy)) : ~0ull;
+        msq = sqb[j] < msq ? sqb[j] : msq;
+    }
+    unsigned bidx = kNoEdge;
+    int jb = 0xFF;
+    if (msq != ~0ull) {
+        const double mv = bitsd(msq);
+        const unsigned long long best = dbits(sqrt(mv));
+        const unsigned long long thr = dbits(mv * 1.0000000000000036);  // (1 + 2^-48) mv
+DOFS_UNROLL
+        for (int j = 0; j < 8; ++j) {
+            if (sqb[j] > thr) continue;  // also the non-candidates (~0)
+            const bool tie = sqb[j] == msq || dbits(sqrt(bitsd(sqb[j]))) == best;
+            const unsigned idx = (unsigned)(4 * (j < 4 ? p : q[j]) + (j & 3));
+            if (tie && idx < bidx) {
+                bidx = idx;
+                jb = j;
+            }
+        }
+    }
+    *bidx_out = bidx;
+    return jb;
+}
+
 // Round 0: every pixel is its own component, so its minimum edge is the min over its <= 8 incident
 // edges (4 it emits, 4 its right/lower neighbours emit towards it) — no atomics. The minimum edges
 // form a forest whose only cycles are the mutual pairs (a unique minimum per component under the
@@ -452,40 +493,9 @@ DOFS_UNROLL
             allow_bits = al[p] & 0xfu;
             for (int j = 4; j < 8; ++j) allow_bits |= ((al[q[j]] >> (j - 4)) & 1u) << j;
         }
-        // the lexicographic minimum (weight, index): edge_weight(b, s, e) = sqrt(sq) with s the emitting
-        // pixel (float differences, double squares). sqrt is monotone and correctly rounded, so the
-        // minimum weight is sqrt of the minimum sq, and only edges whose sq lies within 2^-48 (relative)
-        // of it can tie with it (a weight's rounding interval is 2^-52 wide): one sqrt per pixel, not
-        // eight (as k_boruvka_min4 does in the later rounds)
-        unsigned long long sqb[8];
-        unsigned long long msq = ~0ull;  // bits of non-negative doubles order like the values
-DOFS_UNROLL
-        for (int j = 0; j < 8; ++j) {
-            const F2 bs = j < 4 ? bp : bq[j], be = j < 4 ? bq[j] : bp;
-            const double dx = bs.x - be.x, dy = bs.y - be.y;
-            sqb[j] = (ok[j] && ((allow_bits >> j) & 1)) ? dbits(sq_len(dx, dy)) : ~0ull;
-            msq = sqb[j] < msq ? sqb[j] : msq;
-        }
-        unsigned long long best = ~0ull;
-        unsigned bidx = kNoEdge;
-        int64_t far = p;
-        int jb = 0xFF;
-        if (msq != ~0ull) {
-            const double mv = bitsd(msq);
-            best = dbits(sqrt(mv));
-            const unsigned long long thr = dbits(mv * 1.0000000000000036);  // (1 + 2^-48) mv
-DOFS_UNROLL
-            for (int j = 0; j < 8; ++j) {
-                if (sqb[j] > thr) continue;  // also the non-candidates (~0)
-                const bool tie = sqb[j] == msq || dbits(sqrt(bitsd(sqb[j]))) == best;
-                const unsigned idx = (unsigned)(4 * (j < 4 ? p : q[j]) + (j & 3));
-                if (tie && idx < bidx) {
-                    bidx = idx;
-                    far = q[j];
-                    jb = j;
-                }
-            }
-        }
+        unsigned bidx;
+        const int jb = first_min_slot(bp, bq, ok, allow_bits, p, q, &bidx);
+        const int64_t far = jb == 0xFF ? p : q[jb];
         // the pixel's minimum incident edge as its slot 0..7 (0xFF: none), in the leaf part of lite (free:
         // path-top flags are written and read for merge nodes only) until KMstEmit reads it
         if (w.single) w.lite[f * d.NL + p] = (unsigned char)jb;

@@ -275,11 +275,12 @@ struct Pipeline {
         const Dims& d = w.d;
         const int B = d.B;
         const int64_t N = d.N;
-        be.launch(B, N, KBoruvkaInit{w});
+        const bool first_done = be.boruvka_first(w);  // (HIP: init + round 0's minimum edges per LDS tile)
+        if (!first_done) be.launch(B, N, KBoruvkaInit{w});
         const int R = std::min(ceil_log2(N) + 2, kRoundsMax - 1);
         for (int r = 0; r < R; ++r) {
             if (r == 0) {  // every pixel hooks along its minimum edge (a forest of pointers)
-                be.launch(B, N, KBoruvkaFirst{w});
+                if (!first_done) be.launch(B, N, KBoruvkaFirst{w});
                 if (!be.pairs_in_relabel(w)) be.launch(B, N, KBoruvkaPairs{w});  // (HIP: k_boruvka_tile0)
             } else {
                 be.boruvka_min(w, r, 0);  // KBoruvkaMinW (HIP: workgroup-aggregated per tile)

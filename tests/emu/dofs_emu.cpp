@@ -101,6 +101,7 @@ struct HostBackend {
     static constexpr bool kKrtLabelWords = true;  // the deep depths run as global kernels here
     static constexpr bool kDncAuto = false;       // the block-start labels by the sequential sweep (krt_seq)
     static int64_t jump_chain_bound(int64_t M) { return M; }
+    bool boruvka_first(const Ws&) { return false; }  // KBoruvkaInit + KBoruvkaFirst
     void dnc_deep(const Ws& w) {
         const int64_t M = w.d.M;
         int64_t top = 1;
