@@ -1,0 +1,22 @@
+# Round 0's minima words at the roots only (FR) against HEAD (HB): parity, the kernel's serial duration under
+# rocprofv3 for both, then an A/B with a second copy of HEAD (HB2) so each variant meets both run-to-run modes
+set -u
+export TMPDIR=/tmp
+v=${V:-FR}
+DOFS_LIB=$PWD/exp/$v/libdofs_hip.so timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+  tests/test_gpu_parity.py tests/test_gpu_bench_config.py tests/test_gpu_intraframe.py > gpurun_out/par_$v.log 2>&1 || { echo "parity $v failed"; tail -30 gpurun_out/par_$v.log; exit 1; }
+tail -1 gpurun_out/par_$v.log
+for x in HB $v; do
+  rm -rf gpurun_out/st_$x
+  DOFS_LIB=$PWD/exp/$x/libdofs_hip.so DOFS_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/st_$x -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --cpu-frames 0 --no-h2d --no-stages > /dev/null 2>&1 || exit 1
+  python - "$x" <<'PY'
+import csv, glob, sys
+f = glob.glob(f"gpurun_out/st_{sys.argv[1]}/**/*kernel_stats.csv", recursive=True)[0]
+for r in csv.DictReader(open(f)):
+    n = r["Name"]
+    if any(k in n for k in ("boruvka_first", "KBoruvkaFirst", "KBoruvkaInit", "boruvka_tile0", "boruvka_recs", "relabel")):
+        print(sys.argv[1], n[:60], r["Calls"], "avg us", round(float(r["AverageNs"]) / 1e3, 1))
+PY
+  rm -rf gpurun_out/st_$x
+done
+VARIANTS="HB $v HB2" N=${N:-3} bash tools/ab.sh
