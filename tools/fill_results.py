@@ -1,6 +1,5 @@
-"""Fill DESIGN.md §8's RESULT_* fields from an evidence directory (tools/round_evidence.sh → profiles/rNN):
-python tools/fill_results.py profiles/r06 [DESIGN.md]. Prints the filled paragraph; rewrites the file only if it
-still holds the placeholders (the template lines are kept in tools/results_template.md)."""
+"""Rewrite DESIGN.md §8 from tools/results_template.md, its RESULT_* fields filled from an evidence directory
+(tools/round_evidence.sh → profiles/rNN): python tools/fill_results.py profiles/r06 [DESIGN.md]. Prints the values."""
 import csv
 import json
 import os
@@ -31,6 +30,7 @@ vals = {
     "RESULT_SHA": json.load(open(os.path.join(src, "pmc_kernels.json"))).get("lib_sha256", "?")[:12],
     "RESULT_VALUE": f"{b['value']:,.1f}",
     "RESULT_STEP": f"{b['ms_per_step']}",
+    "RESULT_MEDIAN": f"{b['ms_per_step_median']}",
     "RESULT_STAGES": ", ".join(f"{k} {v}" for k, v in st.items()) + " ms",
     "RESULT_CPU": f"{cpu['O2']['value']} Mpixels/s at -O2, {cpu['O0']['value']} at -O0",
     "RESULT_KRT": (f"{r['ms_per_batch']} ms per batch ({r['avg_launch_us'] / 1e3:.1f} ms per launch), "
@@ -42,8 +42,10 @@ vals = {
     "RESULT_4K": f"{m['one_gpu_ms_per_frame']}",
     "RESULT_SPLIT": f"{m.get('projected_speedup_split', m.get('projected_speedup'))}",
 }
+sec8 = open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "results_template.md")).read()
+for k in sorted(vals, key=len, reverse=True):  # (RESULT_SPLIT before RESULT_S...: longest names first)
+    sec8 = sec8.replace(k, vals[k])
 s = open(path).read()
-for k, v in vals.items():
-    s = s.replace(k, v)
-open(path, "w").write(s)
+a, z = s.index("## 8. Results"), s.index("## 9. History")
+open(path, "w").write(s[:a] + sec8 + s[z:])
 print(json.dumps(vals, indent=1))
