@@ -16,6 +16,7 @@ for i in $(seq 1 $N); do
         case $tok in @*) bargs="$bargs ${tok#@}" ;; *) envs="$envs $tok" ;; esac
       done
     fi
+    if [ -n "${TINY:-}" ]; then python -c "import torch; torch.cuda.mem_get_info()" || exit 1; fi  # (tools/ab.sh)
     env $envs DOFS_LIB=$PWD/exp/$lib/libdofs_hip.so timeout -k 10 300 python bench.py --cpu-frames 0 --no-h2d ${ARGS:-} $bargs > gpurun_out/abe_$name$i.log 2>&1 || exit 1
     tail -1 gpurun_out/abe_$name$i.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); s=d['stages_ms_per_batch'] or {}; print('$name', d['value'], d['ms_per_step'], d.get('ms_per_step_median'), ' '.join(f'{k}={v}' for k, v in s.items()))"
   done
