@@ -23,9 +23,9 @@ def test_synthetic_parity(gpu, calib, H, W, seed, min_size, nbr):
 
 
 @pytest.mark.parametrize("kind", ["zeros", "const", "normal", "ints"])
-def test_adversarial_parity(gpu, calib, kind):
+@pytest.mark.parametrize("H,W", [(70, 90), (72, 96)])  # (72 x 96: W % 4 == 0, the record path and its tiled round 0)
+def test_adversarial_parity(gpu, calib, kind, H, W):
     rng = np.random.default_rng(1)
-    H, W = 70, 90
     flow = {"zeros": np.zeros((H, W, 2)), "const": np.full((H, W, 2), 1.5),
             "normal": rng.normal(size=(H, W, 2)),
             "ints": np.round(rng.normal(size=(H, W, 2)) * 4) + 2.0}[kind].astype(np.float32)
