@@ -2894,6 +2894,14 @@ struct HipBackend {
     }
     static constexpr int64_t deep_block() { return kDeepTop; }
     void dnc_parent(const Ws&) {}  // done by k_dnc_deep's epilogue
+    // the merges' ord entries for stage B's preorder (k_pre_sweep): the merge mark, one fill (KLeafPos places the
+    // leaves). Issued in stage A after the blur — ord is no stage-A array — off stage B's chain of one sweep
+    // per frame then KLeafPos (the jumping form, Ws::jscatter, writes the merges' entries itself)
+    void ord_mark(const Ws& w) {
+        if (pre_jump(w.d)) return;
+        note(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.ord), kOrdMerge, (size_t)w.d.B * w.d.NL, stream),
+             "hipMemsetD32Async");
+    }
     void blur(const Ws& w) {  // KBlurRow + KBlurCol, LDS-tiled
         const int64_t cap = std::max<int64_t>(1, grid_cap() / w.d.B);
         if (w.bn == 2 * kFbR + 1 && w.d.W >= 128 && w.d.H >= 64) {  // sigma = 3: one pass
@@ -2981,9 +2989,6 @@ struct HipBackend {
             });
             if (hipGetLastError() != hipSuccess) note(hipErrorLaunchFailure, "k_pre_sweep launch");
         }
-        if (!w.jscatter)  // the merges' ord entries: the merge mark, one fill (KLeafPos places the leaves)
-            note(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.ord), kOrdMerge, (size_t)w.d.B * w.d.NL, stream),
-                 "hipMemsetD32Async");
         launch(w.d.B, w.d.M, KLeafPos{w});
         return true;
     }

@@ -338,6 +338,7 @@ struct Pipeline {
         // K1 blur (segment.cpp:52): KBlurRow + KBlurCol (HIP: LDS-tiled) — the only reader of the input
         be.blur(w);
         if (ev_input) be.record(ev_input, be.cur_stream());
+        be.ord_mark(w);  // (HIP: stage B's merge marks in ord, off its chain)
         if (M <= 0) {  // single pixel: no edge, no merge
             be.launch(B, N, KLabelInit{w, true});
             be.launch(B, 1, KSingle{w});
@@ -380,6 +381,7 @@ struct Pipeline {
         be.memset(w.ctr, 0, sizeof(int) * kCounters);
         be.mark(0);
         be.launch(1, N, KCopyFlow{w});
+        be.ord_mark(w);
         if (M <= 0) {
             be.launch(1, N, KLabelInit{w, true});
             be.launch(1, 1, KSingle{w});

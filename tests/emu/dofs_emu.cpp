@@ -94,6 +94,7 @@ struct HostBackend {
     // emulator runs them with the global kernels (same parents and sizes)
     static constexpr int64_t deep_block() { return 4096; }
     void dnc_parent(const Ws& w) { launch(w.d.B, w.d.M, KDncParent{w}); }
+    void ord_mark(const Ws&) {}  // (KOrd writes every position)
     void blur(const Ws& w) {
         launch(w.d.B, w.d.N, KBlurRow{w});
         launch(w.d.B, w.d.N, KBlurCol{w});
