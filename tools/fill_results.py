@@ -41,6 +41,8 @@ vals = {
     "RESULT_PERIOD": period,
     "RESULT_4K": f"{m['one_gpu_ms_per_frame']}",
     "RESULT_SPLIT": f"{m.get('projected_speedup_split', m.get('projected_speedup'))}",
+    "RESULT_K20": (f"{jl('bench_steps20.json')['value']:,.1f}" if os.path.exists(os.path.join(src, "bench_steps20.json"))
+                   else "(not measured)"),
 }
 sec8 = open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "results_template.md")).read()
 for k in sorted(vals, key=len, reverse=True):  # (RESULT_SPLIT before RESULT_S...: longest names first)
