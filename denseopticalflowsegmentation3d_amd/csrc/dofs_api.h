@@ -177,6 +177,7 @@ inline std::string result_err_msg(int bits) {
     std::string m = "the results of this batch are invalid:";
     if (bits & kErrGiveUp) m += " its replay gave up a bounded wait;";
     if (bits & kErrRecord) m += " a replay record held a union-find root outside its frame (refused on the device);";
+    if (bits & kErrMst) m += " a frame's minimum spanning tree did not have N - 1 edges;";
     return m;
 }
 

@@ -82,7 +82,7 @@ enum Counter {
     C_KEEP = 54,     // merges whose replay record the lean replay stores (size >= min_size; KPathInit)
     C_OVF_ANY = 56,  // frame 0 only: 1 if any frame of the batch overflowed its snapshot records
     C_LONGM = 57,    // merges on long heavy paths (replayed by the wave-per-path kernel)
-    C_FLOWERR = 58,  // frame 0 only: the batch's results are invalid (bits kErrGiveUp, kErrRecord; dofs_kernels.h)
+    C_FLOWERR = 58,  // frame 0 only: the batch's results are invalid (bits kErrGiveUp, kErrRecord, kErrMst; dofs_kernels.h)
     C_ROOTL = 59,    // 1 + position in list_long of the frame's root heavy path (0: the root path is short)
     C_SORTFIX = 60,  // frame 0 only, 3 counters: pairs the MST sort fix-up moved, its fallback flag, barrier
     C_BMAX = 63      // the frame's largest |blurred flow component| (float bits, atomicMax by the HIP blur)

@@ -3213,6 +3213,24 @@ struct HipBackend {
         __device__ void operator()(int f, int64_t i) const { out[f * n + i] -= start[f]; }
     };
     void scan_excl(const int* in, int* out, int64_t n, int nf) { scan_excl_it(in, out, n, nf); }
+    // as scan_excl, for segments whose sums are all `total` (a frame's MST edge counts: N - 1 for a connected
+    // grid): subtracting it at every segment's last element makes the batch-wide sum segment-local, as the leaf
+    // scan below does — no rebase pass. total < 0: unknown (scan_excl)
+    struct FixedSum {
+        const int* in;
+        int64_t n;
+        int total;
+        __host__ __device__ int operator()(int64_t i) const { return in[i] - ((i + 1) % n == 0 ? total : 0); }
+    };
+    void scan_excl_total(const int* in, int* out, int64_t n, int nf, int total) {
+        if (total < 0 || nf <= 1 || (int64_t)n * nf >= (int64_t)0x7FFFFFFF) {
+            scan_excl_it(in, out, n, nf);
+            return;
+        }
+        hipcub::CountingInputIterator<int64_t> ci(0);
+        hipcub::TransformInputIterator<int, FixedSum, hipcub::CountingInputIterator<int64_t>> it(ci, FixedSum{in, n, total});
+        scan_excl_it(it, out, n * nf, 1);
+    }
     // leaf ranks in preorder: exclusive scan of (ord[q] < N) read through a transform iterator
     // (no flag array written by KOrd)
     struct IsLeaf {

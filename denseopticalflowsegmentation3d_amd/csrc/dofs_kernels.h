@@ -196,6 +196,7 @@ DOFS_HD inline int* state_at(const Ws& w, int64_t pos) { return &w.Rv[pos].pad0;
 // out-of-range atomic or gather.
 constexpr int kErrGiveUp = 1;
 constexpr int kErrRecord = 2;
+constexpr int kErrMst = 4;  // a frame's MST without N - 1 edges where its offsets assumed them (KMstEmit)
 DOFS_HD inline bool root_ok(const Ws& w, int root) {
     if ((unsigned)root < (unsigned)w.d.N) return true;
     dofs_aor(w.C(0) + C_FLOWERR, kErrRecord);
@@ -712,7 +713,12 @@ struct KMstEmit {
             }
             ++j;
         }
-        if (p == d.N - 1) w.C(f)[C_MST] = (int)j;
+        if (p == d.N - 1) {
+            w.C(f)[C_MST] = (int)j;
+            // the offsets' scan took N - 1 edges per unmasked frame (scan_excl_total): a frame that ends
+            // elsewhere (never, for a connected grid) has shifted every later frame's edges — fail loudly
+            if (!w.allow && j != d.M) dofs_aor(w.C(0) + C_FLOWERR, kErrMst);
+        }
     }
 };
 

@@ -351,7 +351,8 @@ struct Pipeline {
         boruvka();
         be.mark(2);
         be.launch(B, N, KMstCount{w});
-        be.scan_excl(w.cnt, w.off, N, B);
+        // each frame's MST spans its connected grid: N - 1 edges (not so under an edge mask: a forest)
+        be.scan_excl_total(w.cnt, w.off, N, B, w.allow ? -1 : (int)(N - 1));
         // Kruskal order: val_out holds each frame's MST edges by (weight, index); when the backend sorts
         // the whole batch at once the frame id rides above the index bits and key_out is not per frame
         const int vb = ceil_log2(4 * N);

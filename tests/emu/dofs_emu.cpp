@@ -226,6 +226,7 @@ struct HostBackend {
             }
         }
     }
+    void scan_excl_total(const int* in, int* out, int64_t n, int nf, int) { scan_excl(in, out, n, nf); }
     void scan_excl(const int* in, int* out, int64_t n, int nf) {
         for (int f = 0; f < nf; ++f) {
             int s = 0;
